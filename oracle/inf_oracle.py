@@ -1,0 +1,235 @@
+"""CPU oracle for the intrinsic-neural-fields hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is the *checker*: only `tests/`,
+`__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may import it.  The
+product path (intrinsic-neural-fields_amd/) never imports it and fails loudly when
+the HIP library is missing.
+
+It is a from-scratch numpy restatement of the reference algorithm, one function per
+step of the path, each citing the reference file:line it follows
+(reference = tum-vision/intrinsic-neural-fields, mounted read-only at /root/reference
+in the build container; it is never read at run time).
+
+Parity pinning: every function below is checked against golden vectors produced by
+running the reference itself (tests/golden/make_golden.py -> tests/golden/*.npz) in
+tests/test_oracle_golden.py.
+
+Arithmetic is done in the dtype of the inputs (fp32 by default, pass fp64 arrays for
+an accuracy reference).  Weight layout follows torch.nn.Linear: W[out, in].
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# ------------------------------------------------------------------------------------
+# Table producer and gather
+# ------------------------------------------------------------------------------------
+
+
+def load_first_k_eigenfunctions(table: np.ndarray, k, rescale_strategy: str = "standard") -> np.ndarray:
+    """mesh.py:53-108 (column select :60-65, rescale :99-106; embed strategies not used by
+    any config on the path).  `table` is the stored V x kmax eigenfunction matrix."""
+    if isinstance(k, (list, tuple, np.ndarray)):
+        E = table[:, np.asarray(k)]
+    else:
+        assert k <= table.shape[1]
+        E = table[:, :k]
+    if rescale_strategy == "standard":
+        E = E / (E.max(axis=0, keepdims=True) - E.min(axis=0, keepdims=True))
+    elif rescale_strategy == "one-norm":
+        E = E / np.linalg.norm(E, ord=2, axis=-1, keepdims=True)
+    elif rescale_strategy != "unscaled":
+        raise RuntimeError(f"Unknown rescaling strategy: {rescale_strategy}")
+    return np.ascontiguousarray(E, dtype=np.float32)
+
+
+def gather(E: np.ndarray, vids: np.ndarray, bary: np.ndarray) -> np.ndarray:
+    """mesh.py:313-324 get_k_eigenfunc_vec_vals: F[b,:] = sum_i bary[b,i] * E[vids[b,i],:]
+    (index -> B x 3 x k, then a (B,1,3)x(B,3,k) batched product)."""
+    rows = E[vids.reshape(-1)].reshape(vids.shape[0], 3, E.shape[1])
+    acc = bary[:, 0:1] * rows[:, 0]
+    acc = acc + bary[:, 1:2] * rows[:, 1]
+    acc = acc + bary[:, 2:3] * rows[:, 2]
+    return acc.astype(E.dtype, copy=False)
+
+
+# ------------------------------------------------------------------------------------
+# MLP (TextureField) forward / backward
+# ------------------------------------------------------------------------------------
+
+
+def layer_names(num_layers: int, skip: int):
+    """Parameter names in model.parameters() order (model.py:43-96, layers.py:50-57)."""
+    names = []
+    for i in range(num_layers):
+        if i == skip:
+            names += [f"layers.{i}.Lx.weight", f"layers.{i}.Lx.bias",
+                      f"layers.{i}.Ly.weight", f"layers.{i}.Ly.bias"]
+        else:
+            names += [f"layers.{i}.0.weight", f"layers.{i}.0.bias"]
+    return names
+
+
+def _sigmoid(z):
+    return 1.0 / (1.0 + np.exp(-z))
+
+
+def mlp_forward(w: dict, x: np.ndarray, num_layers: int, skip: int):
+    """model.py:98-112 TextureField.forward with layers.py:60-62 at the skip layer.
+    Returns (pred[B,3], cache) where cache holds each layer's input and output."""
+    cache = {"x": x, "in": [], "out": []}
+    h = x
+    for i in range(num_layers):
+        cache["in"].append(h)
+        if i == skip:
+            z = (h @ w[f"layers.{i}.Lx.weight"].T + w[f"layers.{i}.Lx.bias"]) + \
+                (x @ w[f"layers.{i}.Ly.weight"].T + w[f"layers.{i}.Ly.bias"])
+            h = np.maximum(z, 0)
+        elif i == num_layers - 1:
+            z = h @ w[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
+            h = _sigmoid(z)
+        else:
+            z = h @ w[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
+            h = np.maximum(z, 0)
+        cache["out"].append(h)
+    return h.astype(x.dtype, copy=False), cache
+
+
+CAUCHY_C2 = (20 / 255) * (20 / 255)
+
+
+def loss_value(pred: np.ndarray, tgt: np.ndarray, loss_type: str) -> float:
+    """config.py:113-122 (mean reduction over B*3)."""
+    d = pred - tgt
+    if loss_type == "L2":
+        return float(np.mean(d * d))
+    if loss_type == "L1":
+        return float(np.mean(np.abs(d)))
+    if loss_type == "cauchy":
+        return float(np.mean(CAUCHY_C2 * np.log(1 + d * d / CAUCHY_C2)))
+    raise RuntimeError(f"Unknown loss function: {loss_type}")
+
+
+def loss_grad(pred: np.ndarray, tgt: np.ndarray, loss_type: str, n_total: int | None = None) -> np.ndarray:
+    """d loss / d pred for the mean losses of config.py:113-122; n_total = number of
+    elements of the (global) mean, default pred.size.  sign(0) = 0 as torch's l1 grad."""
+    n = pred.size if n_total is None else n_total
+    d = pred - tgt
+    if loss_type == "L2":
+        g = 2.0 * d
+    elif loss_type == "L1":
+        g = np.sign(d)
+    elif loss_type == "cauchy":
+        g = 2.0 * d / (1 + d * d / CAUCHY_C2)
+    else:
+        raise RuntimeError(loss_type)
+    return (g / n).astype(pred.dtype, copy=False)
+
+
+def mlp_backward(w: dict, cache: dict, dpred: np.ndarray, num_layers: int, skip: int) -> dict:
+    """Reverse-mode of mlp_forward (what autograd computes at trainer.py:81)."""
+    g = {}
+    out = cache["out"]
+    # sigmoid head
+    dz = dpred * out[-1] * (1 - out[-1])
+    for i in range(num_layers - 1, -1, -1):
+        hin = cache["in"][i]
+        if i == skip:
+            g[f"layers.{i}.Lx.weight"] = dz.T @ hin
+            g[f"layers.{i}.Lx.bias"] = dz.sum(0)
+            g[f"layers.{i}.Ly.weight"] = dz.T @ cache["x"]
+            g[f"layers.{i}.Ly.bias"] = dz.sum(0)
+            wmat = w[f"layers.{i}.Lx.weight"]
+        else:
+            g[f"layers.{i}.0.weight"] = dz.T @ hin
+            g[f"layers.{i}.0.bias"] = dz.sum(0)
+            wmat = w[f"layers.{i}.0.weight"]
+        if i == 0:
+            break
+        dh = dz @ wmat
+        dz = dh * (out[i - 1] > 0)
+    return g
+
+
+# ------------------------------------------------------------------------------------
+# Adam (torch.optim.Adam defaults, non-capturable single-tensor formula; config.py:108)
+# ------------------------------------------------------------------------------------
+
+
+def adam_step(p, g, m, v, step: int, lr: float, beta1=0.9, beta2=0.999, eps=1e-8):
+    """One Adam update in place; `step` is the post-increment step count.
+    m <- lerp(m, g, 1-b1); v <- b2*v + (1-b2)*g*g;
+    p <- p - lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)."""
+    dt = p.dtype
+    m += dt.type(1 - beta1) * (g - m)
+    v *= dt.type(beta2)
+    v += dt.type(1 - beta2) * g * g
+    bc1 = 1 - beta1 ** step
+    bc2_sqrt = (1 - beta2 ** step) ** 0.5
+    step_size = lr / bc1
+    denom = np.sqrt(v) / dt.type(bc2_sqrt) + dt.type(eps)
+    p += dt.type(-step_size) * (m / denom)
+
+
+class OracleTrainer:
+    """Minimal restatement of Trainer._train_step (trainer.py:71-84) over the oracle
+    functions: forward -> loss -> backward -> Adam, with torch-Adam state semantics."""
+
+    def __init__(self, weights: dict, num_layers: int, skip: int, lr: float, loss_type: str):
+        self.w = {k: np.array(v, copy=True) for k, v in weights.items()}
+        self.L, self.s, self.lr, self.loss_type = num_layers, skip, lr, loss_type
+        self.names = layer_names(num_layers, skip)
+        self.m = {n: np.zeros_like(self.w[n]) for n in self.names}
+        self.v = {n: np.zeros_like(self.w[n]) for n in self.names}
+        self.t = 0
+
+    def step(self, x, rgb):
+        pred, cache = mlp_forward(self.w, x, self.L, self.s)
+        loss = loss_value(pred, rgb, self.loss_type)
+        grads = mlp_backward(self.w, cache, loss_grad(pred, rgb, self.loss_type), self.L, self.s)
+        self.t += 1
+        for n in self.names:
+            adam_step(self.w[n], grads[n], self.m[n], self.v[n], self.t, self.lr)
+        return loss, pred, grads
+
+
+# ------------------------------------------------------------------------------------
+# Loader batching, metrics, render scatter
+# ------------------------------------------------------------------------------------
+
+
+def loader_batches(N: int, B: int, drop_last: bool, perm: np.ndarray | None = None):
+    """ray_dataloader.py:88-113: number of batches and the row indices of each batch."""
+    nb = N // B if drop_last else (N + B - 1) // B
+    idxs = np.arange(N) if perm is None else np.asarray(perm)
+    return [idxs[i * B:min((i + 1) * B, N)] for i in range(nb)]
+
+
+def psnr(fake, real, obj_mask_1d=None):
+    """evaluation_metrics.py:5-22."""
+    if obj_mask_1d is not None:
+        fake = fake.reshape(-1, 3)[obj_mask_1d]
+        real = real.reshape(-1, 3)[obj_mask_1d]
+    mse = np.mean((fake - real) ** 2)
+    if mse == 0:
+        return float("inf")
+    return 20 * np.log10(1.0 / np.sqrt(mse))
+
+
+def epoch_psnr(epoch_mse):
+    """evaluation_metrics.py:25-26 (callers divide summed sq. error by rays, trainer.py:263)."""
+    return -10 * np.log10(epoch_mse)
+
+
+def render_scatter(pred, hit_ray_idxs, H, W, obj_mask_1d=None, background="white"):
+    """renderer.py:121-146: place predicted colours at hit rays over a constant background,
+    then unmask to H*W if an object mask was used."""
+    fill = 1.0 if background == "white" else 0.0
+    n = H * W if obj_mask_1d is None else int(np.sum(obj_mask_1d))
+    img = np.full((n, 3), fill, np.float32)
+    img[hit_ray_idxs] = pred
+    if obj_mask_1d is not None:
+        full = np.full((H * W, 3), fill, np.float32)
+        full[np.asarray(obj_mask_1d, bool)] = img
+        img = full
+    return img.reshape(H, W, 3)

@@ -1,0 +1,374 @@
+"""Generate golden input/output vectors by running the *reference* implementation.
+
+TEST INFRASTRUCTURE ONLY.  This script is run by hand in the build container, where
+the reference lives read-only at /root/reference.  It imports the reference's own
+Python modules (mesh.py, ray_dataloader.py, model.py, layers.py, config.py,
+trainer.py, renderer.py, evaluation_metrics.py, utils.py) with empty stand-ins for
+the third-party modules that are absent here and never executed on the hot path
+(igl, trimesh, imageio, torchinfo, tensorboardX, skimage), and records small
+fixtures (inputs + expected outputs) as .npz files next to this script.
+
+Nothing under /root/reference is copied; only numbers are stored.  Bytecode writing
+is disabled so the read-only tree is never touched.
+
+Fixtures:
+  g1_gather_k{37,64,1023,1024}.npz   mesh.get_k_eigenfunc_vec_vals        mesh.py:313-324
+  g1_load_efuncs.npz                 mesh.load_first_k_eigenfunctions     mesh.py:53-108
+  g2_forward_{A,R,B}.npz             model.make_model + forward           model.py:98-112,199-258
+  g3_step_{A,R,B}_{L2,L1,cauchy}.npz Trainer._train_step (1 step)         trainer.py:71-84
+  g4_adam20_{A_L2,R_L1}.npz          20 train steps, optimizer state      trainer.py:71-84, config.py:108
+  g5_loader.npz                      RayDataLoader batch sequences        ray_dataloader.py:103-145
+  g6_psnr.npz                        psnr / epoch_psnr                    evaluation_metrics.py:5-26
+  g7_render.npz                      Renderer.render MLP slice + scatter  renderer.py:64-146
+  g8_train_curve.npz                 tiny synthetic texture-recon run     trainer.py:164-187,232-283
+
+Run:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+import numpy as np
+import torch
+
+
+def _install_stubs():
+    """Empty stand-ins for third-party modules the reference imports at module level
+    but never calls on the paths exercised here."""
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        for k, v in attrs.items():
+            setattr(m, k, v)
+        sys.modules[name] = m
+        return m
+
+    mod("igl")
+    tm = mod("trimesh")
+    tm.ray = mod("trimesh.ray")
+    tm.PointCloud = type("PointCloud", (), {})
+    tm.Trimesh = type("Trimesh", (), {})
+    im = mod("imageio", imread=lambda *a, **k: None)
+    im.plugins = mod("imageio.plugins")
+    im.plugins.freeimage = mod("imageio.plugins.freeimage", download=lambda: None)
+    mod("torchinfo", summary=lambda *a, **k: None)
+
+    class _Writer:
+        def __init__(self, *a, **k):
+            self.scalars = []
+
+        def add_scalar(self, *a, **k):
+            self.scalars.append(a)
+
+        def add_image(self, *a, **k):
+            pass
+
+    mod("tensorboardX", SummaryWriter=_Writer)
+    sk = mod("skimage")
+    sk.metrics = mod("skimage.metrics", structural_similarity=lambda *a, **k: 0.0)
+    return _Writer
+
+
+Writer = _install_stubs()
+sys.path.insert(0, REF)
+
+import mesh as ref_mesh                      # noqa: E402
+import ray_dataloader as ref_loader          # noqa: E402
+import model as ref_model                    # noqa: E402
+import config as ref_config                  # noqa: E402
+import trainer as ref_trainer                # noqa: E402
+import renderer as ref_renderer              # noqa: E402
+import evaluation_metrics as ref_metrics     # noqa: E402
+
+K_LIST_1023 = list(range(0, 256)) + list(range(1793, 2304)) + list(range(3840, 4096))
+assert len(K_LIST_1023) == 1023
+
+CONFIGS = {
+    # name: (k, num_layers, hidden, skip)
+    "A": (64, 4, 128, 2),
+    "R": (K_LIST_1023, 6, 128, 3),
+    "B": (1024, 8, 256, 4),
+}
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print("wrote", path, sum(np.asarray(v).nbytes for v in arrays.values()), "bytes raw")
+
+
+def rescaled_table(rng, V, k):
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E = E / (E.max(0, keepdims=True) - E.min(0, keepdims=True))
+    return E.astype(np.float32)
+
+
+def synthetic_rays(rng, V, N, include_edges=True):
+    vids = rng.integers(0, V, size=(N, 3)).astype(np.int64)
+    u = rng.random((N, 3)).astype(np.float64)
+    bary = -np.log(np.maximum(u, 1e-12))
+    bary = (bary / bary.sum(1, keepdims=True)).astype(np.float32)
+    if include_edges and N >= 8:
+        vids[0] = [0, 0, 0]
+        vids[1] = [V - 1, V - 1, V - 1]
+        vids[2] = [0, V - 1, V // 2]
+        vids[3] = vids[4]
+        bary[0] = [1, 0, 0]
+        bary[1] = [0, 1, 0]
+        bary[2] = [0, 0, 1]
+        bary[5] = [0.5, 0.5, 0.0]
+    return vids, bary
+
+
+def state_dict_arrays(model, prefix="w:"):
+    return {prefix + k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def model_cfg(name):
+    k, L, H, s = CONFIGS[name]
+    return {"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s, "batchnorm": False}
+
+
+def in_dim(name):
+    k = CONFIGS[name][0]
+    return len(k) if isinstance(k, list) else k
+
+
+# ---------------------------------------------------------------------------------
+def g1_gather():
+    rng = np.random.default_rng(1)
+    B = 64
+    for k in (37, 64, 1023, 1024):
+        V = 257 if k < 1000 else 61
+        E = rescaled_table(rng, V, k)
+        vids, bary = synthetic_rays(rng, V, B)
+        out = ref_mesh.get_k_eigenfunc_vec_vals(torch.from_numpy(E), torch.from_numpy(vids),
+                                                torch.from_numpy(bary))
+        save(f"g1_gather_k{k}.npz", E=E, vids=vids, bary=bary, out=out.numpy())
+
+
+def g1_load_efuncs(tmpdir):
+    rng = np.random.default_rng(2)
+    V, kmax = 129, 96
+    table = rng.standard_normal((V, kmax)).astype(np.float32)
+    path = os.path.join(tmpdir, "efuncs.npy")
+    np.save(path, table)
+    k_list = list(range(0, 16)) + list(range(40, 56)) + list(range(80, 96))
+    res = {"table": table, "k_list": np.array(k_list)}
+    for strat in ("standard", "one-norm", "unscaled"):
+        res[f"int_{strat}"] = ref_mesh.load_first_k_eigenfunctions(path, 24, rescale_strategy=strat).numpy()
+        res[f"list_{strat}"] = ref_mesh.load_first_k_eigenfunctions(path, k_list, rescale_strategy=strat).numpy()
+    save("g1_load_efuncs.npz", **res)
+
+
+def g2_forward():
+    for name in CONFIGS:
+        torch.manual_seed(0)
+        model = ref_model.make_model(model_cfg(name))
+        rng = np.random.default_rng(3)
+        feats = (rng.standard_normal((64, in_dim(name))) * 0.3).astype(np.float32)
+        with torch.no_grad():
+            pred = model({"eigenfunctions": torch.from_numpy(feats)}).numpy()
+        save(f"g2_forward_{name}.npz", features=feats, pred=pred, **state_dict_arrays(model))
+
+
+def _bare_trainer(model, optim, loss_fn):
+    t = ref_trainer.Trainer.__new__(ref_trainer.Trainer)
+    t.model, t.optim, t.loss_fn = model, optim, loss_fn
+    t.device = "cpu"
+    t.writer = Writer()
+    return t
+
+
+def g3_step():
+    for name in CONFIGS:
+        for loss_type in ("L2", "L1", "cauchy"):
+            if name == "B" and loss_type != "L2":
+                continue
+            cfg = {"model": model_cfg(name), "training": {"lr": 1e-4, "loss_type": loss_type}}
+            torch.manual_seed(0)
+            model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+            loss_fn = ref_config.get_loss_fn(cfg)
+            rng = np.random.default_rng(4)
+            B = 64
+            feats = (rng.standard_normal((B, in_dim(name))) * 0.3).astype(np.float32)
+            rgb = rng.random((B, 3)).astype(np.float32)
+            batch = {"eigenfunctions": torch.from_numpy(feats), "expected_rgbs": torch.from_numpy(rgb)}
+            tr = _bare_trainer(model, optim, loss_fn)
+            # grads: re-run forward/backward on a copy to capture .grad before the step
+            torch.manual_seed(0)
+            m2, _ = ref_config.get_model_and_optim(cfg, None, "cpu")
+            p2 = m2(batch)
+            l2 = loss_fn(p2, batch["expected_rgbs"])
+            l2.backward()
+            grads = {"g:" + n: p.grad.numpy().copy() for n, p in m2.named_parameters()}
+            loss, pred = tr._train_step(batch)
+            # w0 is the seed-0 init stored in g2_forward_{name}.npz (same seed, same constructor).
+            w1 = state_dict_arrays(model, "w1:") if (name == "A" or (name, loss_type) == ("R", "L1")) else {}
+            save(f"g3_step_{name}_{loss_type}.npz", features=feats, rgb=rgb, loss=np.float32(loss),
+                 pred=pred.detach().numpy(), **grads, **w1)
+
+
+def g4_adam20():
+    for name, loss_type in (("A", "L2"), ("A", "cauchy"), ("R", "L1")):
+        cfg = {"model": model_cfg(name), "training": {"lr": 1e-3, "loss_type": loss_type}}
+        torch.manual_seed(0)
+        model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+        loss_fn = ref_config.get_loss_fn(cfg)
+        tr = _bare_trainer(model, optim, loss_fn)
+        rng = np.random.default_rng(5)
+        B, steps = 32, 20
+        feats = (rng.standard_normal((steps, B, in_dim(name))) * 0.3).astype(np.float32)
+        rgb = rng.random((steps, B, 3)).astype(np.float32)
+        losses = []
+        for i in range(steps):
+            loss, _ = tr._train_step({"eigenfunctions": torch.from_numpy(feats[i]),
+                                      "expected_rgbs": torch.from_numpy(rgb[i])})
+            losses.append(loss)
+        sd = optim.state_dict()
+        names = [n for n, _ in model.named_parameters()]
+        st = {}
+        for idx, n in enumerate(names):
+            s = sd["state"][idx]
+            st["m:" + n] = s["exp_avg"].numpy()
+            st["v:" + n] = s["exp_avg_sq"].numpy()
+            st["step:" + n] = np.float32(float(s["step"]))
+        save(f"g4_adam20_{name}_{loss_type}.npz", features=feats, rgb=rgb, losses=np.array(losses, np.float32),
+             lr=np.float32(1e-3), **state_dict_arrays(model, "w20:"), **st)
+
+
+def g5_loader():
+    rng = np.random.default_rng(6)
+    V, k, N = 23, 5, 10
+    E = rng.random((V, k)).astype(np.float32)
+    vids, bary = synthetic_rays(rng, V, N)
+    rgb = rng.random((N, 3)).astype(np.float32)
+    res = {"E": E, "vids": vids, "bary": bary, "rgb": rgb}
+    for B in (3, 4, 10, 16):
+        for drop_last in (True, False):
+            ld = ref_loader.RayDataLoader(torch.from_numpy(E), "efuncs", torch.from_numpy(vids),
+                                          torch.from_numpy(bary), torch.from_numpy(rgb), None, None,
+                                          B, False, drop_last, device="cpu")
+            tag = f"B{B}_{'drop' if drop_last else 'keep'}"
+            res[f"len_{tag}"] = np.int64(len(ld))
+            effs, rgbs = [], []
+            for batch in ld:
+                effs.append(batch["eigenfunctions"].numpy())
+                rgbs.append(batch["expected_rgbs"].numpy())
+            res[f"nb_{tag}"] = np.int64(len(effs))
+            if effs:
+                res[f"eff_{tag}"] = np.concatenate(effs)
+                res[f"rgb_{tag}"] = np.concatenate(rgbs)
+                res[f"sizes_{tag}"] = np.array([e.shape[0] for e in effs])
+    # The reference's own __main__ smoke case (ray_dataloader.py:148-205), on CPU.
+    smoke_vids = np.array([[0, 1, 2], [1, 2, 3], [7, 8, 9], [5, 6, 7], [3, 4, 5]], np.int64)
+    res["smoke_vids"] = smoke_vids
+    save("g5_loader.npz", **res)
+
+
+def g6_psnr():
+    rng = np.random.default_rng(7)
+    a = rng.random((16, 12, 3)).astype(np.float32)
+    b = np.clip(a + rng.standard_normal(a.shape).astype(np.float32) * 0.05, 0, 1)
+    mask = rng.random(16 * 12) > 0.3
+    save("g6_psnr.npz", a=a, b=b, mask=mask,
+         psnr_full=np.float64(ref_metrics.psnr(a, b)),
+         psnr_mask=np.float64(ref_metrics.psnr(a, b, mask)),
+         epoch_mse=np.float64(0.0123), epoch_psnr=np.float64(ref_metrics.epoch_psnr(0.0123)))
+
+
+def g7_render():
+    rng = np.random.default_rng(8)
+    name = "A"
+    torch.manual_seed(0)
+    model = ref_model.make_model(model_cfg(name))
+    V, k = 300, in_dim(name)
+    E = rescaled_table(rng, V, k)
+    H, W = 24, 20
+    res = {"E": E, "H": np.int64(H), "W": np.int64(W), **state_dict_arrays(model)}
+    for masked in (False, True):
+        obj_mask = rng.random(H * W) > 0.25 if masked else None
+        npix = int(obj_mask.sum()) if masked else H * W
+        hit = np.sort(rng.choice(npix, size=npix * 2 // 3, replace=False)).astype(np.int64)
+        rng.shuffle(hit)  # ray casting does not preserve order
+        vids, bary = synthetic_rays(rng, V, hit.shape[0], include_edges=False)
+        efv = ref_mesh.get_k_eigenfunc_vec_vals(torch.from_numpy(E), torch.from_numpy(vids),
+                                                torch.from_numpy(bary))
+
+        dirs = torch.zeros((hit.shape[0], 3))
+        faces = torch.zeros((hit.shape[0],), dtype=torch.int64)
+
+        def fake_ray_tracing(*a, **kw):
+            return efv, torch.from_numpy(hit), dirs, faces
+
+        ref_renderer.ray_tracing = fake_ray_tracing
+        ref_renderer.get_ray_mesh_intersector = lambda m: None
+        r = ref_renderer.Renderer(model, None, eigenfunctions=torch.from_numpy(E), H=H, W=W, device="cpu")
+        img = r.render(None, None, obj_mask_1d=None if obj_mask is None else torch.from_numpy(obj_mask))
+        tag = "mask" if masked else "full"
+        res[f"vids_{tag}"] = vids
+        res[f"bary_{tag}"] = bary
+        res[f"hit_{tag}"] = hit
+        res[f"img_{tag}"] = img
+        if masked:
+            res["obj_mask"] = obj_mask
+    save("g7_render.npz", **res)
+
+
+def g8_train_curve():
+    """Tiny synthetic texture reconstruction: a learnable per-vertex colour field."""
+    rng = np.random.default_rng(9)
+    name = "A"
+    V, k = 2000, in_dim(name)
+    E = rescaled_table(rng, V, k)
+    proj = rng.standard_normal((16, 3)).astype(np.float32) * 2.0
+    vert_rgb = 1.0 / (1.0 + np.exp(-(E[:, :16] * 4.0) @ proj))
+    def rays(n):
+        vids, bary = synthetic_rays(rng, V, n, include_edges=False)
+        rgb = np.einsum("ni,nic->nc", bary, vert_rgb[vids]).astype(np.float32)
+        return vids, bary, rgb
+    tr_v, tr_b, tr_rgb = rays(8192)
+    va_v, va_b, va_rgb = rays(2048)
+    cfg = {"model": model_cfg(name), "training": {"lr": 1e-3, "loss_type": "L1"}}
+    torch.manual_seed(0)
+    model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+    loss_fn = ref_config.get_loss_fn(cfg)
+    tr = _bare_trainer(model, optim, loss_fn)
+    Et = torch.from_numpy(E)
+    train_ld = ref_loader.RayDataLoader(Et, "efuncs", torch.from_numpy(tr_v), torch.from_numpy(tr_b),
+                                        torch.from_numpy(tr_rgb), None, None, 512, False, True, device="cpu")
+    val_ld = ref_loader.RayDataLoader(Et, "efuncs", torch.from_numpy(va_v), torch.from_numpy(va_b),
+                                      torch.from_numpy(va_rgb), None, None, 512, False, False, device="cpu")
+    tr.val_data_loader = val_ld
+    val_psnr, train_psnr = [], []
+    for epoch in range(12):
+        acc_l2, total = 0.0, 0
+        for batch in train_ld:  # shuffle=False: deterministic batch order
+            loss, pred = tr._train_step(batch)
+            acc_l2 += torch.nn.functional.mse_loss(pred, batch["expected_rgbs"], reduction="sum").item()
+            total += batch["expected_rgbs"].shape[0]
+        train_psnr.append(ref_metrics.epoch_psnr(acc_l2 / total))
+        _, vp = tr.evaluate(epoch)
+        val_psnr.append(vp)
+    save("g8_train_curve.npz", E=E, tr_vids=tr_v, tr_bary=tr_b, tr_rgb=tr_rgb, va_vids=va_v, va_bary=va_b,
+         va_rgb=va_rgb, val_psnr=np.array(val_psnr), train_psnr=np.array(train_psnr), lr=np.float32(1e-3),
+         batch=np.int64(512))
+
+
+if __name__ == "__main__":
+    import tempfile
+    torch.set_num_threads(8)
+    with tempfile.TemporaryDirectory() as td:
+        g1_gather()
+        g1_load_efuncs(td)
+        g2_forward()
+        g3_step()
+        g4_adam20()
+        g5_loader()
+        g6_psnr()
+        g7_render()
+        g8_train_curve()

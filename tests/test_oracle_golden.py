@@ -1,0 +1,129 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself."""
+import numpy as np
+import pytest
+
+from oracle import inf_oracle as O
+from conftest import golden
+
+CFG = {"A": (64, 4, 2), "R": (1023, 6, 3), "B": (1024, 8, 4)}
+
+
+def weights(d, prefix="w:"):
+    return {k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)}
+
+
+@pytest.mark.parametrize("k", [37, 64, 1023, 1024])
+def test_gather(k):
+    d = golden(f"g1_gather_k{k}.npz")
+    out = O.gather(d["E"], d["vids"], d["bary"])
+    np.testing.assert_allclose(out, d["out"], rtol=0, atol=1e-6)
+
+
+def test_load_efuncs():
+    d = golden("g1_load_efuncs.npz")
+    for strat in ("standard", "one-norm", "unscaled"):
+        np.testing.assert_allclose(O.load_first_k_eigenfunctions(d["table"], 24, strat), d[f"int_{strat}"],
+                                   rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(O.load_first_k_eigenfunctions(d["table"], list(d["k_list"]), strat),
+                                   d[f"list_{strat}"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["A", "R", "B"])
+def test_forward(name):
+    d = golden(f"g2_forward_{name}.npz")
+    _, L, s = CFG[name]
+    assert set(weights(d)) == set(O.layer_names(L, s))
+    pred, _ = O.mlp_forward(weights(d), d["features"], L, s)
+    np.testing.assert_allclose(pred, d["pred"], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L2"), ("R", "L1"),
+                                       ("R", "cauchy"), ("B", "L2")])
+def test_train_step(name, loss):
+    d = golden(f"g3_step_{name}_{loss}.npz")
+    w0 = weights(golden(f"g2_forward_{name}.npz"))
+    _, L, s = CFG[name]
+    tr = O.OracleTrainer(w0, L, s, 1e-4, loss)
+    lval, pred, grads = tr.step(d["features"], d["rgb"])
+    assert abs(lval - float(d["loss"])) < 1e-6
+    np.testing.assert_allclose(pred, d["pred"], atol=1e-6)
+    for n in O.layer_names(L, s):
+        ref = d["g:" + n]
+        scale = max(np.abs(ref).max(), 1e-12)
+        assert np.abs(grads[n] - ref).max() <= 1e-4 * scale + 1e-9, n
+    if "w1:" + O.layer_names(L, s)[0] in d.files:
+        for n in O.layer_names(L, s):
+            np.testing.assert_allclose(tr.w[n], d["w1:" + n], atol=1e-6, err_msg=n)  # ~1% of an lr=1e-4 step
+
+
+@pytest.mark.parametrize("tag,L,s", [("A_L2", 4, 2), ("A_cauchy", 4, 2), ("R_L1", 6, 3)])
+def test_adam20(tag, L, s):
+    d = golden(f"g4_adam20_{tag}.npz")
+    name, loss = tag.split("_")
+    tr = O.OracleTrainer(weights(golden(f"g2_forward_{name}.npz")), L, s, float(d["lr"]), loss)
+    for i in range(d["features"].shape[0]):
+        lval, _, _ = tr.step(d["features"][i], d["rgb"][i])
+        assert abs(lval - float(d["losses"][i])) < 2e-5
+    for n in O.layer_names(L, s):
+        np.testing.assert_allclose(tr.w[n], d["w20:" + n], atol=5e-5, err_msg=n)
+        np.testing.assert_allclose(tr.m[n], d["m:" + n], atol=1e-5, err_msg=n)
+        np.testing.assert_allclose(tr.v[n], d["v:" + n], rtol=1e-3, atol=1e-10, err_msg=n)
+        assert int(d["step:" + n]) == tr.t
+
+
+def test_loader():
+    d = golden("g5_loader.npz")
+    N = d["vids"].shape[0]
+    for B in (3, 4, 10, 16):
+        for drop in (True, False):
+            tag = f"B{B}_{'drop' if drop else 'keep'}"
+            batches = O.loader_batches(N, B, drop)
+            assert len(batches) == int(d[f"len_{tag}"]) == int(d[f"nb_{tag}"])
+            if batches:
+                idx = np.concatenate(batches)
+                np.testing.assert_array_equal([len(b) for b in batches], d[f"sizes_{tag}"])
+                eff = O.gather(d["E"], d["vids"][idx], d["bary"][idx])
+                np.testing.assert_allclose(eff, d[f"eff_{tag}"], atol=1e-6)
+                np.testing.assert_array_equal(d["rgb"][idx], d[f"rgb_{tag}"])
+
+
+def test_psnr():
+    d = golden("g6_psnr.npz")
+    assert abs(O.psnr(d["a"], d["b"]) - float(d["psnr_full"])) < 1e-9
+    assert abs(O.psnr(d["a"], d["b"], d["mask"]) - float(d["psnr_mask"])) < 1e-9
+    assert abs(O.epoch_psnr(float(d["epoch_mse"])) - float(d["epoch_psnr"])) < 1e-12
+
+
+def test_render_slice():
+    d = golden("g7_render.npz")
+    w = weights(d)
+    H, W = int(d["H"]), int(d["W"])
+    for tag in ("full", "mask"):
+        feats = O.gather(d["E"], d[f"vids_{tag}"], d[f"bary_{tag}"])
+        pred, _ = O.mlp_forward(w, feats, 4, 2)
+        img = O.render_scatter(pred, d[f"hit_{tag}"], H, W, d["obj_mask"] if tag == "mask" else None)
+        np.testing.assert_allclose(img, d[f"img_{tag}"], atol=1e-6)
+
+
+def test_train_curve():
+    """G8: statistical parity of a short synthetic texture-reconstruction run."""
+    d = golden("g8_train_curve.npz")
+    w0 = None
+    import torch
+    # the reference initialises with torch.manual_seed(0) + nn.Linear + xavier (model.py:194-258);
+    # the oracle takes those same weights from the A-config forward fixture (same seed, same shapes)
+    w0 = weights(golden("g2_forward_A.npz"))
+    tr = O.OracleTrainer(w0, 4, 2, float(d["lr"]), "L1")
+    B = int(d["batch"])
+    val = []
+    for epoch in range(len(d["val_psnr"])):
+        for idx in O.loader_batches(d["tr_vids"].shape[0], B, True):
+            x = O.gather(d["E"], d["tr_vids"][idx], d["tr_bary"][idx])
+            tr.step(x, d["tr_rgb"][idx])
+        sse = 0.0
+        for idx in O.loader_batches(d["va_vids"].shape[0], B, False):
+            x = O.gather(d["E"], d["va_vids"][idx], d["va_bary"][idx])
+            p, _ = O.mlp_forward(tr.w, x, 4, 2)
+            sse += float(np.sum((p - d["va_rgb"][idx]) ** 2))
+        val.append(O.epoch_psnr(sse / d["va_vids"].shape[0]))
+    np.testing.assert_allclose(val, d["val_psnr"], atol=0.05)
