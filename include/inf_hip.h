@@ -1,0 +1,175 @@
+/*
+ * inf_hip.h -- C ABI of the MI355X (gfx950) intrinsic-neural-fields hot path.
+ *
+ * The reference (tum-vision/intrinsic-neural-fields) has no native code: its hot path
+ * is stock PyTorch ops called from Python.  This library replaces those ops; the
+ * Python host layer (intrinsic-neural-fields_amd/) binds it with ctypes and keeps the
+ * reference's call surface.  Each entry point names the reference interface it
+ * replaces (paths relative to the reference root).
+ *
+ * Conventions
+ *   - every function returns INF_OK (0) or a negative INF_ERR_* code and never throws;
+ *     inf_last_error() returns a thread-local message for the last failure;
+ *   - all pointers are device pointers owned by the caller (PyTorch's allocator);
+ *     the library never allocates or synchronises on the hot path, so every call can
+ *     be captured into a HIP graph;
+ *   - `stream` is a hipStream_t passed as void*; all work is enqueued on it.
+ */
+#ifndef INF_HIP_H
+#define INF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* inf_stream_t; /* hipStream_t */
+
+enum {
+  INF_OK = 0,
+  INF_ERR_ARG = -1,         /* bad argument (shape, dtype, null pointer)       */
+  INF_ERR_HIP = -2,         /* a HIP runtime call failed                        */
+  INF_ERR_UNSUPPORTED = -3, /* configuration not supported by the kernels       */
+  INF_ERR_STATE = -4        /* plan not bound / wrong call order                */
+};
+
+enum { INF_DTYPE_F32 = 0, INF_DTYPE_BF16 = 1, INF_DTYPE_I32 = 2, INF_DTYPE_I64 = 3 };
+enum { INF_MODE_FP32 = 0, INF_MODE_BF16 = 1 };             /* GEMM arithmetic          */
+enum { INF_LOSS_L2 = 0, INF_LOSS_L1 = 1, INF_LOSS_CAUCHY = 2 }; /* config.py:113-122   */
+
+/* TextureField architecture (model.py:12-96, make_model model.py:199-258). */
+typedef struct inf_mlp_desc {
+  int32_t in_dim;     /* k (int) or len(k) (list)                          */
+  int32_t hidden;     /* mlp_hidden_dim                                    */
+  int32_t num_layers; /* num_layers (> 2)                                  */
+  int32_t skip;       /* skip_layer_idx, 0 < skip < num_layers-1           */
+  int32_t out_dim;    /* 3 (RGB_COLOR_DIM, model.py:9)                     */
+  int32_t mode;       /* INF_MODE_*                                        */
+  int32_t loss;       /* INF_LOSS_*                                        */
+} inf_mlp_desc;
+
+/* Sizes the caller needs to allocate for a plan (all in bytes unless noted). */
+typedef struct inf_plan_info {
+  int64_t num_params;     /* P: floats in the flat parameter arena            */
+  int32_t num_segments;   /* parameter tensors (model.parameters() order)     */
+  int32_t in_pad;         /* k padded to the GEMM tile                        */
+  int32_t max_batch_pad;  /* max_batch padded to the GEMM tile                */
+  int32_t dw_splits;      /* split-K factor of the weight-gradient GEMMs      */
+  int64_t shadow_bytes;   /* packed GEMM-dtype weights (W and W^T, padded)    */
+  int64_t workspace_bytes;/* activations, gradient slabs, loss accumulators   */
+  int64_t table_ld;       /* row stride (elements) expected of a device table */
+} inf_plan_info;
+
+/* A batch of rays, in one of two forms.
+ *  (a) rays:     table != NULL -> the library gathers F = sum_i bary_i * E[vid_i]
+ *                (mesh.py:313-324) for rays idx[offset + b] (ray_dataloader.py:115-129);
+ *  (b) features: features != NULL -> F given as fp32 [B][ld_features]
+ *                (model.py:104, batch["eigenfunctions"]).                       */
+typedef struct inf_batch {
+  const void* table;     /* [V][table_ld], dtype table_dtype, columns >= in_dim zero */
+  int32_t table_dtype;   /* INF_DTYPE_F32 / INF_DTYPE_BF16                            */
+  int64_t num_vertices;  /* V                                                         */
+  const void* vids;      /* [N][3] INF_DTYPE_I32 or INF_DTYPE_I64                     */
+  int32_t vid_dtype;
+  const float* bary;     /* [N][3]                                                    */
+  const float* rgb;      /* [N][3] targets (training only)                            */
+  const void* ray_idx;   /* [N] permutation (nullable: identity)                      */
+  int32_t idx_dtype;     /* INF_DTYPE_I32 / INF_DTYPE_I64                             */
+  int64_t idx_offset;    /* first entry of ray_idx (or of the rays) used              */
+  int32_t offset_from_ctrl; /* 1: add ctrl->batch_index * batch to idx_offset         */
+  const float* features; /* form (b)                                                  */
+  int64_t ld_features;
+  int32_t batch;         /* rays in this batch (<= max_batch)                         */
+  int64_t loss_count;    /* elements of the loss mean (3 x global batch); 0 = 3*batch */
+  int32_t loss;          /* INF_LOSS_* of a training call; -1 = the plan's desc.loss   */
+} inf_batch;
+
+/* Device-resident step state (lets a captured HIP graph replay a whole epoch). */
+typedef struct inf_ctrl {
+  int32_t step;        /* Adam step count t (post-increment semantics of torch Adam) */
+  int32_t batch_index; /* batch number inside the current epoch                     */
+  float lr;            /* learning rate (ReduceLROnPlateau may change it)            */
+  int32_t pad;
+  double loss_sum;     /* sum of element losses of the last step                     */
+  double sse_sum;      /* sum of squared errors of the last step                     */
+  double epoch_loss;   /* accumulated over the epoch (host resets)                   */
+  double epoch_sse;
+} inf_ctrl;
+
+/* ---- library ----------------------------------------------------------------- */
+const char* inf_last_error(void);
+int inf_abi_version(void);
+
+/* ---- gather: mesh.get_k_eigenfunc_vec_vals (mesh.py:313-324) and its chunked
+ *      form get_k_eigenfunc_vec_vals_batched (mesh.py:327-339), with the loader's
+ *      index-select fused in (ray_dataloader.py:122-129).
+ *      out[b][j] = bary[r][0]*E[v0][j] + bary[r][1]*E[v1][j] + bary[r][2]*E[v2][j],
+ *      r = idx ? idx[idx_offset+b] : idx_offset+b, j < k; columns k..ld_out-1 and rows
+ *      batch..rows_out-1 are written as zero.                                        */
+int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, int64_t table_ld,
+               const void* vids, int vid_dtype, const float* bary,
+               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
+               void* out, int out_dtype, int64_t ld_out, int rows_out,
+               void* out_t, int64_t ld_out_t, inf_stream_t stream);
+
+/* ---- plan: one TextureField (model.py:12-112) + its training step ---------------- */
+typedef struct inf_plan inf_plan;
+
+int inf_plan_create(const inf_mlp_desc* desc, int max_batch, inf_plan** plan);
+void inf_plan_destroy(inf_plan* plan);
+int inf_plan_get_info(const inf_plan* plan, inf_plan_info* info);
+/* Offsets/numels (floats) of each parameter tensor in the flat arena, in
+ * model.parameters() order: layers.{i}.0.weight/bias, layers.{s}.Lx.*, layers.{s}.Ly.* */
+int inf_plan_param_layout(const inf_plan* plan, int64_t* offsets, int64_t* numels, int n);
+
+/* Bind caller-owned buffers.  params/grads/exp_avg/exp_avg_sq: P floats each
+ * (grads/exp_avg/exp_avg_sq may be NULL for inference-only plans). */
+int inf_plan_bind(inf_plan* plan, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                  void* shadow, void* workspace, inf_ctrl* ctrl);
+/* Adam hyper-parameters (torch.optim.Adam defaults: 0.9, 0.999, 1e-8; config.py:108). */
+int inf_plan_set_adam(inf_plan* plan, float beta1, float beta2, float eps);
+
+/* Re-derive the packed GEMM weights from the fp32 parameters (after init,
+ * load_state_dict, or any host-side parameter edit). */
+int inf_sync_shadow(inf_plan* plan, inf_stream_t stream);
+
+/* Forward (model.py:98-112): pred[B][3] fp32.  save != 0 keeps the activations for
+ * inf_backward (autograd path, trainer.py:75/81). */
+int inf_forward(inf_plan* plan, const inf_batch* batch, float* pred, int save, inf_stream_t stream);
+
+/* Backward of the last saved forward given dL/dpred [B][3] (autograd, trainer.py:81).
+ * Writes the reduced parameter gradient (P floats, arena layout) into `grads`; the
+ * caller hands it to autograd, which accumulates into param.grad exactly as torch
+ * does (zero_grad(set_to_none=True), trainer.py:80). */
+int inf_backward(inf_plan* plan, const float* dpred, float* grads, inf_stream_t stream);
+
+/* Fused training step (trainer.py:71-84 + loss config.py:113-122):
+ * gather -> forward -> loss -> backward -> gradient reduction, and, if
+ * apply_adam != 0, the Adam update (torch.optim.Adam, config.py:108).  With
+ * apply_adam == 0 the reduced gradient is left in `grads` for a cross-GPU
+ * all-reduce followed by inf_adam().  pred may be NULL.  Loss sums go to ctrl. */
+int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int apply_adam,
+                   inf_stream_t stream);
+
+/* Adam update from the bound `grads` arena (optim.step(), trainer.py:82).  step > 0
+ * and lr > 0 are used as given (torch state["step"] after its increment, param_group
+ * lr); otherwise both are read from ctrl (graph-replayed steps, where head_bwd has
+ * already advanced ctrl->step). */
+int inf_adam(inf_plan* plan, int step, float lr, inf_stream_t stream);
+
+/* Render slice (renderer.py:112-146): forward of `batch` and placement of each
+ * predicted colour at image row pixel_map[hit[b]] (hit = hit_ray_idxs; pixel_map maps
+ * masked-pixel index -> full-image pixel, NULL for identity).  img is [H*W][3] fp32
+ * and must already hold the background. */
+int inf_render(inf_plan* plan, const inf_batch* batch, const int64_t* hit, const int64_t* pixel_map,
+               float* img, inf_stream_t stream);
+
+/* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
+int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INF_HIP_H */

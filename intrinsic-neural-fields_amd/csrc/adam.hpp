@@ -1,0 +1,51 @@
+// Gradient reduction / Adam / packed-weight refresh (see adam.hip).
+#pragma once
+
+#include "common.hpp"
+
+namespace inf {
+
+enum GradSource { GRAD_NONE = 0, GRAD_SLABS = 1, GRAD_FLAT = 2 };
+
+struct AdamSeg {
+  int64_t off;          // offset (floats) of the parameter tensor in the flat arena
+  int32_t R, C;         // matrix: R = out rows, C = in cols; vector: R = 1, C = numel
+  int32_t matrix;       // 1: GEMM weight (64x64 tiles, packed shadows)
+  int32_t nslab;        // gradient partials to sum
+  const float* slab;    // element (r, c) of partial s: slab[s * slab_stride + r * slab_ld + c]
+  int64_t slab_stride;
+  int64_t slab_ld;
+  void* W;              // packed [R][ldw] GEMM-dtype weight
+  int64_t ldw;
+  void* WT;             // packed [C_pad][ldwt] transposed weight
+  int64_t ldwt;
+};
+
+struct AdamItem {
+  int32_t seg;
+  int32_t r0, c0;
+  int32_t pad;
+};
+
+struct AdamArgs {
+  const AdamSeg* segs;
+  const AdamItem* items;
+  int32_t num_items;
+  float* params;
+  float* grads;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int32_t grad_src;     // GradSource
+  int32_t write_grads;
+  int32_t do_adam;
+  int32_t write_shadow;
+  int32_t step_host;    // > 0: use this t, else ctrl->step
+  float lr_host;        // > 0: use this lr, else ctrl->lr
+  const inf_ctrl* ctrl;
+  double beta1_d, beta2_d;
+  float one_minus_b1, beta2, one_minus_b2, eps;
+};
+
+int launch_update(const AdamArgs& a, int mode, hipStream_t stream);
+
+}  // namespace inf

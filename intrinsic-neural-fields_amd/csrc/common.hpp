@@ -1,0 +1,80 @@
+// Shared helpers for the gfx950 kernels of the intrinsic-neural-fields hot path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "inf_hip.h"
+
+namespace inf {
+
+using bf16 = __bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- error channel ---------------------------------------------------------------
+void set_error(const std::string& msg);
+
+#define INF_CHECK_ARG(cond, msg)                                  \
+  do {                                                            \
+    if (!(cond)) {                                                \
+      ::inf::set_error(std::string("invalid argument: ") + (msg)); \
+      return INF_ERR_ARG;                                         \
+    }                                                             \
+  } while (0)
+
+#define INF_HIP_TRY(expr)                                                               \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      ::inf::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));              \
+      return INF_ERR_HIP;                                                               \
+    }                                                                                   \
+  } while (0)
+
+#define INF_LAUNCH_CHECK()                                                              \
+  do {                                                                                  \
+    hipError_t e_ = hipGetLastError();                                                  \
+    if (e_ != hipSuccess) {                                                             \
+      ::inf::set_error(std::string("kernel launch: ") + hipGetErrorString(e_));         \
+      return INF_ERR_HIP;                                                               \
+    }                                                                                   \
+  } while (0)
+
+// ---- element conversion ----------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float to_f32(T x) { return (float)x; }
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float x) { return (T)x; }
+
+__host__ __device__ constexpr inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ constexpr inline int64_t ceil_div(int64_t x, int64_t m) { return (x + m - 1) / m; }
+
+// Index of ray b of a batch: ray_idx[offset + b] (int32/int64) or offset + b.
+__device__ __forceinline__ int64_t ray_row(const void* ray_idx, int idx_dtype, int64_t offset, int b) {
+  if (ray_idx == nullptr) return offset + b;
+  if (idx_dtype == INF_DTYPE_I64) return reinterpret_cast<const int64_t*>(ray_idx)[offset + b];
+  return reinterpret_cast<const int32_t*>(ray_idx)[offset + b];
+}
+
+__device__ __forceinline__ int64_t vid_at(const void* vids, int vid_dtype, int64_t i) {
+  if (vid_dtype == INF_DTYPE_I64) return reinterpret_cast<const int64_t*>(vids)[i];
+  return reinterpret_cast<const int32_t*>(vids)[i];
+}
+
+// ---- kernel launch wrappers (defined in the .hip files) --------------------------
+int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
+                  int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
+                  const int32_t* ctrl_batch_index, int64_t ctrl_stride, int batch, void* out, int out_dtype,
+                  int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream);
+
+// Pack fp32 features [B][ld_in] into the GEMM dtype [rows_out][ld_out] (+ transposed copy).
+int launch_pack_features(const float* in, int64_t ld_in, int k, int batch, void* out, int out_dtype,
+                         int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream);
+
+}  // namespace inf

@@ -1,0 +1,271 @@
+// Barycentric eigenfunction gather (reference: mesh.py:313-324 get_k_eigenfunc_vec_vals,
+// with the loader's per-batch index-select ray_dataloader.py:122-129 fused in).
+//
+//   F[b][j] = bary[r][0] * E[v0][j] + bary[r][1] * E[v1][j] + bary[r][2] * E[v2][j]
+//   r = ray_idx[offset + b], (v0, v1, v2) = vids[r]
+//
+// One 256-thread workgroup produces a 64-ray x 64-column tile.  Four consecutive lanes
+// cover one 64-column segment of a vertex row (256 B fp32 / 128 B bf16), so every
+// table read is a full, aligned run of cache lines; the three vertex rows of a ray are
+// read by the same lanes so their FMAs stay in registers.  The row-major tile is stored
+// straight from registers; the transposed copy (used by the weight-gradient GEMMs) goes
+// through a padded LDS tile so both stores are coalesced.
+#include "common.hpp"
+
+namespace inf {
+
+namespace {
+
+constexpr int GT_ROWS = 64;  // rays per tile
+constexpr int GT_COLS = 64;  // columns per tile
+constexpr int GT_THREADS = 256;
+
+template <typename TabT>
+__device__ __forceinline__ void load16(const TabT* __restrict__ p, float (&v)[16]);
+
+template <>
+__device__ __forceinline__ void load16<float>(const float* __restrict__ p, float (&v)[16]) {
+  const f32x4* q = reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x4 t = q[i];
+    v[4 * i + 0] = t[0];
+    v[4 * i + 1] = t[1];
+    v[4 * i + 2] = t[2];
+    v[4 * i + 3] = t[3];
+  }
+}
+
+template <>
+__device__ __forceinline__ void load16<bf16>(const bf16* __restrict__ p, float (&v)[16]) {
+  const bf16x8* q = reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    bf16x8 t = q[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[8 * i + j] = (float)t[j];
+  }
+}
+
+template <typename OutT>
+__device__ __forceinline__ void store16(OutT* __restrict__ p, const float (&v)[16]);
+
+template <>
+__device__ __forceinline__ void store16<float>(float* __restrict__ p, const float (&v)[16]) {
+  f32x4* q = reinterpret_cast<f32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+}
+
+template <>
+__device__ __forceinline__ void store16<bf16>(bf16* __restrict__ p, const float (&v)[16]) {
+  bf16x8* q = reinterpret_cast<bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    bf16x8 t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = (bf16)v[8 * i + j];
+    q[i] = t;
+  }
+}
+
+// VEC: table rows / output rows are 16-byte aligned and ld multiple of 16 elements, so a
+// lane moves its 16 columns with vector loads/stores.  Otherwise a masked scalar path.
+template <typename TabT, typename OutT, bool VEC>
+__global__ __launch_bounds__(GT_THREADS) void gather_kernel(
+    const TabT* __restrict__ table, int64_t V, int k, int64_t table_ld, const void* __restrict__ vids,
+    int vid_dtype, const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype,
+    int64_t idx_offset, const int32_t* __restrict__ ctrl_batch_index, int batch, OutT* __restrict__ out,
+    int64_t ld_out, int rows_out, OutT* __restrict__ out_t, int64_t ld_out_t) {
+  __shared__ float tile[GT_COLS][GT_ROWS + 1];
+
+  const int t = threadIdx.x;
+  const int r = t >> 2;        // ray within tile
+  const int cq = (t & 3) * 16; // first column within tile
+  const int b = blockIdx.x * GT_ROWS + r;
+  const int64_t c0 = (int64_t)blockIdx.y * GT_COLS + cq;
+
+  int64_t offset = idx_offset;
+  if (ctrl_batch_index != nullptr) offset += (int64_t)(*ctrl_batch_index) * batch;
+
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  if (b < batch) {
+    const int64_t row = ray_row(ray_idx, idx_dtype, offset, b);
+    const float w0 = bary[3 * row + 0];
+    const float w1 = bary[3 * row + 1];
+    const float w2 = bary[3 * row + 2];
+    const int64_t v0 = vid_at(vids, vid_dtype, 3 * row + 0);
+    const int64_t v1 = vid_at(vids, vid_dtype, 3 * row + 1);
+    const int64_t v2 = vid_at(vids, vid_dtype, 3 * row + 2);
+    if (VEC) {
+      if (c0 < k) {  // k is a multiple of 16 on this path
+        float e0[16], e1[16], e2[16];
+        load16<TabT>(table + v0 * table_ld + c0, e0);
+        load16<TabT>(table + v1 * table_ld + c0, e1);
+        load16<TabT>(table + v2 * table_ld + c0, e2);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = fmaf(w2, e2[i], fmaf(w1, e1[i], w0 * e0[i]));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t c = c0 + i;
+        if (c < k) {
+          const float e0 = (float)table[v0 * table_ld + c];
+          const float e1 = (float)table[v1 * table_ld + c];
+          const float e2 = (float)table[v2 * table_ld + c];
+          acc[i] = fmaf(w2, e2, fmaf(w1, e1, w0 * e0));
+        }
+      }
+    }
+  }
+
+  // row-major tile
+  if (out != nullptr && b < rows_out) {
+    OutT* dst = out + (int64_t)b * ld_out + c0;
+    if (VEC) {
+      if (c0 < ld_out) store16<OutT>(dst, acc);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (c0 + i < ld_out) dst[i] = (OutT)acc[i];
+    }
+  }
+
+  if (out_t != nullptr) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tile[cq + i][r] = acc[i];
+    __syncthreads();
+    const int c = t >> 2;
+    const int rq = (t & 3) * 16;
+    const int64_t gc = (int64_t)blockIdx.y * GT_COLS + c;
+    const int gb = blockIdx.x * GT_ROWS + rq;
+    if (gc < ld_out) {
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = tile[c][rq + i];
+      OutT* dst = out_t + gc * ld_out_t + gb;
+      if (VEC && gb + 16 <= rows_out) {
+        store16<OutT>(dst, v);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (gb + i < rows_out) dst[i] = (OutT)v[i];
+      }
+    }
+  }
+}
+
+template <typename TabT, typename OutT>
+int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const void* vids, int vid_dtype,
+                 const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_bi,
+                 int batch, void* out, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t,
+                 hipStream_t stream) {
+  dim3 grid((unsigned)ceil_div(rows_out, GT_ROWS), (unsigned)ceil_div(ld_out, GT_COLS));
+  const bool vec = (k % 16 == 0) && (table_ld % 16 == 0) && (ld_out % 16 == 0) &&
+                   (out_t == nullptr || ld_out_t % 16 == 0) && ((uintptr_t)table % 16 == 0) &&
+                   ((uintptr_t)out % 16 == 0) && ((uintptr_t)out_t % 16 == 0);
+  if (vec) {
+    gather_kernel<TabT, OutT, true><<<grid, GT_THREADS, 0, stream>>>(
+        (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, batch,
+        (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
+  } else {
+    gather_kernel<TabT, OutT, false><<<grid, GT_THREADS, 0, stream>>>(
+        (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, batch,
+        (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
+  }
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
+
+}  // namespace
+
+int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
+                  int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
+                  const int32_t* ctrl_batch_index, int64_t /*ctrl_stride*/, int batch, void* out, int out_dtype,
+                  int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
+  INF_CHECK_ARG(table != nullptr && vids != nullptr && bary != nullptr, "gather: null input");
+  INF_CHECK_ARG(k > 0 && table_ld >= k && V > 0, "gather: bad table shape");
+  INF_CHECK_ARG(batch >= 0 && rows_out >= batch && ld_out >= k, "gather: bad output shape");
+  INF_CHECK_ARG(out != nullptr || out_t != nullptr, "gather: no output");
+  INF_CHECK_ARG(out_t == nullptr || ld_out_t >= rows_out, "gather: bad transposed output stride");
+  INF_CHECK_ARG(vid_dtype == INF_DTYPE_I32 || vid_dtype == INF_DTYPE_I64, "gather: vids must be int32/int64");
+  INF_CHECK_ARG(ray_idx == nullptr || idx_dtype == INF_DTYPE_I32 || idx_dtype == INF_DTYPE_I64,
+                "gather: ray_idx must be int32/int64");
+  if (rows_out == 0) return INF_OK;
+  const bool tf = table_dtype == INF_DTYPE_F32, of = out_dtype == INF_DTYPE_F32;
+  INF_CHECK_ARG(tf || table_dtype == INF_DTYPE_BF16, "gather: table dtype must be f32/bf16");
+  INF_CHECK_ARG(of || out_dtype == INF_DTYPE_BF16, "gather: out dtype must be f32/bf16");
+  if (tf && of)
+    return launch_typed<float, float>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
+                                      ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+  if (tf && !of)
+    return launch_typed<float, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
+                                     ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+  if (!tf && of)
+    return launch_typed<bf16, float>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
+                                     ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+  return launch_typed<bf16, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
+                                  ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+}
+
+// Features given by the caller (model(batch) with batch["eigenfunctions"], model.py:104):
+// the same tile machinery with an identity "gather" (one vertex, weight 1).
+namespace {
+template <typename OutT>
+__global__ __launch_bounds__(GT_THREADS) void pack_kernel(const float* __restrict__ in, int64_t ld_in, int k, int batch,
+                                                          OutT* __restrict__ out, int64_t ld_out, int rows_out,
+                                                          OutT* __restrict__ out_t, int64_t ld_out_t) {
+  __shared__ float tile[GT_COLS][GT_ROWS + 1];
+  const int t = threadIdx.x;
+  const int r = t >> 2;
+  const int cq = (t & 3) * 16;
+  const int b = blockIdx.x * GT_ROWS + r;
+  const int64_t c0 = (int64_t)blockIdx.y * GT_COLS + cq;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t c = c0 + i;
+    v[i] = (b < batch && c < k) ? in[(int64_t)b * ld_in + c] : 0.f;
+  }
+  if (out != nullptr && b < rows_out) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (c0 + i < ld_out) out[(int64_t)b * ld_out + c0 + i] = (OutT)v[i];
+  }
+  if (out_t != nullptr) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tile[cq + i][r] = v[i];
+    __syncthreads();
+    const int c = t >> 2;
+    const int rq = (t & 3) * 16;
+    const int64_t gc = (int64_t)blockIdx.y * GT_COLS + c;
+    const int gb = blockIdx.x * GT_ROWS + rq;
+    if (gc < ld_out) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (gb + i < rows_out) out_t[gc * ld_out_t + gb + i] = (OutT)tile[c][rq + i];
+    }
+  }
+}
+}  // namespace
+
+int launch_pack_features(const float* in, int64_t ld_in, int k, int batch, void* out, int out_dtype, int64_t ld_out,
+                         int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
+  INF_CHECK_ARG(in != nullptr && ld_in >= k && ld_out >= k && rows_out >= batch, "pack_features: bad shape");
+  if (rows_out == 0) return INF_OK;
+  dim3 grid((unsigned)ceil_div(rows_out, GT_ROWS), (unsigned)ceil_div(ld_out, GT_COLS));
+  if (out_dtype == INF_DTYPE_F32)
+    pack_kernel<float><<<grid, GT_THREADS, 0, stream>>>(in, ld_in, k, batch, (float*)out, ld_out, rows_out,
+                                                         (float*)out_t, ld_out_t);
+  else
+    pack_kernel<bf16><<<grid, GT_THREADS, 0, stream>>>(in, ld_in, k, batch, (bf16*)out, ld_out, rows_out,
+                                                        (bf16*)out_t, ld_out_t);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
+
+}  // namespace inf

@@ -1,0 +1,333 @@
+// Grouped NT GEMM on gfx950 matrix cores.  See gemm.hpp for the operand contract.
+//
+// Block = 256 threads = 4 waves in a 2x2 arrangement; each wave owns a (BM/2)x(BN/2)
+// sub-tile built from 16x16 MFMA tiles.
+//   bf16 mode: v_mfma_f32_16x16x32_bf16, k-tile BK = 64 (128-byte LDS rows)
+//   fp32 mode: v_mfma_f32_16x16x4_f32 (exact f32 FMA chain), k-tile BK = 32 (128-byte
+//              rows); a lane's 16-byte fragment read holds 4 consecutive k that feed 4
+//              consecutive MFMAs, so every operand read is one ds_read_b128 in both modes.
+// Operand tiles are staged global -> registers -> LDS with a double buffer: the loads
+// for k-tile t+1 are issued before the MFMAs of tile t and written to the other LDS
+// buffer afterwards (one barrier per k-tile).  LDS rows are 8 x 16-byte chunks stored
+// at chunk ^ (row & 7), which spreads the 16 rows a ds_read_b128 lane group touches
+// over all bank slots of a 256-byte bank row pair (2-way at worst).
+// Epilogue: accumulators -> padded fp32 LDS tile -> bias / ReLU / ReLU-mask ->
+// coalesced row-major store, transposed store and per-tile column sums.
+#include "gemm.hpp"
+
+namespace inf {
+namespace {
+
+template <typename T>
+struct ModeTraits;
+
+template <>
+struct ModeTraits<bf16> {
+  static constexpr int BK = 64;  // elements per k-tile (128 B rows)
+  static constexpr int CH = 8;   // elements per 16-byte chunk
+};
+template <>
+struct ModeTraits<float> {
+  static constexpr int BK = 32;
+  static constexpr int CH = 4;
+};
+
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+template <typename T, int BM, int BN>
+struct Tile {
+  static constexpr int BK = ModeTraits<T>::BK;
+  static constexpr int CH = ModeTraits<T>::CH;
+  static constexpr int A_CHUNKS = BM * 8 / 256;  // 16-byte chunks per thread per k-tile
+  static constexpr int B_CHUNKS = BN * 8 / 256;
+  static constexpr int OPER_BYTES = 2 * (BM + BN) * 128;
+  static constexpr int CLD = BN + 4;  // fp32 C staging row stride
+  static constexpr int C_BYTES = BM * CLD * 4;
+  static constexpr int LDS_BYTES = OPER_BYTES > C_BYTES ? OPER_BYTES : C_BYTES;
+  static constexpr int WM = BM / 2, WN = BN / 2;
+  static constexpr int TM = WM / 16, TN = WN / 16;
+};
+
+template <typename T, int BM, int BN>
+__device__ __forceinline__ void compute_tile(const char* __restrict__ As, const char* __restrict__ Bs, int wm0,
+                                             int wn0, int lane, f32x4 (&acc)[Tile<T, BM, BN>::TM][Tile<T, BM, BN>::TN]) {
+  using TL = Tile<T, BM, BN>;
+  constexpr int TM = TL::TM, TN = TL::TN;
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm0 + i * 16 + r16;
+        a[i] = *reinterpret_cast<const bf16x8*>(As + swz(row, kk * 4 + g));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn0 + j * 16 + r16;
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(row, kk * 4 + g));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f32x4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm0 + i * 16 + r16;
+        a[i] = *reinterpret_cast<const f32x4*>(As + swz(row, kk * 4 + g));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn0 + j * 16 + r16;
+        b[j] = *reinterpret_cast<const f32x4*>(Bs + swz(row, kk * 4 + g));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ float ld_elem(const void* p, int64_t i) {
+  return (float)reinterpret_cast<const T*>(p)[i];
+}
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const GemmBatch batch) {
+  using TL = Tile<T, BM, BN>;
+  constexpr int BK = TL::BK, CH = TL::CH;
+  __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
+
+  // ---- locate problem / tile -----------------------------------------------------
+  int pi = 0;
+#pragma unroll 1
+  for (int i = 1; i < batch.nprob; ++i)
+    if ((int)blockIdx.x >= batch.p[i].block_begin) pi = i;
+  const GemmProblem& P = batch.p[pi];
+  int local = (int)blockIdx.x - P.block_begin;
+  const int tiles = P.tiles_m * P.tiles_n;
+  const int split = local / tiles;
+  local -= split * tiles;
+  const int tm = local / P.tiles_n;
+  const int tn = local - tm * P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm0 = (wave >> 1) * TL::WM;
+  const int wn0 = (wave & 1) * TL::WN;
+
+  // ---- k-tile schedule ------------------------------------------------------------
+  const int kt0 = P.K[0] / BK;
+  const int kt1 = P.nseg > 1 ? P.K[1] / BK : 0;
+  int t_begin = 0, t_end = kt0 + kt1;
+  if (P.splits > 1) {
+    const int per = kt0 / P.splits;
+    t_begin = split * per;
+    t_end = t_begin + per;
+  }
+
+  char* As_base = smem;
+  char* Bs_base = smem + 2 * BM * 128;
+
+  i32x4 ra[TL::A_CHUNKS], rb[TL::B_CHUNKS];
+
+  auto load_global = [&](int t) {
+    const int seg = t < kt0 ? 0 : 1;
+    const int k0 = (seg == 0 ? t : t - kt0) * BK;
+    const T* A = reinterpret_cast<const T*>(P.A[seg]);
+    const T* Bm = reinterpret_cast<const T*>(P.B[seg]);
+    const int64_t lda = P.lda[seg], ldb = P.ldb[seg];
+#pragma unroll
+    for (int i = 0; i < TL::A_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      ra[i] = *reinterpret_cast<const i32x4*>(A + (int64_t)(m0 + row) * lda + k0 + ch * CH);
+    }
+#pragma unroll
+    for (int i = 0; i < TL::B_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      rb[i] = *reinterpret_cast<const i32x4*>(Bm + (int64_t)(n0 + row) * ldb + k0 + ch * CH);
+    }
+  };
+  auto store_lds = [&](int buf) {
+    char* As = As_base + buf * BM * 128;
+    char* Bs = Bs_base + buf * BN * 128;
+#pragma unroll
+    for (int i = 0; i < TL::A_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<i32x4*>(As + swz(c >> 3, c & 7)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < TL::B_CHUNKS; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<i32x4*>(Bs + swz(c >> 3, c & 7)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TL::TM][TL::TN];
+#pragma unroll
+  for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TL::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (t_begin < t_end) {
+    load_global(t_begin);
+    store_lds(0);
+    __syncthreads();
+    int buf = 0;
+#pragma unroll 1
+    for (int t = t_begin; t < t_end; ++t) {
+      const bool more = t + 1 < t_end;
+      if (more) load_global(t + 1);
+      compute_tile<T, BM, BN>(As_base + buf * BM * 128, Bs_base + buf * BN * 128, wm0, wn0, lane, acc);
+      if (more) store_lds(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // ---- epilogue ------------------------------------------------------------------
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int CLD = TL::CLD;
+  {
+    const int cr = (lane >> 4) * 4;
+    const int cc = lane & 15;
+#pragma unroll
+    for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TL::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cs[(wm0 + i * 16 + cr + r) * CLD + wn0 + j * 16 + cc] = acc[i][j][r];
+  }
+  __syncthreads();
+
+  constexpr int NQ = BN / 4;  // float4 chunks per row
+  if (P.slab != nullptr) {
+    float* dst = P.slab + (int64_t)split * P.slab_stride;
+#pragma unroll 4
+    for (int c = tid; c < BM * NQ; c += 256) {
+      const int row = c / NQ, q = c - row * NQ;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Cs + row * CLD + q * 4);
+      *reinterpret_cast<f32x4*>(dst + (int64_t)(m0 + row) * P.slab_ld + n0 + q * 4) = v;
+    }
+    return;
+  }
+
+  const bool need_back = P.CT != nullptr || P.colsum != nullptr;
+#pragma unroll 4
+  for (int c = tid; c < BM * NQ; c += 256) {
+    const int row = c / NQ, q = c - row * NQ;
+    const int m = m0 + row, n = n0 + q * 4;
+    f32x4 v = *reinterpret_cast<const f32x4*>(Cs + row * CLD + q * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (P.bias0 != nullptr) x += P.bias0[n + e];
+      if (P.bias1 != nullptr) x += P.bias1[n + e];
+      if (P.relu) x = fmaxf(x, 0.f);
+      if (P.mask != nullptr && !(ld_elem<T>(P.mask, (int64_t)m * P.ldmask + n + e) > 0.f)) x = 0.f;
+      v[e] = x;
+    }
+    if (need_back) *reinterpret_cast<f32x4*>(Cs + row * CLD + q * 4) = v;
+    if (P.C != nullptr) {
+      if (P.c_f32 || sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + (int64_t)m * P.ldc + n) = v;
+      } else {
+        bf16x4 h = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(P.C) + (int64_t)m * P.ldc + n) = h;
+      }
+    }
+  }
+  if (!need_back) return;
+  __syncthreads();
+
+  if (P.CT != nullptr) {
+    constexpr int MQ = BM / 4;
+#pragma unroll 4
+    for (int c = tid; c < BN * MQ; c += 256) {
+      const int col = c / MQ, q = c - col * MQ;
+      const float x0 = Cs[(q * 4 + 0) * CLD + col];
+      const float x1 = Cs[(q * 4 + 1) * CLD + col];
+      const float x2 = Cs[(q * 4 + 2) * CLD + col];
+      const float x3 = Cs[(q * 4 + 3) * CLD + col];
+      const int64_t off = (int64_t)(n0 + col) * P.ldct + m0 + q * 4;
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.CT) + off) = f32x4{x0, x1, x2, x3};
+      } else {
+        bf16x4 h = {(bf16)x0, (bf16)x1, (bf16)x2, (bf16)x3};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(P.CT) + off) = h;
+      }
+    }
+  }
+  if (P.colsum != nullptr) {
+    // one partial per 64 rows, independent of the tile height: the number of partials
+    // of a bias gradient is then a function of the batch only
+    constexpr int PARTS = BM / 64;
+    for (int c = tid; c < BN * PARTS; c += 256) {
+      const int col = c % BN, part = c / BN;
+      float s = 0.f;
+#pragma unroll 8
+      for (int row = part * 64; row < part * 64 + 64; ++row) s += Cs[row * CLD + col];
+      P.colsum[(int64_t)(m0 / 64 + part) * P.N + n0 + col] = s;
+    }
+  }
+}
+
+template <typename T, int BM, int BN>
+int launch_typed(const GemmBatch& b, hipStream_t stream) {
+  gemm_nt_kernel<T, BM, BN><<<dim3((unsigned)b.total_blocks), dim3(256), 0, stream>>>(b);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
+
+}  // namespace
+
+int launch_gemm(GemmBatch& b, int mode, GemmTile tile, hipStream_t stream) {
+  const int BM = tile_bm(tile), BN = tile_bn(tile);
+  const int BK = mode == INF_MODE_BF16 ? 64 : 32;
+  INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= GEMM_MAX_PROBLEMS, "gemm: problem count");
+  int blocks = 0;
+  for (int i = 0; i < b.nprob; ++i) {
+    GemmProblem& p = b.p[i];
+    INF_CHECK_ARG(p.M > 0 && p.N > 0 && p.M % BM == 0 && p.N % BN == 0, "gemm: M/N not tile multiples");
+    INF_CHECK_ARG(p.nseg == 1 || p.nseg == 2, "gemm: nseg");
+    for (int s = 0; s < p.nseg; ++s) {
+      INF_CHECK_ARG(p.K[s] > 0 && p.K[s] % BK == 0, "gemm: K not a k-tile multiple");
+      INF_CHECK_ARG(p.A[s] != nullptr && p.B[s] != nullptr, "gemm: null operand");
+      INF_CHECK_ARG(p.lda[s] % 8 == 0 && p.ldb[s] % 8 == 0, "gemm: operand rows must be 16-byte aligned");
+    }
+    if (p.splits < 1) p.splits = 1;
+    INF_CHECK_ARG(p.splits == 1 || (p.nseg == 1 && (p.K[0] / BK) % p.splits == 0 && p.slab != nullptr),
+                  "gemm: split-K needs one segment, divisible k-tiles and a slab");
+    INF_CHECK_ARG(p.slab != nullptr || p.C != nullptr || p.CT != nullptr || p.colsum != nullptr, "gemm: no output");
+    p.tiles_m = p.M / BM;
+    p.tiles_n = p.N / BN;
+    p.block_begin = blocks;
+    blocks += p.tiles_m * p.tiles_n * p.splits;
+  }
+  b.total_blocks = blocks;
+  if (mode == INF_MODE_BF16) {
+    if (tile == TILE_128x128) return launch_typed<bf16, 128, 128>(b, stream);
+    return launch_typed<bf16, 64, 64>(b, stream);
+  }
+  if (tile == TILE_128x128) return launch_typed<float, 128, 128>(b, stream);
+  return launch_typed<float, 64, 64>(b, stream);
+}
+
+}  // namespace inf

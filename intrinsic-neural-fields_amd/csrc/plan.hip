@@ -1,0 +1,701 @@
+// inf_plan: one TextureField (model.py:12-112) bound to caller-owned buffers, and the
+// launch sequences of its forward, backward, fused training step (trainer.py:71-84),
+// Adam update (config.py:108) and render slice (renderer.py:112-146).
+//
+// Launch sequence of a fused training step (L layers, skip s):
+//   gather (X, X^T) -> L-1 forward GEMMs (Y_l, Y_l^T; bias+ReLU; skip layer = one GEMM
+//   over two K segments [h | x]) -> head_fwd (sigmoid, loss, dz) -> head_bwd (dZ_{L-2})
+//   -> L-2 dX GEMMs (ReLU mask + bias-grad partials) -> ONE grouped split-K dW GEMM over
+//   all weight matrices -> ONE update launch (slab reduction + Adam + packed weights).
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "adam.hpp"
+#include "gemm.hpp"
+#include "head.hpp"
+
+namespace inf {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
+
+__global__ void ctrl_advance_kernel(inf_ctrl* c) { c->batch_index += 1; }
+
+struct ParamSeg {
+  int64_t off = 0;
+  int32_t R = 0, C = 0;  // weight: [R][C]; bias: R = 1
+  int32_t layer = 0;
+  int32_t kind = 0;      // 0 weight, 1 bias
+  int32_t sub = 0;       // skip layer: 0 = Lx, 1 = Ly
+  // packed shadow (GEMM weights only)
+  int32_t gemm = 0;
+  int32_t c_pad = 0;
+  int64_t w_off = 0, wt_off = 0;  // bytes into shadow
+};
+
+constexpr int64_t ALIGN = 256;
+
+}  // namespace
+}  // namespace inf
+
+using namespace inf;
+
+struct inf_plan {
+  inf_mlp_desc d{};
+  int max_batch = 0;
+  int k_pad = 0, H = 0, L = 0, s = 0, mode = 0;
+  int64_t esz = 4;
+  int dw_splits = 1;
+  int train_unit = 128;
+  int bp_max = 0;
+  int grid_hb = 1;
+  std::vector<ParamSeg> segs;
+  int64_t P = 0;
+  int64_t shadow_bytes = 0;
+
+  // workspace layout (byte offsets)
+  int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_ws_end = 0;
+  std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
+  std::vector<int64_t> o_slab;                            // per param segment (weights)
+  int64_t o_hw = 0, o_hb = 0;                             // head partials
+  int64_t table_bytes = 0;
+
+  // bound buffers
+  float* params = nullptr;
+  float* grads = nullptr;
+  float* exp_avg = nullptr;
+  float* exp_avg_sq = nullptr;
+  char* shadow = nullptr;
+  char* ws = nullptr;
+  inf_ctrl* ctrl = nullptr;
+  bool bound = false;
+
+  std::vector<AdamSeg> adam_segs;
+  std::vector<AdamItem> adam_items;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+
+  // saved forward
+  int saved_batch = 0, saved_bp = 0;
+  bool saved = false;
+
+  template <typename T = char>
+  T* W(int64_t off) const { return reinterpret_cast<T*>(ws + off); }
+  const ParamSeg* weight_seg(int layer, int sub) const {
+    for (const auto& p : segs)
+      if (p.layer == layer && p.kind == 0 && p.sub == sub) return &p;
+    return nullptr;
+  }
+  const ParamSeg* bias_seg(int layer, int sub) const {
+    for (const auto& p : segs)
+      if (p.layer == layer && p.kind == 1 && p.sub == sub) return &p;
+    return nullptr;
+  }
+};
+
+namespace {
+
+int64_t align_up(int64_t x) { return round_up(x, ALIGN); }
+
+int build_layout(inf_plan* p) {
+  const auto& d = p->d;
+  p->H = d.hidden;
+  p->L = d.num_layers;
+  p->s = d.skip;
+  p->mode = d.mode;
+  p->esz = d.mode == INF_MODE_BF16 ? 2 : 4;
+  p->k_pad = (int)round_up(d.in_dim, 128);
+  const int H = p->H, L = p->L, s = p->s;
+
+  // ---- parameter arena (model.parameters() order) ----
+  int64_t off = 0;
+  auto add = [&](int layer, int kind, int sub, int R, int C) {
+    ParamSeg g;
+    g.off = off;
+    g.R = R;
+    g.C = C;
+    g.layer = layer;
+    g.kind = kind;
+    g.sub = sub;
+    off += (int64_t)R * C;
+    p->segs.push_back(g);
+  };
+  for (int i = 0; i < L; ++i) {
+    if (i == s) {
+      add(i, 0, 0, H, H);
+      add(i, 1, 0, 1, H);
+      add(i, 0, 1, H, d.in_dim);
+      add(i, 1, 1, 1, H);
+    } else if (i == L - 1) {
+      add(i, 0, 0, d.out_dim, H);
+      add(i, 1, 0, 1, d.out_dim);
+    } else {
+      add(i, 0, 0, H, i == 0 ? d.in_dim : H);
+      add(i, 1, 0, 1, H);
+    }
+  }
+  p->P = off;
+
+  // ---- packed shadows for the GEMM weights ----
+  int64_t sh = 0;
+  int64_t gemm_tiles = 0;
+  for (auto& g : p->segs) {
+    if (g.kind != 0 || g.layer == L - 1) continue;
+    g.gemm = 1;
+    g.c_pad = g.C == H ? H : p->k_pad;
+    g.w_off = sh;
+    sh = align_up(sh + (int64_t)g.R * g.c_pad * p->esz);
+    g.wt_off = sh;
+    sh = align_up(sh + (int64_t)g.c_pad * g.R * p->esz);
+    const int bt = (H % 128 == 0) ? 128 : 64;
+    gemm_tiles += (g.R / bt) * (g.c_pad / bt);
+  }
+  p->shadow_bytes = sh;
+
+  // ---- split-K factor of the weight-gradient GEMMs and batch padding ----
+  int S = 1;
+  const int64_t mb = round_up(std::max(p->max_batch, 1), 128);
+  while (gemm_tiles * S < 512 && S < 16 && mb / (S * 2) >= 512) S *= 2;
+  p->dw_splits = S;
+  p->train_unit = (int)std::max<int64_t>(128, (int64_t)S * 64);
+  p->bp_max = (int)round_up(p->max_batch, p->train_unit);
+  p->grid_hb = (int)std::min<int64_t>(256, p->bp_max / HEAD_BWD_RAYS);
+  const int64_t Bp = p->bp_max;
+
+  // ---- workspace ----
+  int64_t w = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t o = w;
+    w = align_up(w + bytes);
+    return o;
+  };
+  p->o_x0 = take(Bp * p->k_pad * p->esz);
+  p->o_x0t = take((int64_t)p->k_pad * Bp * p->esz);
+  for (int l = 0; l < L - 1; ++l) {
+    p->o_y.push_back(take(Bp * H * p->esz));
+    p->o_yt.push_back(take(Bp * H * p->esz));
+    p->o_dZ.push_back(take(Bp * H * p->esz));
+    p->o_dZT.push_back(take(Bp * H * p->esz));
+    const int64_t parts = std::max<int64_t>(Bp / 64, p->grid_hb);
+    p->o_colsum.push_back(take(parts * H * 4));
+  }
+  p->o_dz = take(Bp * 3 * 4);
+  p->o_pred = take(Bp * 3 * 4);
+  p->o_slab.assign(p->segs.size(), 0);
+  for (size_t i = 0; i < p->segs.size(); ++i) {
+    const auto& g = p->segs[i];
+    if (g.gemm) p->o_slab[i] = take((int64_t)S * g.R * g.c_pad * 4);
+  }
+  p->o_hw = take((int64_t)p->grid_hb * 3 * H * 4);
+  p->o_hb = take((int64_t)p->grid_hb * 3 * 4);
+
+  // update work list
+  int64_t nitems = 0;
+  for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, 64) * ceil_div(g.C, 64) : ceil_div((int64_t)g.R * g.C, 8);
+  p->table_bytes = align_up((int64_t)p->segs.size() * sizeof(AdamSeg)) + align_up(nitems * sizeof(AdamItem));
+  p->o_tables = take(p->table_bytes);
+  p->o_ws_end = w;
+  return INF_OK;
+}
+
+GemmTile pick_tile(const inf_plan* p, int64_t M, int64_t N) {
+  if (M % 128 || N % 128) return TILE_64x64;
+  const int64_t blocks = (M / 128) * (N / 128);
+  return blocks >= 256 ? TILE_128x128 : TILE_64x64;
+}
+
+GemmProblem blank_problem() {
+  GemmProblem q;
+  std::memset(&q, 0, sizeof(q));
+  q.nseg = 1;
+  q.splits = 1;
+  return q;
+}
+
+int dtype_of(const inf_plan* p) { return p->mode == INF_MODE_BF16 ? INF_DTYPE_BF16 : INF_DTYPE_F32; }
+
+// ---------------------------------------------------------------------------------
+int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStream_t st) {
+  void* x0 = p->W(p->o_x0);
+  void* x0t = transposed ? (void*)p->W(p->o_x0t) : nullptr;
+  if (b->table != nullptr) {
+    const int64_t k_table = p->k_pad;  // device tables are packed with k_pad zero-filled columns
+    return launch_gather(b->table, b->table_dtype, b->num_vertices, (int)k_table, k_table, b->vids, b->vid_dtype,
+                         b->bary, b->ray_idx, b->idx_dtype, b->idx_offset,
+                         b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr, 0, b->batch, x0, dtype_of(p),
+                         p->k_pad, Bp, x0t, Bp, st);
+  }
+  INF_CHECK_ARG(b->features != nullptr, "batch has neither a table nor features");
+  return launch_pack_features(b->features, b->ld_features, p->d.in_dim, b->batch, x0, dtype_of(p), p->k_pad, Bp,
+                              x0t, Bp, st);
+}
+
+int run_forward_layers(inf_plan* p, int Bp, bool transposed, hipStream_t st) {
+  const int H = p->H;
+  const GemmTile tile = pick_tile(p, Bp, H);
+  for (int l = 0; l < p->L - 1; ++l) {
+    GemmBatch gb;
+    std::memset(&gb, 0, sizeof(gb));
+    gb.nprob = 1;
+    GemmProblem& q = gb.p[0];
+    q = blank_problem();
+    const ParamSeg* w = p->weight_seg(l, 0);
+    const ParamSeg* bs = p->bias_seg(l, 0);
+    q.A[0] = l == 0 ? (const void*)p->W(p->o_x0) : (const void*)p->W(p->o_y[l - 1]);
+    q.lda[0] = l == 0 ? p->k_pad : H;
+    q.B[0] = p->shadow + w->w_off;
+    q.ldb[0] = w->c_pad;
+    q.K[0] = l == 0 ? p->k_pad : H;
+    q.bias0 = p->params + bs->off;
+    if (l == p->s) {
+      const ParamSeg* wy = p->weight_seg(l, 1);
+      q.nseg = 2;
+      q.A[1] = p->W(p->o_x0);
+      q.lda[1] = p->k_pad;
+      q.B[1] = p->shadow + wy->w_off;
+      q.ldb[1] = wy->c_pad;
+      q.K[1] = p->k_pad;
+      q.bias1 = p->params + p->bias_seg(l, 1)->off;
+    }
+    q.M = Bp;
+    q.N = H;
+    q.relu = 1;
+    q.C = p->W(p->o_y[l]);
+    q.ldc = H;
+    if (transposed) {
+      q.CT = p->W(p->o_yt[l]);
+      q.ldct = Bp;
+    }
+    int rc = launch_gemm(gb, p->mode, tile, st);
+    if (rc) return rc;
+  }
+  return INF_OK;
+}
+
+// Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
+int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
+  const int H = p->H, L = p->L, s = p->s;
+  const GemmTile tile = pick_tile(p, Bp, H);
+  for (int l = L - 2; l >= 1; --l) {
+    GemmBatch gb;
+    std::memset(&gb, 0, sizeof(gb));
+    gb.nprob = 1;
+    GemmProblem& q = gb.p[0];
+    q = blank_problem();
+    const ParamSeg* w = p->weight_seg(l, 0);  // Lx at the skip layer
+    q.A[0] = p->W(p->o_dZ[l]);
+    q.lda[0] = H;
+    q.B[0] = p->shadow + w->wt_off;
+    q.ldb[0] = w->R;
+    q.K[0] = H;
+    q.M = Bp;
+    q.N = H;
+    q.mask = p->W(p->o_y[l - 1]);
+    q.ldmask = H;
+    if (l - 1 >= 1) {
+      q.C = p->W(p->o_dZ[l - 1]);
+      q.ldc = H;
+    }
+    q.CT = p->W(p->o_dZT[l - 1]);
+    q.ldct = Bp;
+    q.colsum = p->W<float>(p->o_colsum[l - 1]);
+    int rc = launch_gemm(gb, p->mode, tile, st);
+    if (rc) return rc;
+  }
+  // weight gradients: one grouped split-K launch (chunks of GEMM_MAX_PROBLEMS)
+  std::vector<GemmProblem> probs;
+  for (size_t i = 0; i < p->segs.size(); ++i) {
+    const ParamSeg& g = p->segs[i];
+    if (!g.gemm) continue;
+    GemmProblem q = blank_problem();
+    const int l = g.layer;
+    q.A[0] = p->W(p->o_dZT[l]);
+    q.lda[0] = Bp;
+    const bool from_input = (l == 0) || (l == s && g.sub == 1);
+    q.B[0] = from_input ? (const void*)p->W(p->o_x0t) : (const void*)p->W(p->o_yt[l - 1]);
+    q.ldb[0] = Bp;
+    q.K[0] = Bp;
+    q.M = g.R;
+    q.N = g.c_pad;
+    q.splits = p->dw_splits;
+    q.slab = p->W<float>(p->o_slab[i]);
+    q.slab_ld = g.c_pad;
+    q.slab_stride = (int64_t)g.R * g.c_pad;
+    probs.push_back(q);
+  }
+  const GemmTile wtile = (H % 128 == 0) ? TILE_128x128 : TILE_64x64;
+  for (size_t i0 = 0; i0 < probs.size(); i0 += GEMM_MAX_PROBLEMS) {
+    GemmBatch gb;
+    std::memset(&gb, 0, sizeof(gb));
+    gb.nprob = (int)std::min<size_t>(GEMM_MAX_PROBLEMS, probs.size() - i0);
+    for (int j = 0; j < gb.nprob; ++j) gb.p[j] = probs[i0 + j];
+    int rc = launch_gemm(gb, p->mode, wtile, st);
+    if (rc) return rc;
+  }
+  return INF_OK;
+}
+
+AdamArgs update_args(inf_plan* p, int Bp) {
+  AdamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.segs = p->W<AdamSeg>(p->o_tables);
+  a.items = reinterpret_cast<const AdamItem*>(p->ws + p->o_tables + align_up(p->segs.size() * sizeof(AdamSeg)));
+  a.num_items = (int)p->adam_items.size();
+  a.params = p->params;
+  a.grads = p->grads;
+  a.exp_avg = p->exp_avg;
+  a.exp_avg_sq = p->exp_avg_sq;
+  a.ctrl = p->ctrl;
+  a.beta1_d = p->beta1;
+  a.beta2_d = p->beta2;
+  a.one_minus_b1 = (float)(1.0 - (double)p->beta1);
+  a.beta2 = p->beta2;
+  a.one_minus_b2 = (float)(1.0 - (double)p->beta2);
+  a.eps = p->eps;
+  (void)Bp;
+  return a;
+}
+
+// The bias partial counts depend on the padded batch: refresh the seg table for it.
+int refresh_tables(inf_plan* p, int Bp, hipStream_t st) {
+  const int parts = Bp / 64;
+  bool changed = false;
+  for (size_t i = 0; i < p->segs.size(); ++i) {
+    const ParamSeg& g = p->segs[i];
+    AdamSeg& a = p->adam_segs[i];
+    if (g.kind == 1 && g.layer < p->L - 2 && a.nslab != parts) {
+      a.nslab = parts;
+      changed = true;
+    }
+  }
+  if (!changed) return INF_OK;
+  // Pageable-source async copies are staged by the runtime before returning, so the
+  // host vector may change afterwards.
+  INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
+                             hipMemcpyHostToDevice, st));
+  return INF_OK;
+}
+
+int pad_batch(inf_plan* p, int B, bool train, int* Bp) {
+  INF_CHECK_ARG(B >= 1 && B <= p->max_batch, "batch size out of range for this plan");
+  *Bp = (int)round_up(B, train ? p->train_unit : 128);
+  INF_CHECK_ARG(*Bp <= p->bp_max, "padded batch exceeds the plan");
+  return INF_OK;
+}
+
+int head_forward(inf_plan* p, const inf_batch* b, int Bp, float* pred, bool loss, const int64_t* hit,
+                 const int64_t* pixel_map, float* img, hipStream_t st) {
+  HeadFwdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const ParamSeg* w = p->weight_seg(p->L - 1, 0);
+  a.h = p->W(p->o_y[p->L - 2]);
+  a.ldh = p->H;
+  a.H = p->H;
+  a.W = p->params + w->off;
+  a.bias = p->params + p->bias_seg(p->L - 1, 0)->off;
+  a.batch = b->batch;
+  a.rows = Bp;
+  a.pred = pred;
+  if (loss) {
+    INF_CHECK_ARG(b->rgb != nullptr, "training batch without target colours");
+    a.rgb = b->rgb;
+    a.ray_idx = b->ray_idx;
+    a.idx_dtype = b->idx_dtype;
+    a.idx_offset = b->idx_offset;
+    a.offset_from_ctrl = b->offset_from_ctrl;
+    a.loss = b->loss >= 0 ? b->loss : p->d.loss;
+    INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
+    const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
+    a.inv_count = (float)(1.0 / (double)cnt);
+    a.dz = p->W<float>(p->o_dz);
+  }
+  a.ctrl = p->ctrl;
+  a.hit = hit;
+  a.pixel_map = pixel_map;
+  a.img = img;
+  return launch_head_fwd(a, p->mode, st);
+}
+
+int head_backward(inf_plan* p, int Bp, const float* dpred, bool count_step, hipStream_t st) {
+  HeadBwdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const int L = p->L;
+  a.dz = dpred == nullptr ? p->W<float>(p->o_dz) : nullptr;
+  a.dpred = dpred;
+  a.pred = p->W<float>(p->o_pred);
+  a.h = p->W(p->o_y[L - 2]);
+  a.ldh = p->H;
+  a.H = p->H;
+  a.W = p->params + p->weight_seg(L - 1, 0)->off;
+  a.batch = p->saved_batch;
+  a.rows = Bp;
+  a.dZ = (L - 2 >= 1) ? p->W(p->o_dZ[L - 2]) : nullptr;
+  a.ldz = p->H;
+  a.dZT = p->W(p->o_dZT[L - 2]);
+  a.ldzt = Bp;
+  a.colsum = p->W<float>(p->o_colsum[L - 2]);
+  a.dW_part = p->W<float>(p->o_hw);
+  a.db_part = p->W<float>(p->o_hb);
+  a.step_ctrl = count_step ? p->ctrl : nullptr;
+  a.grid = p->grid_hb;
+  return launch_head_bwd(a, p->mode, st);
+}
+
+int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool loss, const int64_t* hit,
+                 const int64_t* pixel_map, float* img, hipStream_t st) {
+  INF_CHECK_ARG(b != nullptr, "null batch");
+  int Bp = 0;
+  int rc = pad_batch(p, b->batch, save, &Bp);
+  if (rc) return rc;
+  if ((rc = run_input(p, b, Bp, save, st))) return rc;
+  if ((rc = run_forward_layers(p, Bp, save, st))) return rc;
+  float* pred_ws = p->W<float>(p->o_pred);
+  if ((rc = head_forward(p, b, Bp, save ? pred_ws : pred, loss, hit, pixel_map, img, st))) return rc;
+  if (save && pred != nullptr && pred != pred_ws)
+    INF_HIP_TRY(hipMemcpyAsync(pred, pred_ws, (size_t)b->batch * 3 * 4, hipMemcpyDeviceToDevice, st));
+  p->saved = save;
+  p->saved_batch = b->batch;
+  p->saved_bp = Bp;
+  return INF_OK;
+}
+
+}  // namespace
+
+// =================================================================================
+extern "C" {
+
+const char* inf_last_error(void) { return g_last_error.c_str(); }
+int inf_abi_version(void) { return 1; }
+
+int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, int64_t table_ld, const void* vids,
+               int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
+               void* out, int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t,
+               inf_stream_t stream) {
+  return launch_gather(table, table_dtype, num_vertices, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype,
+                       idx_offset, nullptr, 0, batch, out, out_dtype, ld_out, rows_out, out_t, ld_out_t,
+                       (hipStream_t)stream);
+}
+
+int inf_plan_create(const inf_mlp_desc* desc, int max_batch, inf_plan** plan) {
+  INF_CHECK_ARG(desc != nullptr && plan != nullptr, "null argument");
+  const inf_mlp_desc& d = *desc;
+  INF_CHECK_ARG(d.num_layers > 2 && d.skip > 0 && d.skip < d.num_layers - 1,
+                "need num_layers > 2 and 0 < skip_layer_idx < num_layers-1 (model.py:27)");
+  INF_CHECK_ARG(d.in_dim >= 1, "in_dim must be positive");
+  INF_CHECK_ARG(d.hidden >= 64 && d.hidden % 64 == 0 && d.hidden <= 512,
+                "mlp_hidden_dim must be a multiple of 64 in [64, 512]");
+  INF_CHECK_ARG(d.out_dim == 3, "out_dim must be 3 (RGB head)");
+  INF_CHECK_ARG(d.mode == INF_MODE_FP32 || d.mode == INF_MODE_BF16, "mode");
+  INF_CHECK_ARG(d.loss >= INF_LOSS_L2 && d.loss <= INF_LOSS_CAUCHY, "loss type");
+  INF_CHECK_ARG(max_batch >= 1, "max_batch");
+  inf_plan* p = new inf_plan();
+  p->d = d;
+  p->max_batch = max_batch;
+  int rc = build_layout(p);
+  if (rc) {
+    delete p;
+    return rc;
+  }
+  *plan = p;
+  return INF_OK;
+}
+
+void inf_plan_destroy(inf_plan* plan) { delete plan; }
+
+int inf_plan_get_info(const inf_plan* p, inf_plan_info* info) {
+  INF_CHECK_ARG(p != nullptr && info != nullptr, "null argument");
+  info->num_params = p->P;
+  info->num_segments = (int32_t)p->segs.size();
+  info->in_pad = p->k_pad;
+  info->max_batch_pad = p->bp_max;
+  info->dw_splits = p->dw_splits;
+  info->shadow_bytes = p->shadow_bytes;
+  info->workspace_bytes = p->o_ws_end;
+  info->table_ld = p->k_pad;
+  return INF_OK;
+}
+
+int inf_plan_param_layout(const inf_plan* p, int64_t* offsets, int64_t* numels, int n) {
+  INF_CHECK_ARG(p != nullptr && offsets != nullptr && numels != nullptr, "null argument");
+  INF_CHECK_ARG(n == (int)p->segs.size(), "segment count mismatch");
+  for (int i = 0; i < n; ++i) {
+    offsets[i] = p->segs[i].off;
+    numels[i] = (int64_t)p->segs[i].R * p->segs[i].C;
+  }
+  return INF_OK;
+}
+
+int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* shadow,
+                  void* workspace, inf_ctrl* ctrl) {
+  INF_CHECK_ARG(p != nullptr && params != nullptr && shadow != nullptr && workspace != nullptr && ctrl != nullptr,
+                "bind: params, shadow, workspace and ctrl are required");
+  INF_CHECK_ARG(((uintptr_t)shadow % 256) == 0 && ((uintptr_t)workspace % 256) == 0,
+                "bind: shadow/workspace must be 256-byte aligned");
+  p->params = params;
+  p->grads = grads;
+  p->exp_avg = exp_avg;
+  p->exp_avg_sq = exp_avg_sq;
+  p->shadow = (char*)shadow;
+  p->ws = (char*)workspace;
+  p->ctrl = ctrl;
+
+  // update work list
+  p->adam_segs.clear();
+  p->adam_items.clear();
+  const int L = p->L;
+  for (size_t i = 0; i < p->segs.size(); ++i) {
+    const ParamSeg& g = p->segs[i];
+    AdamSeg a;
+    std::memset(&a, 0, sizeof(a));
+    a.off = g.off;
+    if (g.gemm) {
+      a.R = g.R;
+      a.C = g.C;
+      a.matrix = 1;
+      a.nslab = p->dw_splits;
+      a.slab = p->W<float>(p->o_slab[i]);
+      a.slab_stride = (int64_t)g.R * g.c_pad;
+      a.slab_ld = g.c_pad;
+      a.W = p->shadow + g.w_off;
+      a.ldw = g.c_pad;
+      a.WT = p->shadow + g.wt_off;
+      a.ldwt = g.R;
+      for (int r = 0; r < g.R; r += 64)
+        for (int c = 0; c < g.C; c += 64) p->adam_items.push_back(AdamItem{(int32_t)i, r, c, 0});
+    } else {
+      a.R = 1;
+      a.C = g.R * g.C;
+      a.matrix = 0;
+      if (g.layer == L - 1) {  // output layer: partials from head_bwd
+        a.nslab = p->grid_hb;
+        a.slab = g.kind == 0 ? p->W<float>(p->o_hw) : p->W<float>(p->o_hb);
+        a.slab_stride = (int64_t)g.R * g.C;
+      } else {  // hidden bias: column-sum partials of dZ_layer
+        a.nslab = g.layer == L - 2 ? p->grid_hb : p->bp_max / 64;
+        a.slab = p->W<float>(p->o_colsum[g.layer]);
+        a.slab_stride = p->H;
+      }
+      for (int e = 0; e < a.C; e += 8) p->adam_items.push_back(AdamItem{(int32_t)i, 0, e, 0});
+    }
+    p->adam_segs.push_back(a);
+  }
+  const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
+  INF_CHECK_ARG(seg_bytes + (int64_t)(p->adam_items.size() * sizeof(AdamItem)) <= p->table_bytes, "table size");
+  INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
+                        hipMemcpyHostToDevice));
+  INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables + seg_bytes, p->adam_items.data(),
+                        p->adam_items.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  // padded shadow columns/rows must read as zero
+  INF_HIP_TRY(hipMemset(p->shadow, 0, p->shadow_bytes));
+  p->bound = true;
+  p->saved = false;
+  return INF_OK;
+}
+
+int inf_plan_set_adam(inf_plan* p, float beta1, float beta2, float eps) {
+  INF_CHECK_ARG(p != nullptr, "null plan");
+  INF_CHECK_ARG(beta1 >= 0.f && beta1 < 1.f && beta2 >= 0.f && beta2 < 1.f && eps >= 0.f, "Adam hyper-parameters");
+  p->beta1 = beta1;
+  p->beta2 = beta2;
+  p->eps = eps;
+  return INF_OK;
+}
+
+int inf_sync_shadow(inf_plan* p, inf_stream_t stream) {
+  INF_CHECK_ARG(p != nullptr && p->bound, "plan not bound");
+  AdamArgs a = update_args(p, p->bp_max);
+  a.grad_src = GRAD_NONE;
+  a.write_shadow = 1;
+  return launch_update(a, p->mode, (hipStream_t)stream);
+}
+
+int inf_forward(inf_plan* p, const inf_batch* batch, float* pred, int save, inf_stream_t stream) {
+  if (p == nullptr || !p->bound) {
+    set_error("plan not bound");
+    return INF_ERR_STATE;
+  }
+  INF_CHECK_ARG(pred != nullptr, "forward: pred output required");
+  return forward_impl(p, batch, pred, save != 0, false, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int inf_backward(inf_plan* p, const float* dpred, float* grads, inf_stream_t stream) {
+  if (p == nullptr || !p->bound || !p->saved) {
+    set_error("backward without a saved forward");
+    return INF_ERR_STATE;
+  }
+  INF_CHECK_ARG(dpred != nullptr && grads != nullptr, "backward: dpred and grads required");
+  hipStream_t st = (hipStream_t)stream;
+  const int Bp = p->saved_bp;
+  int rc;
+  if ((rc = head_backward(p, Bp, dpred, false, st))) return rc;
+  if ((rc = run_backward_layers(p, Bp, st))) return rc;
+  if ((rc = refresh_tables(p, Bp, st))) return rc;
+  AdamArgs a = update_args(p, Bp);
+  a.grads = grads;
+  a.grad_src = GRAD_SLABS;
+  a.write_grads = 1;
+  return launch_update(a, p->mode, st);
+}
+
+int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int apply_adam, inf_stream_t stream) {
+  if (p == nullptr || !p->bound) {
+    set_error("plan not bound");
+    return INF_ERR_STATE;
+  }
+  INF_CHECK_ARG(batch != nullptr && batch->rgb != nullptr, "train_step: batch with target colours required");
+  INF_CHECK_ARG(p->grads != nullptr || apply_adam, "train_step: grads not bound");
+  INF_CHECK_ARG(!apply_adam || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr), "train_step: Adam state");
+  hipStream_t st = (hipStream_t)stream;
+  INF_HIP_TRY(hipMemsetAsync(&p->ctrl->loss_sum, 0, 2 * sizeof(double), st));
+  int rc;
+  if ((rc = forward_impl(p, batch, pred, true, true, nullptr, nullptr, nullptr, st))) return rc;
+  const int Bp = p->saved_bp;
+  if ((rc = head_backward(p, Bp, nullptr, true, st))) return rc;
+  if ((rc = run_backward_layers(p, Bp, st))) return rc;
+  if ((rc = refresh_tables(p, Bp, st))) return rc;
+  AdamArgs a = update_args(p, Bp);
+  a.grad_src = GRAD_SLABS;
+  if (apply_adam) {
+    a.do_adam = 1;
+    a.write_shadow = 1;
+  } else {
+    a.write_grads = 1;
+  }
+  return launch_update(a, p->mode, st);
+}
+
+int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) {
+  if (p == nullptr || !p->bound || p->grads == nullptr || p->exp_avg == nullptr || p->exp_avg_sq == nullptr) {
+    set_error("adam: plan not bound with grads and Adam state");
+    return INF_ERR_STATE;
+  }
+  AdamArgs a = update_args(p, p->bp_max);
+  a.grad_src = GRAD_FLAT;
+  a.do_adam = 1;
+  a.write_shadow = 1;
+  a.step_host = step;
+  a.lr_host = lr;
+  return launch_update(a, p->mode, (hipStream_t)stream);
+}
+
+int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const int64_t* pixel_map, float* img,
+               inf_stream_t stream) {
+  if (p == nullptr || !p->bound) {
+    set_error("plan not bound");
+    return INF_ERR_STATE;
+  }
+  INF_CHECK_ARG(hit != nullptr && img != nullptr, "render: hit indices and image required");
+  return forward_impl(p, batch, nullptr, false, false, hit, pixel_map, img, (hipStream_t)stream);
+}
+
+int inf_ctrl_advance(inf_plan* p, inf_stream_t stream) {
+  INF_CHECK_ARG(p != nullptr && p->ctrl != nullptr, "plan not bound");
+  ctrl_advance_kernel<<<1, 1, 0, (hipStream_t)stream>>>(p->ctrl);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
+
+}  // extern "C"

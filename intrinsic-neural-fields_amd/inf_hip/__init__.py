@@ -1,0 +1,102 @@
+"""ctypes binding of libinf_hip.so (C ABI declared in include/inf_hip.h).
+
+The library is built in-tree (``make -C intrinsic-neural-fields_amd/csrc`` or
+``__graft_entry__.build()``).  There is no fallback: importing this module without the
+library raises, and every entry point raises ``RuntimeError`` with the library's own
+message on a non-zero status.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libinf_hip.so")
+
+# ---- constants (inf_hip.h) ---------------------------------------------------------
+INF_OK = 0
+DTYPE_F32, DTYPE_BF16, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
+MODE_FP32, MODE_BF16 = 0, 1
+LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
+LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
+MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
+
+c_void_p, c_int, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int32,
+                                                        ctypes.c_int64, ctypes.c_float, ctypes.c_double)
+
+
+class MlpDesc(ctypes.Structure):
+    _fields_ = [("in_dim", c_int32), ("hidden", c_int32), ("num_layers", c_int32), ("skip", c_int32),
+                ("out_dim", c_int32), ("mode", c_int32), ("loss", c_int32)]
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [("num_params", c_int64), ("num_segments", c_int32), ("in_pad", c_int32),
+                ("max_batch_pad", c_int32), ("dw_splits", c_int32), ("shadow_bytes", c_int64),
+                ("workspace_bytes", c_int64), ("table_ld", c_int64)]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("table", c_void_p), ("table_dtype", c_int32), ("num_vertices", c_int64),
+                ("vids", c_void_p), ("vid_dtype", c_int32), ("bary", c_void_p), ("rgb", c_void_p),
+                ("ray_idx", c_void_p), ("idx_dtype", c_int32), ("idx_offset", c_int64),
+                ("offset_from_ctrl", c_int32), ("features", c_void_p), ("ld_features", c_int64),
+                ("batch", c_int32), ("loss_count", c_int64), ("loss", c_int32)]
+
+
+class Ctrl(ctypes.Structure):
+    _fields_ = [("step", c_int32), ("batch_index", c_int32), ("lr", c_float), ("pad", c_int32),
+                ("loss_sum", c_double), ("sse_sum", c_double), ("epoch_loss", c_double),
+                ("epoch_sse", c_double)]
+
+
+CTRL_BYTES = ctypes.sizeof(Ctrl)
+assert CTRL_BYTES == 48
+
+_SIGNATURES = {
+    "inf_last_error": (ctypes.c_char_p, []),
+    "inf_abi_version": (c_int, []),
+    "inf_gather": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                           c_int64, c_int, c_void_p, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p]),
+    "inf_plan_create": (c_int, [ctypes.POINTER(MlpDesc), c_int, ctypes.POINTER(c_void_p)]),
+    "inf_plan_destroy": (None, [c_void_p]),
+    "inf_plan_get_info": (c_int, [c_void_p, ctypes.POINTER(PlanInfo)]),
+    "inf_plan_param_layout": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64), c_int]),
+    "inf_plan_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "inf_plan_set_adam": (c_int, [c_void_p, c_float, c_float, c_float]),
+    "inf_sync_shadow": (c_int, [c_void_p, c_void_p]),
+    "inf_forward": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_int, c_void_p]),
+    "inf_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "inf_train_step": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_int, c_void_p]),
+    "inf_adam": (c_int, [c_void_p, c_int, c_float, c_void_p]),
+    "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
+    "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+
+def _load():
+    # PyTorch ships its own HIP runtime (same soname, libamdhip64.so.7).  Load it first so
+    # the library binds to the runtime that owns torch's device allocations and streams;
+    # loading ours first would put two HIP runtimes in the process.
+    import torch  # noqa: F401
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP library first (make -C intrinsic-neural-fields_amd/csrc "
+            "or python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != INF_OK:
+        msg = lib.inf_last_error().decode(errors="replace")
+        raise RuntimeError(f"inf_hip {what} failed ({rc}): {msg}")

@@ -1,0 +1,260 @@
+"""Torch-facing runtime over the C ABI: device buffers, packed tables, plans.
+
+PyTorch is plumbing here: it allocates device memory and provides the current HIP
+stream; all arithmetic of the hot path runs in libinf_hip.so.  Every function refuses
+CPU tensors (there is no CPU fallback of the product path).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import (CTRL_BYTES, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, LOSS_CODES, MODE_BF16, MODE_CODES, Batch,
+               MlpDesc, PlanInfo, c_int64, c_void_p, check, lib)
+
+_TORCH_DTYPE = {DTYPE_F32: torch.float32, DTYPE_BF16: torch.bfloat16}
+_CODE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.int32: DTYPE_I32, torch.int64: DTYPE_I64}
+
+
+def require_hip(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("intrinsic-neural-fields_amd runs its hot path on MI355X (HIP) devices only; "
+                               f"got a tensor on {t.device}. There is no CPU fallback.")
+
+
+def stream_handle() -> c_void_p:
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> c_void_p | None:
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _CODE[t.dtype]
+    except KeyError:
+        raise RuntimeError(f"unsupported dtype {t.dtype}") from None
+
+
+# ---------------------------------------------------------------------------------
+# Gather (mesh.py:313-324)
+# ---------------------------------------------------------------------------------
+
+def gather(E: torch.Tensor, vids: torch.Tensor, bary: torch.Tensor, ray_idx: torch.Tensor | None = None,
+           offset: int = 0, batch: int | None = None, out_dtype: torch.dtype = torch.float32,
+           k: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """F[b] = sum_i bary[r, i] * E[vids[r, i]] with r = ray_idx[offset + b] (or offset + b).
+    E: [V, ld] fp32/bf16 (first k columns used); vids [N, 3] int32/int64; bary [N, 3] fp32."""
+    require_hip(E, vids, bary, ray_idx)
+    if E.dim() != 2 or E.stride(1) != 1:
+        raise ValueError("E must be a row-major [V, k] matrix")
+    if vids.dim() != 2 or vids.shape[1] != 3 or not vids.is_contiguous():
+        raise ValueError("vertex ids must be a contiguous [N, 3] tensor")
+    if bary.shape != vids.shape or bary.dtype != torch.float32 or not bary.is_contiguous():
+        raise ValueError("barycentric coordinates must be a contiguous fp32 [N, 3] tensor")
+    k = E.shape[1] if k is None else k
+    n_rows = ray_idx.shape[0] if ray_idx is not None else vids.shape[0]
+    batch = n_rows - offset if batch is None else batch
+    if batch < 0 or offset + batch > n_rows:
+        raise ValueError("batch out of range")
+    if out is None:
+        out = torch.empty((batch, k), dtype=out_dtype, device=E.device)
+    if batch == 0:
+        return out
+    check(lib.inf_gather(ptr(E), dtype_code(E), E.shape[0], k, E.stride(0), ptr(vids), dtype_code(vids), ptr(bary),
+                         ptr(ray_idx), dtype_code(ray_idx) if ray_idx is not None else DTYPE_I64, offset, batch,
+                         ptr(out), dtype_code(out), out.stride(0), out.shape[0], None, 0, stream_handle()), "gather")
+    return out
+
+
+def pack_table(E: torch.Tensor, k_pad: int, dtype: torch.dtype) -> torch.Tensor:
+    """Device copy of the V x k table with zero columns up to k_pad (the GEMM tile),
+    in the GEMM dtype (mesh.py:53-108 produces E; this is the upload of it)."""
+    V, k = E.shape
+    T = torch.zeros((V, k_pad), dtype=dtype, device=E.device)
+    T[:, :k] = E
+    return T
+
+
+# ---------------------------------------------------------------------------------
+# Plan
+# ---------------------------------------------------------------------------------
+
+class Plan:
+    """One TextureField architecture bound to a flat parameter arena on one device."""
+
+    def __init__(self, in_dim: int, hidden: int, num_layers: int, skip: int, mode: str, loss: str,
+                 max_batch: int, params: torch.Tensor, grads: torch.Tensor | None = None,
+                 exp_avg: torch.Tensor | None = None, exp_avg_sq: torch.Tensor | None = None):
+        require_hip(params)
+        self.device = params.device
+        self.mode = mode
+        self.mode_code = MODE_CODES[mode]
+        self.loss = loss
+        self.desc = MlpDesc(in_dim, hidden, num_layers, skip, 3, self.mode_code, LOSS_CODES[loss])
+        handle = c_void_p()
+        check(lib.inf_plan_create(ctypes.byref(self.desc), int(max_batch), ctypes.byref(handle)), "plan_create")
+        self.handle = handle
+        self.info = PlanInfo()
+        check(lib.inf_plan_get_info(self.handle, ctypes.byref(self.info)), "plan_get_info")
+        n = self.info.num_segments
+        offs, nums = (c_int64 * n)(), (c_int64 * n)()
+        check(lib.inf_plan_param_layout(self.handle, offs, nums, n), "param_layout")
+        self.offsets = list(offs)
+        self.numels = list(nums)
+        self.max_batch = int(max_batch)
+        self.in_pad = self.info.in_pad
+        self.gemm_dtype = torch.bfloat16 if self.mode_code == MODE_BF16 else torch.float32
+        if params.numel() != self.info.num_params:
+            raise ValueError(f"parameter arena has {params.numel()} floats, plan needs {self.info.num_params}")
+        with torch.cuda.device(self.device):
+            self.shadow = torch.empty(max(self.info.shadow_bytes, 256), dtype=torch.uint8, device=self.device)
+            self.workspace = torch.empty(max(self.info.workspace_bytes, 256), dtype=torch.uint8, device=self.device)
+            self.ctrl = torch.zeros(CTRL_BYTES, dtype=torch.uint8, device=self.device)
+        for t in (self.shadow, self.workspace):
+            assert t.data_ptr() % 256 == 0
+        self.params = params
+        self.bind(grads, exp_avg, exp_avg_sq)
+
+    def bind(self, grads=None, exp_avg=None, exp_avg_sq=None):
+        for t in (grads, exp_avg, exp_avg_sq):
+            if t is not None and (t.numel() != self.info.num_params or t.device != self.device):
+                raise ValueError("optimizer arenas must match the parameter arena")
+        self.grads, self.exp_avg, self.exp_avg_sq = grads, exp_avg, exp_avg_sq
+        with torch.cuda.device(self.device):
+            check(lib.inf_plan_bind(self.handle, ptr(self.params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq),
+                                    ptr(self.shadow), ptr(self.workspace), ptr(self.ctrl)), "plan_bind")
+            self.sync_shadow()
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            lib.inf_plan_destroy(h)
+            self.handle = None
+
+    # ---- ctrl block -------------------------------------------------------------
+    @property
+    def ctrl_i32(self):
+        return self.ctrl.view(torch.int32)
+
+    @property
+    def ctrl_f32(self):
+        return self.ctrl.view(torch.float32)
+
+    @property
+    def ctrl_f64(self):
+        return self.ctrl.view(torch.float64)
+
+    def set_lr(self, lr: float):
+        self.ctrl_f32[2].fill_(float(lr))
+
+    def set_step(self, step: int):
+        self.ctrl_i32[0].fill_(int(step))
+
+    def set_batch_index(self, i: int):
+        self.ctrl_i32[1].fill_(int(i))
+
+    def reset_epoch_sums(self):
+        self.ctrl_f64[4:6].zero_()
+
+    def read_ctrl(self) -> dict:
+        raw = bytes(self.ctrl.cpu().numpy().tobytes())
+        from . import Ctrl
+        c = Ctrl.from_buffer_copy(raw)
+        return {f: getattr(c, f) for f, _ in Ctrl._fields_}
+
+    # ---- calls ------------------------------------------------------------------
+    def sync_shadow(self):
+        check(lib.inf_sync_shadow(self.handle, stream_handle()), "sync_shadow")
+
+    def set_adam(self, beta1: float, beta2: float, eps: float):
+        check(lib.inf_plan_set_adam(self.handle, beta1, beta2, eps), "set_adam")
+
+    def make_batch(self, *, features=None, rgb=None, source=None, ray_idx=None, offset=0, batch=None, loss_count=0,
+                   offset_from_ctrl=False, loss=None) -> Batch:
+        b = Batch()
+        if features is not None:
+            require_hip(features)
+            if features.dtype != torch.float32 or features.dim() != 2 or features.stride(1) != 1:
+                raise ValueError("features must be a row-major fp32 [B, k] tensor")
+            if features.shape[1] != self.desc.in_dim:
+                raise ValueError(f"features have {features.shape[1]} columns, model expects {self.desc.in_dim}")
+            b.features = features.data_ptr()
+            b.ld_features = features.stride(0)
+            b.batch = features.shape[0] if batch is None else batch
+            if rgb is not None:
+                require_hip(rgb)
+                if rgb.dtype != torch.float32 or not rgb.is_contiguous() or rgb.shape != (b.batch, 3):
+                    raise ValueError("targets must be a contiguous fp32 [B, 3] tensor")
+                b.rgb = rgb.data_ptr()
+        else:
+            src = source
+            T = src.table_for(self)
+            b.table = T.data_ptr()
+            b.table_dtype = dtype_code(T)
+            b.num_vertices = T.shape[0]
+            b.vids = src.vids32.data_ptr()
+            b.vid_dtype = DTYPE_I32
+            b.bary = src.bary.data_ptr()
+            b.rgb = src.rgbs.data_ptr() if src.rgbs is not None else None
+            if ray_idx is not None:
+                b.ray_idx = ray_idx.data_ptr()
+                b.idx_dtype = dtype_code(ray_idx)
+            b.idx_offset = int(offset)
+            b.offset_from_ctrl = 1 if offset_from_ctrl else 0
+            b.batch = int(batch)
+        b.loss_count = int(loss_count)
+        b.loss = -1 if loss is None else LOSS_CODES[loss]
+        if b.batch < 1 or b.batch > self.max_batch:
+            raise ValueError(f"batch of {b.batch} rays outside this plan's range 1..{self.max_batch}")
+        return b
+
+    def forward(self, b: Batch, pred: torch.Tensor, save: bool):
+        check(lib.inf_forward(self.handle, ctypes.byref(b), ptr(pred), 1 if save else 0, stream_handle()), "forward")
+
+    def backward(self, dpred: torch.Tensor, grads: torch.Tensor):
+        check(lib.inf_backward(self.handle, ptr(dpred), ptr(grads), stream_handle()), "backward")
+
+    def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool):
+        check(lib.inf_train_step(self.handle, ctypes.byref(b), ptr(pred), 1 if apply_adam else 0, stream_handle()),
+              "train_step")
+
+    def adam(self, step: int = 0, lr: float = 0.0):
+        check(lib.inf_adam(self.handle, int(step), float(lr), stream_handle()), "adam")
+
+    def render(self, b: Batch, hit: torch.Tensor, pixel_map: torch.Tensor | None, img: torch.Tensor):
+        check(lib.inf_render(self.handle, ctypes.byref(b), ptr(hit), ptr(pixel_map), ptr(img), stream_handle()),
+              "render")
+
+    def ctrl_advance(self):
+        check(lib.inf_ctrl_advance(self.handle, stream_handle()), "ctrl_advance")
+
+
+class RaySource:
+    """Device-resident rays + eigenfunction table (ray_dataloader.py:58-98 moves the same
+    arrays to the device once).  Keeps int32 vertex ids and packed GEMM-dtype tables."""
+
+    def __init__(self, E: torch.Tensor, vids: torch.Tensor, bary: torch.Tensor, rgbs: torch.Tensor | None):
+        require_hip(E, vids, bary, rgbs)
+        self.E = E
+        self.vids = vids
+        V = E.shape[0]
+        if vids.numel() and (int(vids.min()) < 0 or int(vids.max()) >= V):
+            raise ValueError("vertex id out of range of the eigenfunction table")
+        self.vids32 = vids.to(torch.int32).contiguous()
+        self.bary = bary.to(torch.float32).contiguous()
+        self.rgbs = None if rgbs is None else rgbs.to(torch.float32).contiguous()
+        self._tables = {}
+
+    def table_for(self, plan: Plan) -> torch.Tensor:
+        key = (plan.in_pad, plan.gemm_dtype)
+        T = self._tables.get(key)
+        if T is None:
+            if self.E.shape[1] != plan.desc.in_dim:
+                raise ValueError(f"table has {self.E.shape[1]} columns, model expects {plan.desc.in_dim}")
+            T = pack_table(self.E, plan.in_pad, plan.gemm_dtype)
+            self._tables[key] = T
+        return T

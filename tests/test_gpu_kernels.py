@@ -1,0 +1,214 @@
+"""GPU parity of the HIP kernels against the CPU oracle and the reference goldens.
+
+Calls go through the C ABI (inf_hip) directly; the host mirror modules are tested in
+test_gpu_host.py.  Tolerances:
+  fp32 mode: predicted RGB within 1e-5 abs (the bar is 1e-4, north_star), gradients
+             within 1e-4 relative to the largest element, Adam states within 1e-5;
+  bf16 mode: predicted RGB within 2e-2 abs (bf16 operands, fp32 accumulation).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import inf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CFG = {"A": (64, 128, 4, 2), "R": (1023, 128, 6, 3), "B": (1024, 256, 8, 4)}
+
+
+def rt():
+    from inf_hip import runtime
+    return runtime
+
+
+def weights(d, prefix="w:"):
+    return {k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)}
+
+
+def arena_from(w, L, s, dev="cuda"):
+    return torch.cat([torch.from_numpy(np.ascontiguousarray(w[n])).reshape(-1) for n in O.layer_names(L, s)]).to(dev)
+
+
+def arena_to_dict(arena, w_like, L, s):
+    out, off = {}, 0
+    a = arena.detach().cpu().numpy()
+    for n in O.layer_names(L, s):
+        sz = w_like[n].size
+        out[n] = a[off:off + sz].reshape(w_like[n].shape)
+        off += sz
+    return out
+
+
+def make_plan(name, mode="fp32", loss="L2", max_batch=64, w=None, adam=False):
+    k, H, L, s = CFG[name]
+    if w is None:
+        w = weights(golden(f"g2_forward_{name}.npz"))
+    params = arena_from(w, L, s)
+    kw = {}
+    if adam:
+        kw = dict(grads=torch.zeros_like(params), exp_avg=torch.zeros_like(params), exp_avg_sq=torch.zeros_like(params))
+    plan = rt().Plan(k, H, L, s, mode, loss, max_batch, params, **kw)
+    return plan, params, w
+
+
+def test_library_exports():
+    import inf_hip
+    for name in inf_hip.EXPORTED:
+        assert hasattr(inf_hip.lib, name)
+
+
+@pytest.mark.parametrize("k", [37, 64, 1023, 1024])
+def test_gather_golden(k):
+    d = golden(f"g1_gather_k{k}.npz")
+    E = torch.from_numpy(d["E"]).cuda()
+    out = rt().gather(E, torch.from_numpy(d["vids"]).cuda(), torch.from_numpy(d["bary"]).cuda())
+    np.testing.assert_allclose(out.cpu().numpy(), d["out"], atol=1e-6, rtol=0)
+
+
+def test_gather_bf16_table_and_index():
+    rng = np.random.default_rng(0)
+    V, k, N = 1000, 256, 3000
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32)).cuda()
+    vids = torch.from_numpy(rng.integers(0, V, (N, 3)).astype(np.int32)).cuda()
+    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32)).cuda()
+    perm = torch.randperm(N, device="cuda")
+    out = rt().gather(E.to(torch.bfloat16), vids, bary, ray_idx=perm, offset=100, batch=1500)
+    idx = perm[100:1600].cpu().numpy()
+    ref = O.gather(E.to(torch.bfloat16).float().cpu().numpy(), vids.cpu().numpy()[idx], bary.cpu().numpy()[idx])
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["A", "R", "B"])
+def test_forward_fp32_golden(name):
+    d = golden(f"g2_forward_{name}.npz")
+    plan, _, _ = make_plan(name)
+    feats = torch.from_numpy(d["features"]).cuda()
+    pred = torch.empty((feats.shape[0], 3), device="cuda")
+    plan.forward(plan.make_batch(features=feats), pred, save=False)
+    err = np.abs(pred.cpu().numpy() - d["pred"]).max()
+    assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("name", ["A", "R", "B"])
+def test_forward_bf16(name):
+    d = golden(f"g2_forward_{name}.npz")
+    plan, _, _ = make_plan(name, mode="bf16")
+    feats = torch.from_numpy(d["features"]).cuda()
+    pred = torch.empty((feats.shape[0], 3), device="cuda")
+    plan.forward(plan.make_batch(features=feats), pred, save=False)
+    err = np.abs(pred.cpu().numpy() - d["pred"]).max()
+    assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1"), ("R", "L2"),
+                                       ("B", "L2")])
+def test_backward_grads_golden(name, loss):
+    """Autograd-path backward (inf_backward) against the reference's own grads."""
+    d = golden(f"g3_step_{name}_{loss}.npz")
+    k, H, L, s = CFG[name]
+    plan, _, w = make_plan(name, loss=loss)
+    feats = torch.from_numpy(d["features"]).cuda()
+    pred = torch.empty((feats.shape[0], 3), device="cuda")
+    plan.forward(plan.make_batch(features=feats), pred, save=True)
+    p = pred.cpu().numpy()
+    np.testing.assert_allclose(p, d["pred"], atol=1e-5)
+    dpred = torch.from_numpy(O.loss_grad(p, d["rgb"], loss)).cuda()
+    grads = torch.empty(plan.info.num_params, device="cuda")
+    plan.backward(dpred, grads)
+    g = arena_to_dict(grads, w, L, s)
+    for n in O.layer_names(L, s):
+        ref = d["g:" + n]
+        scale = max(np.abs(ref).max(), 1e-12)
+        err = np.abs(g[n] - ref).max() / scale
+        assert err < 1e-4, (n, err)
+
+
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1")])
+def test_fused_train_step_golden(name, loss):
+    """inf_train_step (gather-free features form) + Adam vs the reference's step-1 weights."""
+    d = golden(f"g3_step_{name}_{loss}.npz")
+    k, H, L, s = CFG[name]
+    plan, params, w = make_plan(name, loss=loss, adam=True)
+    plan.set_lr(1e-4)
+    feats = torch.from_numpy(d["features"]).cuda()
+    rgb = torch.from_numpy(d["rgb"]).cuda()
+    pred = torch.empty((feats.shape[0], 3), device="cuda")
+    plan.train_step(plan.make_batch(features=feats, rgb=rgb), pred, apply_adam=True)
+    c = plan.read_ctrl()
+    assert c["step"] == 1
+    assert abs(c["loss_sum"] / (3 * feats.shape[0]) - float(d["loss"])) < 1e-6
+    np.testing.assert_allclose(pred.cpu().numpy(), d["pred"], atol=1e-5)
+    w1 = arena_to_dict(params, w, L, s)
+    for n in O.layer_names(L, s):
+        np.testing.assert_allclose(w1[n], d["w1:" + n], atol=2e-6, err_msg=n)
+
+
+@pytest.mark.parametrize("tag,name,L,s", [("A_L2", "A", 4, 2), ("A_cauchy", "A", 4, 2), ("R_L1", "R", 6, 3)])
+def test_adam20_golden(tag, name, L, s):
+    d = golden(f"g4_adam20_{tag}.npz")
+    loss = tag.split("_")[1]
+    plan, params, w = make_plan(name, loss=loss, adam=True)
+    plan.set_lr(float(d["lr"]))
+    for i in range(d["features"].shape[0]):
+        feats = torch.from_numpy(d["features"][i]).cuda()
+        rgb = torch.from_numpy(d["rgb"][i]).cuda()
+        plan.train_step(plan.make_batch(features=feats, rgb=rgb), None, apply_adam=True)
+        c = plan.read_ctrl()
+        assert abs(c["loss_sum"] / (3 * feats.shape[0]) - float(d["losses"][i])) < 2e-5
+    w20 = arena_to_dict(params, w, L, s)
+    m = arena_to_dict(plan.exp_avg, w, L, s)
+    v = arena_to_dict(plan.exp_avg_sq, w, L, s)
+    for n in O.layer_names(L, s):
+        np.testing.assert_allclose(w20[n], d["w20:" + n], atol=5e-5, err_msg=n)
+        np.testing.assert_allclose(m[n], d["m:" + n], atol=1e-5, err_msg=n)
+        np.testing.assert_allclose(v[n], d["v:" + n], rtol=1e-3, atol=1e-10, err_msg=n)
+
+
+def test_train_step_rays_matches_oracle():
+    """Fused gather + step on device-resident rays (ray-index form) vs the oracle."""
+    rng = np.random.default_rng(11)
+    k, H, L, s = CFG["B"]
+    w0 = weights(golden("g2_forward_B.npz"))
+    V, N, B = 3000, 8192, 1024
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (N, 3))
+    bary = rng.dirichlet([1, 1, 1], N).astype(np.float32)
+    rgb = rng.random((N, 3)).astype(np.float32)
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda())
+    plan, params, w = make_plan("B", max_batch=B, adam=True)
+    plan.set_lr(1e-4)
+    perm = torch.randperm(N, device="cuda")
+    tr = O.OracleTrainer(w0, L, s, 1e-4, "L2")
+    pidx = perm.cpu().numpy()
+    for step in range(3):
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, ray_idx=perm, offset=step * B, batch=B), pred, apply_adam=True)
+        idx = pidx[step * B:(step + 1) * B]
+        loss, p_ref, _ = tr.step(O.gather(E, vids[idx], bary[idx]), rgb[idx])
+        np.testing.assert_allclose(pred.cpu().numpy(), p_ref, atol=1e-5)
+        assert abs(plan.read_ctrl()["loss_sum"] / (3 * B) - loss) < 1e-6
+    got = arena_to_dict(params, w, L, s)
+    for n in O.layer_names(L, s):
+        np.testing.assert_allclose(got[n], tr.w[n], atol=5e-6, err_msg=n)
+
+
+def test_render_golden():
+    d = golden("g7_render.npz")
+    plan, _, _ = make_plan("A", max_batch=1024)
+    H, W = int(d["H"]), int(d["W"])
+    E = torch.from_numpy(d["E"]).cuda()
+    for tag in ("full", "mask"):
+        vids = torch.from_numpy(d[f"vids_{tag}"]).cuda()
+        bary = torch.from_numpy(d[f"bary_{tag}"]).cuda()
+        src = rt().RaySource(E, vids, bary, None)
+        hit = torch.from_numpy(d[f"hit_{tag}"]).cuda()
+        img = torch.ones((H * W, 3), device="cuda")
+        pmap = None
+        if tag == "mask":
+            pmap = torch.nonzero(torch.from_numpy(d["obj_mask"]).cuda()).reshape(-1)
+        plan.render(plan.make_batch(source=src, batch=hit.shape[0]), hit, pmap, img)
+        np.testing.assert_allclose(img.reshape(H, W, 3).cpu().numpy(), d[f"img_{tag}"], atol=1e-5)
