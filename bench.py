@@ -1,0 +1,358 @@
+#!/usr/bin/env python
+"""Benchmark of the intrinsic-neural-fields hot path on MI355X.
+
+Metric (BASELINE.json): training rays/s (+ render pixels/s) of the k=1024, 8x256-MLP
+TextureField (skip 4, L2 loss, Adam lr 1e-4), bf16 MFMA with fp32 master weights.
+A step = one fused training step over one batch of rays resident in HBM:
+gather -> forward -> loss -> backward -> Adam (+ RCCL all-reduce of the gradient when
+N > 1).  Synthetic data (no dataset in the container): table E = randn(V, k) with the
+reference's per-column (max - min) rescale, uniform vertex ids, Dirichlet(1,1,1)
+barycentrics, U[0,1) colours.  Weak scaling: `--batch` rays per GPU per step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--mode bf16|fp32]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "intrinsic-neural-fields_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK = 8000.0  # GB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096, help="rays per GPU per step (reference batch_size 4096)")
+    ap.add_argument("--mode", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--layers", type=int, default=8)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--skip", type=int, default=4)
+    ap.add_argument("--verts", type=int, default=50000)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-render", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--extra-batches", default="65536", help="comma list of extra per-GPU batch sizes to report")
+    return ap.parse_args()
+
+
+def synthetic(V, k, N, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    E = torch.randn((V, k), generator=g)
+    E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
+    vids = torch.randint(0, V, (N, 3), generator=g)
+    u = torch.rand((N, 3), generator=g).clamp_min(1e-12)
+    bary = -torch.log(u)
+    bary = bary / bary.sum(1, keepdim=True)
+    rgb = torch.rand((N, 3), generator=g)
+    return E.to(device), vids.to(device), bary.to(device), rgb.to(device)
+
+
+def build_model(args, device):
+    import model as M
+    torch.manual_seed(0)
+    cfg = {"k": args.k, "num_layers": args.layers, "mlp_hidden_dim": args.hidden, "skip_layer_idx": args.skip,
+           "kernels": {"mode": args.mode}}
+    m = M.make_model(cfg).to(device)
+    m.kernel_mode = args.mode
+    return m
+
+
+class Trainer:
+    """Graph-captured fused steps over one RaySource (one rank)."""
+
+    def __init__(self, args, device, B, rank, world):
+        from inf_hip import runtime
+        self.args, self.B, self.world = args, B, world
+        self.model = build_model(args, device)
+        rt = self.model.hip_runtime()
+        rt.ensure_optimizer_arenas()
+        self.plan = runtime.Plan(args.k, args.hidden, args.layers, args.skip, args.mode, "L2", B, rt.arena,
+                                 rt.grads, rt.exp_avg, rt.exp_avg_sq)
+        self.plan.set_lr(1e-4)
+        self.nb = 32
+        self.N = self.nb * B
+        E, vids, bary, rgb = synthetic(args.verts, args.k, self.N, seed=1 + rank, device=device)
+        self.src = runtime.RaySource(E, vids, bary, rgb)
+        self.perm = torch.randperm(self.N, device=device)
+        self.batch = self.plan.make_batch(source=self.src, ray_idx=self.perm, offset=0, batch=B,
+                                          offset_from_ctrl=True, loss_count=3 * B * world)
+        self.graphs = None
+        self.i = 0
+
+    def _launch(self):
+        if self.world == 1:
+            self.plan.train_step(self.batch, None, apply_adam=True)
+            self.plan.ctrl_advance()
+        else:
+            self.plan.train_step(self.batch, None, apply_adam=False)
+
+    def capture(self):
+        # one eager step: settles the plan's tables before capture
+        self.step_eager()
+        if self.args.no_graph:
+            return
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, stream=s):
+                self._launch()
+            g2 = None
+            if self.world > 1:
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2, stream=s):
+                    self.plan.adam(0, 0.0)
+                    self.plan.ctrl_advance()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graphs = (g1, g2)
+        self.plan.set_batch_index(0)
+        self.i = 0
+
+    def _wrap(self):
+        if self.i == self.nb:
+            self.plan.set_batch_index(0)
+            self.i = 0
+
+    def step_eager(self):
+        self._wrap()
+        self._launch()
+        if self.world > 1:
+            torch.distributed.all_reduce(self.plan.grads)
+            self.plan.adam(0, 0.0)
+            self.plan.ctrl_advance()
+        self.i += 1
+
+    def step(self):
+        if self.graphs is None:
+            return self.step_eager()
+        self._wrap()
+        g1, g2 = self.graphs
+        g1.replay()
+        if g2 is not None:
+            torch.distributed.all_reduce(self.plan.grads)
+            g2.replay()
+        self.i += 1
+
+
+def time_steps(tr, steps, warmup, world):
+    for _ in range(warmup):
+        tr.step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        tr.step()
+    e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    ms = e0.elapsed_time(e1)
+    t = torch.tensor([ms, wall * 1e3], device="cuda")
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t[0]) / steps, float(t[1]) / steps
+
+
+def time_stage(plan, stage, reps=20, batch=None, layer=0):
+    plan.run_stage(stage, layer, batch)  # warm
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        flops, byts = plan.run_stage(stage, layer, batch)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, flops, byts
+
+
+def render_bench(args, device):
+    """Forward-only render slice (renderer.py:112-146) of a 2048x2048 frame at a 50 % hit
+    rate over a V=400k table (config E): gather + MLP + placement into the image."""
+    from inf_hip import runtime
+    H = W = 2048
+    V = 400_000
+    m = build_model(args, device)
+    rt = m.hip_runtime()
+    nhit = H * W // 2
+    chunk = 1 << 18
+    plan = runtime.Plan(args.k, args.hidden, args.layers, args.skip, args.mode, "L2", chunk, rt.arena)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    E = torch.randn((V, args.k), generator=g)
+    E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
+    vids = torch.randint(0, V, (nhit, 3), generator=g).to(device)
+    u = torch.rand((nhit, 3), generator=g).clamp_min(1e-12)
+    bary = (-torch.log(u))
+    bary = (bary / bary.sum(1, keepdim=True)).to(device)
+    src = runtime.RaySource(E.to(device), vids, bary, None)
+    del E
+    hit = torch.randperm(H * W, device=device)[:nhit]
+    img = torch.empty((H * W, 3), device=device)
+    batches = [plan.make_batch(source=src, offset=o, batch=min(chunk, nhit - o)) for o in range(0, nhit, chunk)]
+
+    def frame():
+        img.fill_(1.0)
+        for o, b in zip(range(0, nhit, chunk), batches):
+            plan.render(b, hit[o:o + b.batch], None, img)
+
+    frame()
+    torch.cuda.synchronize()
+    reps = 5
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        frame()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
+            "hits": nhit, "verts": V, "chunk": chunk}
+
+
+def cpu_baseline(args):
+    """The CPU oracle (numpy fp32 restatement of the reference step, oracle/inf_oracle.py)
+    on this host's cores, config B at batch 4096: bounded sample of ~cpu_seconds."""
+    from oracle import inf_oracle as O
+    cores = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    rng = np.random.default_rng(0)
+    k, H, L, s, B, V = args.k, args.hidden, args.layers, args.skip, 4096, 20000
+    names = O.layer_names(L, s)
+    torch.manual_seed(0)
+    import model as M
+    m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s})
+    w = {n: p.detach().numpy().copy() for n, p in m.named_parameters()}
+    assert set(w) == set(names)
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    tr = O.OracleTrainer(w, L, s, 1e-4, "L2")
+
+    def one():
+        vids = rng.integers(0, V, (B, 3))
+        bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+        rgb = rng.random((B, 3)).astype(np.float32)
+        tr.step(O.gather(E, vids, bary), rgb)
+
+    one()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < args.cpu_seconds and n < 200:
+        one()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * B / dt, "unit": "rays/s", "cores": cores, "kind": "port",
+            "sample": f"{n} oracle train steps (numpy fp32) of {B} rays, k={k} {L}x{H} skip {s}, V={V}, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    tr = Trainer(args, device, args.batch, rank, world)
+    tr.capture()
+    ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
+    value = world * args.batch / (ms * 1e-3)
+
+    from inf_hip import STAGE_DW_GEMM, STAGE_FWD_GEMM, STAGE_GATHER
+    # dominant kernel: the grouped split-K weight-gradient GEMM (one launch, all layers)
+    dw_ms, dw_flops, dw_bytes = time_stage(tr.plan, STAGE_DW_GEMM)
+    fwd_ms, fwd_flops, _ = time_stage(tr.plan, STAGE_FWD_GEMM, layer=1)
+    ga_ms, _, ga_bytes = time_stage(tr.plan, STAGE_GATHER, batch=tr.batch)
+    achieved = dw_flops / (dw_ms * 1e-3) / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "dw_gemm_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(f"{args.mode}_B{args.batch}")
+        except Exception:
+            traffic = None
+
+    extra = {}
+    for eb in [int(x) for x in args.extra_batches.split(",") if x]:
+        if eb == args.batch:
+            continue
+        del tr
+        torch.cuda.empty_cache()
+        tr2 = Trainer(args, device, eb, rank, world)
+        tr2.capture()
+        ms2, _ = time_steps(tr2, max(10, args.steps // 8), 3, world)
+        d_ms, d_fl, _ = time_stage(tr2.plan, STAGE_DW_GEMM, reps=5)
+        extra[str(eb)] = {"value": world * eb / (ms2 * 1e-3), "ms_per_step": ms2,
+                          "dw_gemm_tflops": d_fl / (d_ms * 1e-3) / 1e12}
+        tr = tr2
+
+    render = None
+    if not args.no_render and rank == 0:
+        del tr
+        torch.cuda.empty_cache()
+        render = render_bench(args, device)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        L, H, k = args.layers, args.hidden, args.k
+        flops_ray = 2 * (2 * (2 * k * H + (L - 2) * H * H + 3 * H) + (L - 2) * H * H + 3 * H)
+        line = {
+            "metric": "training rays/sec (k=1024, 8x256 MLP)",
+            "value": value,
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.mode,
+            "data": "synthetic (randn table with reference column rescale, uniform vertex ids, Dirichlet "
+                    "barycentrics, U[0,1) colours); seed-0 reference init",
+            "config": {"workload": f"cat texture_reconstruction k={k} {L}x{H} MLP skip {args.skip}, L2, Adam "
+                                   f"lr 1e-4, fused gather+fwd+bwd+Adam step",
+                       "rays_per_gpu_per_step": args.batch, "global_batch": args.batch * world,
+                       "verts": args.verts, "parallelism": f"dp{world}", "graph": not args.no_graph},
+            "model_tflops": flops_ray * value / 1e12,
+            "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel (grouped split-K weight-gradient GEMM)",
+                         "achieved": achieved, "peak": PEAK[args.mode], "unit": "TFLOP/s",
+                         "frac": achieved / PEAK[args.mode], "traffic": traffic,
+                         "avg_ms": dw_ms, "flops_per_launch": dw_flops},
+            "stages": {"fwd_gemm_layer1_ms": fwd_ms, "fwd_gemm_layer1_tflops": fwd_flops / (fwd_ms * 1e-3) / 1e12,
+                       "gather_ms": ga_ms, "gather_gbs": ga_bytes / (ga_ms * 1e-3) / 1e9,
+                       "gather_hbm_frac": ga_bytes / (ga_ms * 1e-3) / 1e9 / HBM_PEAK,
+                       "host_wall_ms_per_step": wall_ms},
+            "large_batch": extra,
+            "render": render,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -166,6 +166,18 @@ int inf_adam(inf_plan* plan, int step, float lr, inf_stream_t stream);
 int inf_render(inf_plan* plan, const inf_batch* batch, const int64_t* hit, const int64_t* pixel_map,
                float* img, inf_stream_t stream);
 
+/* Diagnostics: re-launch one stage of the last saved training step on its saved
+ * inputs (used by bench.py to time a single kernel with HIP events).  Stages:
+ *   INF_STAGE_GATHER   - the gather kernel (X, X^T)
+ *   INF_STAGE_FWD_GEMM - the forward GEMM of hidden layer `layer` (1..L-2)
+ *   INF_STAGE_DW_GEMM  - the grouped split-K weight-gradient GEMM
+ *   INF_STAGE_UPDATE   - the slab-reduction/Adam/packed-weight launch (reduce only:
+ *                        parameters are not modified)
+ * *flops / *bytes receive the stage's algorithmic work per launch (unpadded). */
+enum { INF_STAGE_GATHER = 0, INF_STAGE_FWD_GEMM = 1, INF_STAGE_DW_GEMM = 2, INF_STAGE_UPDATE = 3 };
+int inf_run_stage(inf_plan* plan, const inf_batch* batch, int stage, int layer, double* flops, double* bytes,
+                  inf_stream_t stream);
+
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);
 

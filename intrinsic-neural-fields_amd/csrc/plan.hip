@@ -233,10 +233,20 @@ int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStrea
                               x0t, Bp, st);
 }
 
+int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t st);
+
 int run_forward_layers(inf_plan* p, int Bp, bool transposed, hipStream_t st) {
+  for (int l = 0; l < p->L - 1; ++l) {
+    int rc = run_forward_layer(p, Bp, transposed, l, st);
+    if (rc) return rc;
+  }
+  return INF_OK;
+}
+
+int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t st) {
   const int H = p->H;
   const GemmTile tile = pick_tile(p, Bp, H);
-  for (int l = 0; l < p->L - 1; ++l) {
+  {
     GemmBatch gb;
     std::memset(&gb, 0, sizeof(gb));
     gb.nprob = 1;
@@ -275,9 +285,11 @@ int run_forward_layers(inf_plan* p, int Bp, bool transposed, hipStream_t st) {
   return INF_OK;
 }
 
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st);
+
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
-  const int H = p->H, L = p->L, s = p->s;
+  const int H = p->H, L = p->L;
   const GemmTile tile = pick_tile(p, Bp, H);
   for (int l = L - 2; l >= 1; --l) {
     GemmBatch gb;
@@ -305,6 +317,11 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
     int rc = launch_gemm(gb, p->mode, tile, st);
     if (rc) return rc;
   }
+  return run_weight_grads(p, Bp, st);
+}
+
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st) {
+  const int H = p->H, s = p->s;
   // weight gradients: one grouped split-K launch (chunks of GEMM_MAX_PROBLEMS)
   std::vector<GemmProblem> probs;
   for (size_t i = 0; i < p->segs.size(); ++i) {
@@ -689,6 +706,61 @@ int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const in
   }
   INF_CHECK_ARG(hit != nullptr && img != nullptr, "render: hit indices and image required");
   return forward_impl(p, batch, nullptr, false, false, hit, pixel_map, img, (hipStream_t)stream);
+}
+
+int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double* flops, double* bytes,
+                  inf_stream_t stream) {
+  if (p == nullptr || !p->bound || !p->saved) {
+    set_error("run_stage needs a saved training step");
+    return INF_ERR_STATE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int Bp = p->saved_bp;
+  const double B = p->saved_batch, H = p->H, k = p->d.in_dim;
+  const double e = (double)p->esz;
+  double f = 0, by = 0;
+  int rc = INF_OK;
+  switch (stage) {
+    case INF_STAGE_GATHER:
+      INF_CHECK_ARG(b != nullptr && b->table != nullptr, "gather stage needs the ray batch");
+      rc = run_input(p, b, Bp, true, st);
+      f = 6.0 * B * k;
+      // three table rows per ray + ids/bary; outputs X and X^T
+      by = B * (3.0 * k * (b->table_dtype == INF_DTYPE_BF16 ? 2 : 4) + 24.0) + 2.0 * B * p->k_pad * e;
+      break;
+    case INF_STAGE_FWD_GEMM: {
+      INF_CHECK_ARG(layer >= 1 && layer <= p->L - 2, "forward stage layer must be a hidden layer");
+      rc = run_forward_layer(p, Bp, true, layer, st);
+      const double K = (layer == p->s) ? H + k : H;
+      f = 2.0 * B * H * K;
+      by = B * (K + 2.0 * H) * e;
+      break;
+    }
+    case INF_STAGE_DW_GEMM: {
+      rc = run_weight_grads(p, Bp, st);
+      for (const auto& g : p->segs)
+        if (g.gemm) {
+          f += 2.0 * g.R * g.C * B;
+          by += (double)B * (g.R + g.C) * e + 4.0 * g.R * g.C * p->dw_splits;
+        }
+      break;
+    }
+    case INF_STAGE_UPDATE: {
+      if ((rc = refresh_tables(p, Bp, st))) return rc;
+      AdamArgs a = update_args(p, Bp);
+      INF_CHECK_ARG(p->grads != nullptr, "update stage needs a bound grads arena");
+      a.grad_src = GRAD_SLABS;  // reduce only into the grads arena: parameters unchanged
+      a.write_grads = 1;
+      rc = launch_update(a, p->mode, st);
+      for (const auto& g : p->segs) by += 4.0 * g.R * g.C;
+      break;
+    }
+    default:
+      INF_CHECK_ARG(false, "unknown stage");
+  }
+  if (flops) *flops = f;
+  if (bytes) *bytes = by;
+  return rc;
 }
 
 int inf_ctrl_advance(inf_plan* p, inf_stream_t stream) {

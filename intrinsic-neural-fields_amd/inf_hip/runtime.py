@@ -229,6 +229,13 @@ class Plan:
         check(lib.inf_render(self.handle, ctypes.byref(b), ptr(hit), ptr(pixel_map), ptr(img), stream_handle()),
               "render")
 
+    def run_stage(self, stage: int, layer: int = 0, b: Batch | None = None):
+        """Re-launch one stage of the last saved step; returns (flops, bytes) per launch."""
+        f, by = ctypes.c_double(), ctypes.c_double()
+        check(lib.inf_run_stage(self.handle, ctypes.byref(b) if b is not None else None, int(stage), int(layer),
+                                ctypes.byref(f), ctypes.byref(by), stream_handle()), "run_stage")
+        return f.value, by.value
+
     def ctrl_advance(self):
         check(lib.inf_ctrl_advance(self.handle, stream_handle()), "ctrl_advance")
 

@@ -1,0 +1,284 @@
+"""Host mirror of the reference model.py (TextureField + make_model).
+
+The module tree, parameter names/order and the seeded initialisation are the
+reference's (model.py:12-96 TextureField.__init__, 194-258 init_weights/make_model),
+so `state_dict()` files are interchangeable with the reference's.  The arithmetic of
+`forward` (model.py:98-112) and of its autograd backward runs in libinf_hip.so: the
+parameters live in one flat fp32 arena on the HIP device (each nn.Parameter is a view
+into it), the kernels read packed GEMM-dtype copies that are refreshed whenever a
+parameter changes, and a batch whose features were not materialised is gathered inside
+the same launch sequence (mesh.py:313-324 fused into the forward).
+
+Kernel arithmetic mode: `model_config["kernels"]["mode"]` ("fp32" exact f32 MFMA, the
+default, or "bf16" MFMA with fp32 accumulation), overridable by INF_MODE.
+"""
+from __future__ import annotations
+
+import os
+import weakref
+
+import torch
+import torch.nn as nn
+
+from layers import LinearWithConcatAndActivation
+
+RGB_COLOR_DIM = 3
+
+# arena base pointer -> runtime (lets the optimizer find the arena of its params)
+_RUNTIMES: "weakref.WeakValueDictionary[int, _Runtime]" = weakref.WeakValueDictionary()
+
+
+def _hip():
+    from inf_hip import runtime  # raises if the HIP library is missing: no fallback
+    return runtime
+
+
+class _Runtime:
+    """Device state of one TextureField: parameter arena, optimizer arenas, plan."""
+
+    def __init__(self, module: "TextureField", device: torch.device, arena: torch.Tensor):
+        self.module_ref = weakref.ref(module)
+        self.device = device
+        self.arena = arena
+        self.grads = None
+        self.exp_avg = None
+        self.exp_avg_sq = None
+        self.plan = None
+        self.synced = None          # parameter versions the packed weights reflect
+        self.gen = 0                # id of the last forward that saved activations
+        self.saved_gen = None
+        self.dev_step = None        # value of ctrl.step as last set/advanced
+        self.dev_lr = None
+        _RUNTIMES[arena.data_ptr()] = self
+
+    def ensure_optimizer_arenas(self):
+        if self.exp_avg is None:
+            self.grads = torch.zeros_like(self.arena)
+            self.exp_avg = torch.zeros_like(self.arena)
+            self.exp_avg_sq = torch.zeros_like(self.arena)
+            if self.plan is not None:
+                self.plan.bind(self.grads, self.exp_avg, self.exp_avg_sq)
+
+
+class TextureField(nn.Module):
+    """Reference model.py:12-112.  Supported: feature strategy "efuncs", ReLU,
+    batchnorm=False, sigmoid RGB head (every intrinsic config in configs/)."""
+
+    def __init__(self, num_layers, in_dim, hidden_dim, skip_layer_idx, input_feature_embed=None, embed_dim=None,
+                 embed_include_input=True, embed_std=1., return_rgb=True, out_dim=RGB_COLOR_DIM, batchnorm=False,
+                 activation=nn.ReLU):
+        super().__init__()
+        assert num_layers > 2 and 0 < skip_layer_idx and skip_layer_idx < num_layers - 1
+        if input_feature_embed in ("ff", "rff", "xyz"):
+            raise NotImplementedError(f"feature strategy '{input_feature_embed}' (extrinsic baselines) is outside "
+                                      "this build's hot path; use 'efuncs'")
+        if batchnorm:
+            raise NotImplementedError("batchnorm=True is not used by any intrinsic config and is not implemented")
+        if activation is not nn.ReLU:
+            raise NotImplementedError("only the ReLU activation is implemented")
+        if not return_rgb or out_dim != RGB_COLOR_DIM:
+            raise NotImplementedError("only the sigmoid RGB head is implemented")
+        self.skip_layer_idx = skip_layer_idx
+        self.input_feature_embed = input_feature_embed
+        self.embedding = None
+        self.num_layers = num_layers
+        self.in_dim = in_dim
+        self.hidden_dim = hidden_dim
+
+        layers = [nn.Sequential(nn.Linear(in_dim, hidden_dim), activation())]
+        for i in range(1, num_layers - 1):
+            if i == skip_layer_idx:
+                layers.append(LinearWithConcatAndActivation(hidden_dim, in_dim, hidden_dim, batchnorm=batchnorm,
+                                                            activation=activation))
+            else:
+                layers.append(nn.Sequential(nn.Linear(hidden_dim, hidden_dim), activation()))
+        layers.append(nn.Sequential(nn.Linear(hidden_dim, out_dim), nn.Sigmoid()))
+        self.layers = nn.ModuleList(layers)
+
+        self.kernel_mode = os.environ.get("INF_MODE", "fp32")
+        self.max_batch_hint = 4096
+        self._rt: _Runtime | None = None
+
+    # ---- device binding ----------------------------------------------------------
+    def _layout(self):
+        params = list(self.parameters())
+        offs, off = [], 0
+        for p in params:
+            offs.append(off)
+            off += p.numel()
+        return params, offs, off
+
+    def hip_runtime(self) -> _Runtime:
+        """Bind the parameters to a flat arena on their HIP device (once; re-binds after
+        .to(), load_state_dict(assign=True) or any other re-pointing of .data)."""
+        params, offs, P = self._layout()
+        dev = params[0].device
+        if dev.type != "cuda" or any(p.device != dev for p in params):
+            raise RuntimeError("TextureField runs on one MI355X (HIP) device; move it with .to('cuda'). "
+                               "There is no CPU fallback.")
+        rt = self._rt
+        if rt is None or rt.device != dev or rt.arena.numel() != P:
+            with torch.no_grad():
+                arena = torch.empty(P, dtype=torch.float32, device=dev)
+                for p, o in zip(params, offs):
+                    arena[o:o + p.numel()].copy_(p.detach().reshape(-1))
+            rt = _Runtime(self, dev, arena)
+            self._rt = rt
+        base = rt.arena.data_ptr()
+        for p, o in zip(params, offs):
+            if p.data_ptr() != base + 4 * o or not p.is_contiguous() or p.dtype != torch.float32:
+                with torch.no_grad():
+                    rt.arena[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = rt.arena[o:o + p.numel()].view(p.shape)
+                rt.synced = None
+        return rt
+
+    def _versions(self):
+        return tuple(p._version for p in self.parameters())
+
+    def hip_plan(self, batch: int, loss: str = "L2"):
+        rt = self.hip_runtime()
+        plan = rt.plan
+        if plan is None or batch > plan.max_batch or plan.mode != self.kernel_mode:
+            mb = max(batch, self.max_batch_hint, 2 * plan.max_batch if plan is not None and batch > plan.max_batch
+                     else 0)
+            rt.plan = None  # free the old workspace first
+            plan = _hip().Plan(self.in_dim, self.hidden_dim, self.num_layers, self.skip_layer_idx,
+                               self.kernel_mode, loss, mb, rt.arena, rt.grads, rt.exp_avg, rt.exp_avg_sq)
+            rt.plan = plan
+            rt.synced = self._versions()
+            rt.saved_gen = None
+            rt.dev_step = 0
+            rt.dev_lr = None
+        versions = self._versions()
+        if rt.synced != versions:
+            plan.sync_shadow()
+            rt.synced = versions
+        return plan
+
+    # ---- forward (model.py:98-112) -----------------------------------------------
+    def forward(self, batch):
+        params = list(self.parameters())
+        lazy = getattr(batch, "is_lazy_rays", None)
+        if lazy is not None and lazy():
+            feats, rays = None, batch.ray_args()
+            B = rays["batch"]
+        else:
+            feats = batch["eigenfunctions"]
+            if not feats.is_cuda:
+                raise RuntimeError("TextureField runs on MI355X (HIP) devices only; features are on "
+                                   f"{feats.device}. There is no CPU fallback.")
+            if feats.requires_grad:
+                raise NotImplementedError("gradients w.r.t. the eigenfunction features are not needed by the "
+                                          "reference (they are data) and are not implemented")
+            feats = feats.to(torch.float32).contiguous()
+            rays, B = None, feats.shape[0]
+        return _TextureFieldFn.apply(self, feats, rays, B, *params)
+
+    # ---- fused training step (used by trainer.Trainer) ------------------------------
+    def fused_train_step(self, batch, optim, loss_type: str, want_pred: bool = True, loss_count: int = 0):
+        """gather -> forward -> loss -> backward -> Adam in one launch sequence
+        (trainer.py:71-84 with the loss of config.py:113-122).  Returns pred or None."""
+        rays = batch.ray_args()
+        B = rays["batch"]
+        rt = self.hip_runtime()
+        group = optim.fused_group_for(self)
+        rt.ensure_optimizer_arenas()
+        plan = self.hip_plan(B, loss_type)
+        optim.sync_runtime_state(self, rt, plan, group)
+        pred = torch.empty((B, 3), device=rt.device) if want_pred else None
+        b = plan.make_batch(source=rays["source"], ray_idx=rays["ray_idx"], offset=rays["offset"], batch=B,
+                            loss_count=loss_count, loss=loss_type)
+        plan.train_step(b, pred, apply_adam=True)
+        rt.saved_gen = None
+        optim.after_fused_step(self, rt, group)
+        return pred
+
+
+class _TextureFieldFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, module, feats, rays, B, *params):
+        needs = any(ctx.needs_input_grad[4:])
+        plan = module.hip_plan(B)
+        rt = module._rt
+        if rays is not None:
+            b = plan.make_batch(source=rays["source"], ray_idx=rays["ray_idx"], offset=rays["offset"], batch=B)
+        else:
+            b = plan.make_batch(features=feats)
+        pred = torch.empty((B, 3), device=rt.device)
+        plan.forward(b, pred, save=needs)
+        if needs:
+            rt.gen += 1
+            rt.saved_gen = rt.gen
+            ctx.gen = rt.gen
+            ctx.module = module
+            ctx.rays = rays
+            ctx.B = B
+            ctx.plan = plan
+            ctx.shapes = [p.shape for p in params]
+            if feats is not None:
+                ctx.save_for_backward(feats)
+        else:
+            rt.saved_gen = None
+        return pred
+
+    @staticmethod
+    def backward(ctx, dpred):
+        module, plan = ctx.module, ctx.plan
+        rt = module._rt
+        if rt.plan is not plan or rt.saved_gen != ctx.gen:
+            # activations were overwritten by another forward: recompute them
+            plan = module.hip_plan(ctx.B)
+            if ctx.rays is not None:
+                r = ctx.rays
+                b = plan.make_batch(source=r["source"], ray_idx=r["ray_idx"], offset=r["offset"], batch=ctx.B)
+            else:
+                b = plan.make_batch(features=ctx.saved_tensors[0])
+            plan.forward(b, torch.empty((ctx.B, 3), device=rt.device), save=True)
+            rt.gen += 1
+            rt.saved_gen = rt.gen
+            ctx.gen = rt.gen
+        grads = torch.empty(plan.info.num_params, dtype=torch.float32, device=rt.device)
+        plan.backward(dpred.to(torch.float32).contiguous(), grads)
+        out = []
+        for off, n, shape in zip(plan.offsets, plan.numels, ctx.shapes):
+            out.append(grads[off:off + n].view(shape))
+        return (None, None, None, None, *out)
+
+
+def init_weights(m):
+    """Reference model.py:194-196."""
+    if isinstance(m, nn.Linear):
+        torch.nn.init.xavier_uniform_(m.weight.data)
+
+
+def make_model(model_config, mesh=None):
+    """Reference model.py:199-258 for the intrinsic (efuncs) configurations."""
+    view_dependence_config = model_config.get("view_dependence")
+    feature_strategy = model_config.get("feature_strategy", "efuncs")
+    if model_config.get("type") == "neutex":
+        raise NotImplementedError("the NeuTex baseline is outside this build's scope")
+    if view_dependence_config is not None:
+        raise NotImplementedError("view-dependent heads are outside this build's scope (no config uses them)")
+    if feature_strategy == "xyz":
+        in_dim = 3
+    elif isinstance(model_config["k"], int):
+        in_dim = model_config["k"]
+    else:
+        assert isinstance(model_config["k"], list)
+        in_dim = len(model_config["k"])
+    activation_fn = model_config.get("activation", "relu")
+    if activation_fn != "relu":
+        raise NotImplementedError(f"Activation function {activation_fn} not yet implemented.")
+    model = TextureField(model_config["num_layers"], in_dim, model_config["mlp_hidden_dim"],
+                         model_config["skip_layer_idx"], input_feature_embed=feature_strategy,
+                         embed_dim=model_config.get("k"),
+                         embed_include_input=model_config.get("embed_include_input", True),
+                         embed_std=model_config.get("embed_std", 1.), batchnorm=model_config.get("batchnorm", False),
+                         activation=nn.ReLU)
+    model.apply(init_weights)
+    kernels = model_config.get("kernels") or {}
+    model.kernel_mode = os.environ.get("INF_MODE", kernels.get("mode", "fp32"))
+    if kernels.get("max_batch"):
+        model.max_batch_hint = int(kernels["max_batch"])
+    return model
