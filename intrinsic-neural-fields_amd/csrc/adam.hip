@@ -53,46 +53,75 @@ __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   if (a.do_adam) __syncthreads();
 
   if (seg.matrix) {
+    // 16 elements per thread; every load of a phase is issued before its first use so
+    // one thread keeps 16 (slab sum) or 48 (Adam state) loads in flight
     const int r0 = item.r0, c0 = item.c0;
-#pragma unroll 4
+    const int c = tid & 63;
+    const int rb = tid >> 6;  // rows rb, rb+4, ..., rb+60
+    const int gc = c0 + c;
+    bool ok[16];
+    int64_t e[16];
+    float w[16], g[16];
+#pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int idx = tid + 256 * i;
-      const int r = idx >> 6, c = idx & 63;
-      const int gr = r0 + r, gc = c0 + c;
-      float w = 0.f;
-      if (gr < seg.R && gc < seg.C) {
-        const int64_t e = seg.off + (int64_t)gr * seg.C + gc;
-        w = a.params[e];
-        if (a.grad_src != GRAD_NONE) {
-          float g;
-          if (a.grad_src == GRAD_FLAT) {
-            g = a.grads[e];
-          } else {
-            const float* s = seg.slab + (int64_t)gr * seg.slab_ld + gc;
-            g = s[0];
-            for (int k = 1; k < seg.nslab; ++k) g += s[k * seg.slab_stride];
-          }
-          if (a.write_grads) a.grads[e] = g;
-          if (a.do_adam) {
-            float m = a.exp_avg[e], v = a.exp_avg_sq[e];
-            adam_elem(w, m, v, g, a, sc);
-            a.params[e] = w;
-            a.exp_avg[e] = m;
-            a.exp_avg_sq[e] = v;
+      const int gr = r0 + rb + 4 * i;
+      ok[i] = gr < seg.R && gc < seg.C;
+      e[i] = seg.off + (int64_t)(ok[i] ? gr : 0) * seg.C + (ok[i] ? gc : 0);
+      w[i] = ok[i] ? a.params[e[i]] : 0.f;
+    }
+    if (a.grad_src == GRAD_FLAT) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g[i] = ok[i] ? a.grads[e[i]] : 0.f;
+    } else if (a.grad_src == GRAD_SLABS) {
+      const float* base = seg.slab + gc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g[i] = ok[i] ? base[(int64_t)(r0 + rb + 4 * i) * seg.slab_ld] : 0.f;
+#pragma unroll 1
+      for (int k = 1; k < seg.nslab; ++k) {
+        const float* sk = base + (int64_t)k * seg.slab_stride;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (ok[i]) g[i] += sk[(int64_t)(r0 + rb + 4 * i) * seg.slab_ld];
+      }
+    }
+    if (a.grad_src != GRAD_NONE) {
+      if (a.write_grads) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (ok[i]) a.grads[e[i]] = g[i];
+      }
+      if (a.do_adam) {
+        float m[16], v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          m[i] = ok[i] ? a.exp_avg[e[i]] : 0.f;
+          v[i] = ok[i] ? a.exp_avg_sq[e[i]] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (ok[i]) {
+            adam_elem(w[i], m[i], v[i], g[i], a, sc);
+            a.params[e[i]] = w[i];
+            a.exp_avg[e[i]] = m[i];
+            a.exp_avg_sq[e[i]] = v[i];
           }
         }
-        if (a.write_shadow) reinterpret_cast<T*>(seg.W)[(int64_t)gr * seg.ldw + gc] = (T)w;
       }
-      tile[c][r] = w;
     }
     if (!a.write_shadow) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = rb + 4 * i;
+      if (ok[i]) reinterpret_cast<T*>(seg.W)[(int64_t)(r0 + r) * seg.ldw + gc] = (T)w[i];
+      tile[c][r] = w[i];
+    }
     __syncthreads();
 #pragma unroll 4
     for (int i = 0; i < 16; ++i) {
       const int idx = tid + 256 * i;
-      const int c = idx >> 6, r = idx & 63;
-      const int gr = r0 + r, gc = c0 + c;
-      if (gr < seg.R && gc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gc * seg.ldwt + gr] = (T)tile[c][r];
+      const int cc = idx >> 6, r = idx & 63;
+      const int gr = r0 + r, gcc = c0 + cc;
+      if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
     }
   } else {
     // vector chunk: 8 elements x 32 lanes

@@ -1,7 +1,7 @@
 // Output layer (Linear(H,3) + Sigmoid, model.py:89-94), the training losses
 // (config.py:113-122) and the first backward stage, on the vector ALUs.
 //
-// head_fwd:  one wave per ray; lanes split the H-wide dot products, wave-reduced.
+// head_fwd:  16 lanes per ray; lanes split the H-wide dot products, shuffle-reduced.
 //            pred = sigmoid(h . W^T + b); with targets also the loss (mean over
 //            loss_count elements), dL/dpred and dz = dL/dpred * p * (1 - p); with a
 //            pixel map the colour is placed into the image (renderer.py:124-146).
@@ -17,105 +17,96 @@ namespace {
 
 constexpr float CAUCHY_C2 = (20.f / 255.f) * (20.f / 255.f);
 
-__device__ __forceinline__ float wave_sum(float x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
-
-template <typename T>
+// 16 lanes per ray (EPL = H/16 hidden units each, contiguous), 16 rays per 256-thread
+// block, one ray per lane group: every load of a ray (index, colour, activation row) is
+// issued up front, the three dot products finish with 4 xor-shuffles.
+template <typename T, int EPL>
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadFwdArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  __shared__ float red[2][16];
+  const int lane16 = threadIdx.x & 15;
+  const int grp = threadIdx.x >> 4;
+  const int b = blockIdx.x * 16 + grp;
   const int H = a.H;
-  const int epl = H >> 6;  // elements per lane (H multiple of 64, <= 512)
-  float w0[8], w1[8], w2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int kk = lane * epl + e;
-    const bool ok = e < epl;
-    w0[e] = ok ? a.W[kk] : 0.f;
-    w1[e] = ok ? a.W[H + kk] : 0.f;
-    w2[e] = ok ? a.W[2 * H + kk] : 0.f;
-  }
-  const float b0 = a.bias[0], b1 = a.bias[1], b2 = a.bias[2];
+  const bool in_rows = b < a.rows;
+  const bool valid = b < a.batch;
 
   int64_t offset = a.idx_offset;
   if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
-
-  float loss_acc = 0.f, sse_acc = 0.f;
-  const int ray0 = blockIdx.x * HEAD_RAYS_PER_BLOCK + wave * (HEAD_RAYS_PER_BLOCK / 4);
-#pragma unroll 1
-  for (int rr = 0; rr < HEAD_RAYS_PER_BLOCK / 4; ++rr) {
-    const int b = ray0 + rr;
-    if (b >= a.rows) break;
-    float z0 = 0.f, z1 = 0.f, z2 = 0.f;
-    const T* hrow = reinterpret_cast<const T*>(a.h) + (int64_t)b * a.ldh + lane * epl;
+  float tgt = 0.f;
+  if (a.rgb != nullptr && valid && lane16 < 3) {
+    const int64_t row = ray_row(a.ray_idx, a.idx_dtype, offset, b);
+    tgt = a.rgb[row * 3 + lane16];
+  }
+  float hv[EPL];
+  const T* hrow = reinterpret_cast<const T*>(a.h) + (int64_t)(in_rows ? b : 0) * a.ldh + lane16 * EPL;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (e < epl) {
-        const float hv = (float)hrow[e];
-        z0 = fmaf(hv, w0[e], z0);
-        z1 = fmaf(hv, w1[e], z1);
-        z2 = fmaf(hv, w2[e], z2);
-      }
+  for (int e = 0; e < EPL; ++e) hv[e] = (float)hrow[e];
+  float z0 = 0.f, z1 = 0.f, z2 = 0.f;
+  const float* W = a.W + lane16 * EPL;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    z0 = fmaf(hv[e], W[e], z0);
+    z1 = fmaf(hv[e], W[H + e], z1);
+    z2 = fmaf(hv[e], W[2 * H + e], z2);
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) {
+    z0 += __shfl_xor(z0, o, 16);
+    z1 += __shfl_xor(z1, o, 16);
+    z2 += __shfl_xor(z2, o, 16);
+  }
+  float lsum = 0.f, ssum = 0.f;
+  if (lane16 < 3 && in_rows) {
+    const float z = (lane16 == 0 ? z0 : (lane16 == 1 ? z1 : z2)) + a.bias[lane16];
+    const float pv = 1.f / (1.f + expf(-z));
+    if (valid && a.pred != nullptr) a.pred[(int64_t)b * 3 + lane16] = pv;
+    if (valid && a.img != nullptr) {
+      int64_t pix = a.hit[b];
+      if (a.pixel_map != nullptr) pix = a.pixel_map[pix];
+      a.img[pix * 3 + lane16] = pv;
     }
-    z0 = wave_sum(z0) + b0;
-    z1 = wave_sum(z1) + b1;
-    z2 = wave_sum(z2) + b2;
-    const float p[3] = {1.f / (1.f + expf(-z0)), 1.f / (1.f + expf(-z1)), 1.f / (1.f + expf(-z2))};
-    const bool valid = b < a.batch;
-    if (lane < 3) {
-      const float pv = p[lane];
-      if (valid && a.pred != nullptr) a.pred[(int64_t)b * 3 + lane] = pv;
-      if (valid && a.img != nullptr) {
-        int64_t pix = a.hit[b];
-        if (a.pixel_map != nullptr) pix = a.pixel_map[pix];
-        a.img[pix * 3 + lane] = pv;
-      }
-      if (a.rgb != nullptr) {
-        float dz = 0.f;
-        if (valid) {
-          const int64_t row = ray_row(a.ray_idx, a.idx_dtype, offset, b);
-          const float d = pv - a.rgb[row * 3 + lane];
-          float l, g;
-          if (a.loss == INF_LOSS_L2) {
-            l = d * d;
-            g = 2.f * d;
-          } else if (a.loss == INF_LOSS_L1) {
-            l = fabsf(d);
-            g = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-          } else {
-            const float q = d * d / CAUCHY_C2;
-            l = CAUCHY_C2 * logf(1.f + q);
-            g = 2.f * d / (1.f + q);
-          }
-          g *= a.inv_count;
-          dz = g * (1.f - pv) * pv;  // sigmoid backward (torch: grad * (1 - y) * y)
-          loss_acc += l;
-          sse_acc += d * d;
+    if (a.rgb != nullptr) {
+      float dz = 0.f;
+      if (valid) {
+        const float d = pv - tgt;
+        float l, g;
+        if (a.loss == INF_LOSS_L2) {
+          l = d * d;
+          g = 2.f * d;
+        } else if (a.loss == INF_LOSS_L1) {
+          l = fabsf(d);
+          g = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        } else {
+          const float q = d * d / CAUCHY_C2;
+          l = CAUCHY_C2 * logf(1.f + q);
+          g = 2.f * d / (1.f + q);
         }
-        a.dz[(int64_t)b * 3 + lane] = dz;
+        g *= a.inv_count;
+        dz = g * (1.f - pv) * pv;  // sigmoid backward (torch: grad * (1 - y) * y)
+        lsum = l;
+        ssum = d * d;
       }
+      a.dz[(int64_t)b * 3 + lane16] = dz;
     }
   }
   if (a.rgb != nullptr && a.ctrl != nullptr) {
-    __shared__ float red[2][4];
-    // lanes 0..2 hold partial sums; fold them into lane 0
-    float ls = loss_acc + __shfl_down(loss_acc, 1, 64) + __shfl_down(loss_acc, 2, 64);
-    float ss = sse_acc + __shfl_down(sse_acc, 1, 64) + __shfl_down(sse_acc, 2, 64);
-    if (lane == 0) {
-      red[0][wave] = ls;
-      red[1][wave] = ss;
+    // lanes 0..2 of each group hold the ray's three element losses
+    lsum += __shfl_down(lsum, 1, 16) + __shfl_down(lsum, 2, 16);
+    ssum += __shfl_down(ssum, 1, 16) + __shfl_down(ssum, 2, 16);
+    if (lane16 == 0) {
+      red[0][grp] = lsum;
+      red[1][grp] = ssum;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const double L = (double)red[0][0] + red[0][1] + red[0][2] + red[0][3];
-      const double S = (double)red[1][0] + red[1][1] + red[1][2] + red[1][3];
-      atomicAdd(&a.ctrl->loss_sum, L);
-      atomicAdd(&a.ctrl->sse_sum, S);
-      atomicAdd(&a.ctrl->epoch_loss, L);
-      atomicAdd(&a.ctrl->epoch_sse, S);
+    if (threadIdx.x < 32) {
+      const int which = threadIdx.x >> 4, i = threadIdx.x & 15;
+      float v = red[which][i];
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
+      if (i == 0) {
+        atomicAdd(which == 0 ? &a.ctrl->loss_sum : &a.ctrl->sse_sum, (double)v);
+        atomicAdd(which == 0 ? &a.ctrl->epoch_loss : &a.ctrl->epoch_sse, (double)v);
+      }
     }
   }
 }
@@ -198,11 +189,27 @@ int launch_head_fwd(const HeadFwdArgs& a, int mode, hipStream_t stream) {
   INF_CHECK_ARG(a.H % 64 == 0 && a.H <= 512, "head: hidden width must be a multiple of 64 and <= 512");
   INF_CHECK_ARG(a.rows >= a.batch, "head: rows < batch");
   if (a.rows == 0) return INF_OK;
-  const unsigned grid = (unsigned)ceil_div(a.rows, HEAD_RAYS_PER_BLOCK);
-  if (mode == INF_MODE_BF16)
-    head_fwd_kernel<bf16><<<grid, 256, 0, stream>>>(a);
-  else
-    head_fwd_kernel<float><<<grid, 256, 0, stream>>>(a);
+  const unsigned grid = (unsigned)ceil_div(a.rows, 16);
+#define HEAD_FWD_CASE(EPL)                                                    \
+  case EPL:                                                                   \
+    if (mode == INF_MODE_BF16)                                                \
+      head_fwd_kernel<bf16, EPL><<<grid, 256, 0, stream>>>(a);                \
+    else                                                                      \
+      head_fwd_kernel<float, EPL><<<grid, 256, 0, stream>>>(a);               \
+    break;
+  switch (a.H / 16) {
+    HEAD_FWD_CASE(4)
+    HEAD_FWD_CASE(8)
+    HEAD_FWD_CASE(12)
+    HEAD_FWD_CASE(16)
+    HEAD_FWD_CASE(20)
+    HEAD_FWD_CASE(24)
+    HEAD_FWD_CASE(28)
+    HEAD_FWD_CASE(32)
+    default:
+      INF_CHECK_ARG(false, "head: unsupported hidden width");
+  }
+#undef HEAD_FWD_CASE
   INF_LAUNCH_CHECK();
   return INF_OK;
 }

@@ -97,9 +97,12 @@ class Adam(torch.optim.Adam):
             rt.dev_lr = lr
 
     def after_fused_step(self, module, rt, group):
+        self.after_fused_steps(module, rt, group, 1)
+
+    def after_fused_steps(self, module, rt, group, n):
         for p in module.parameters():
-            self.state[p]["step"] += 1
-        rt.dev_step += 1
+            self.state[p]["step"] += n
+        rt.dev_step += n
 
     # ---- torch API -------------------------------------------------------------------
     @torch.no_grad()

@@ -157,8 +157,20 @@ class TextureField(nn.Module):
         return plan
 
     # ---- forward (model.py:98-112) -----------------------------------------------
+    def __deepcopy__(self, memo):
+        """Copies parameters and structure, not the device runtime (plan handles and
+        workspaces are per instance; the copy binds its own on first use)."""
+        import copy as _copy
+        cls = self.__class__
+        new = cls.__new__(cls)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            new.__dict__[k] = None if k == "_rt" else _copy.deepcopy(v, memo)
+        return new
+
     def forward(self, batch):
         params = list(self.parameters())
+        needs = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         lazy = getattr(batch, "is_lazy_rays", None)
         if lazy is not None and lazy():
             feats, rays = None, batch.ray_args()
@@ -173,7 +185,7 @@ class TextureField(nn.Module):
                                           "reference (they are data) and are not implemented")
             feats = feats.to(torch.float32).contiguous()
             rays, B = None, feats.shape[0]
-        return _TextureFieldFn.apply(self, feats, rays, B, *params)
+        return _TextureFieldFn.apply(self, feats, rays, B, needs, *params)
 
     # ---- fused training step (used by trainer.Trainer) ------------------------------
     def fused_train_step(self, batch, optim, loss_type: str, want_pred: bool = True, loss_count: int = 0):
@@ -197,8 +209,7 @@ class TextureField(nn.Module):
 
 class _TextureFieldFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, module, feats, rays, B, *params):
-        needs = any(ctx.needs_input_grad[4:])
+    def forward(ctx, module, feats, rays, B, needs, *params):
         plan = module.hip_plan(B)
         rt = module._rt
         if rays is not None:
@@ -243,7 +254,7 @@ class _TextureFieldFn(torch.autograd.Function):
         out = []
         for off, n, shape in zip(plan.offsets, plan.numels, ctx.shapes):
             out.append(grads[off:off + n].view(shape))
-        return (None, None, None, None, *out)
+        return (None, None, None, None, None, *out)
 
 
 def init_weights(m):

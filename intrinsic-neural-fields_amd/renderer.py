@@ -1,0 +1,116 @@
+"""Host mirror of the reference renderer.py.
+
+The MLP slice of `Renderer.render` (reference renderer.py:112-146: batched inference
+over the hit rays, then placement of each colour into a white/black image, then the
+un-masking to H x W) runs on the HIP device in `render_hits`: gather + forward + scatter
+in one launch sequence per 2^18-ray chunk (csrc/plan.hip inf_render), with the table
+resident on the device instead of the reference's host-side M x k feature buffer.
+
+Ray casting (reference renderer.py:71-81 -> mesh.ray_tracing) needs trimesh/embree and
+is outside this build's scope: `render()` takes its hits from a
+`ray_tracer` callable with the signature and return value of mesh.ray_tracing
+(features-or-None, hit_ray_idxs, unit_ray_dirs, face_idxs) extended by the hit
+vertex ids and barycentric coordinates, or raises.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from mesh import load_first_k_eigenfunctions
+from utils import load_trained_model
+
+RENDER_CHUNK = 1 << 18
+
+
+def make_renderer_with_trained_model(config, device="cuda"):
+    """Reference renderer.py:9-32 (without the mesh: ray casting is out of scope)."""
+    efuncs = load_first_k_eigenfunctions(config["data"]["eigenfunctions_path"], config["model"].get("k"),
+                                         rescale_strategy=config["data"].get("rescale_strategy", "standard"),
+                                         embed_strategy=config["data"].get("embed_strategy"),
+                                         eigenvalues_path=config["data"].get("eigenvalues_path"))
+    weights_path = os.path.join(config["training"]["out_dir"], "model.pt")
+    model = load_trained_model(config["model"], weights_path, device, mesh=None)
+    return Renderer(model, None, eigenfunctions=efuncs, device=device, H=config["data"]["img_height"],
+                    W=config["data"]["img_width"])
+
+
+class Renderer:
+    """Reference renderer.py:35-146."""
+
+    def __init__(self, model, mesh, eigenfunctions=None, feature_strategy="efuncs", background="white", device="cpu",
+                 *, H, W, ray_tracer=None):
+        if feature_strategy != "efuncs":
+            raise ValueError(f"Unknown feature strategy: {feature_strategy}")
+        self.model = model
+        self.mesh = mesh
+        self.feature_strategy = feature_strategy
+        self.features = eigenfunctions
+        self.H = H
+        self.W = W
+        self.background = background
+        self.device = device
+        self.ray_tracer = ray_tracer
+        self._dev_features = None
+
+    def set_height(self, height):
+        self.H = height
+
+    def set_width(self, width):
+        self.W = width
+
+    def _features_on_device(self, device):
+        if self._dev_features is None or self._dev_features.device != device:
+            self._dev_features = self.features.to(device=device, dtype=torch.float32).contiguous()
+        return self._dev_features
+
+    @torch.no_grad()
+    def render_hits(self, vertex_idxs_of_hit_faces, barycentric_coords, hit_ray_idxs, obj_mask_1d=None,
+                    return_tensor=False):
+        """Colours of precomputed hits placed into an H x W x 3 image (renderer.py:112-146)."""
+        from inf_hip import runtime
+        assert obj_mask_1d is None or obj_mask_1d.size()[0] == self.H * self.W
+        self.model.eval()
+        dev = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
+        if dev.type != "cuda":
+            raise RuntimeError("Renderer.render_hits runs on the HIP device; construct it with device='cuda'")
+        E = self._features_on_device(dev)
+        vids = vertex_idxs_of_hit_faces.to(dev)
+        bary = barycentric_coords.to(dev, torch.float32)
+        hit = hit_ray_idxs.to(dev, torch.int64).contiguous()
+        num_rays = hit.shape[0]
+        assert num_rays > 0
+        M = self.H * self.W
+        fill = 1.0 if self.background == "white" else 0.0
+        assert self.background in ("white", "black")
+        img = torch.full((M, 3), fill, dtype=torch.float32, device=dev)
+        pixel_map = None
+        if obj_mask_1d is not None:
+            assert obj_mask_1d.dtype == torch.bool
+            pixel_map = torch.nonzero(obj_mask_1d.to(dev)).reshape(-1)
+        src = runtime.RaySource(E, vids, bary, None)
+        chunk = min(RENDER_CHUNK, num_rays)
+        plan = self.model.hip_plan(chunk)
+        for low in range(0, num_rays, chunk):
+            n = min(chunk, num_rays - low)
+            b = plan.make_batch(source=src, offset=low, batch=n)
+            plan.render(b, hit[low:low + n], pixel_map, img)
+        self.model._rt.saved_gen = None
+        img = img.reshape(self.H, self.W, 3)
+        return img if return_tensor else img.cpu().numpy()
+
+    @torch.no_grad()
+    def render(self, camCv2world, K, obj_mask_1d=None, eval_render=False, distortion_coeffs=None,
+               distortion_type=None):
+        """Reference renderer.py:64-146 with hits from `self.ray_tracer`."""
+        if self.ray_tracer is None:
+            raise NotImplementedError("ray casting (mesh.ray_tracing, trimesh/embree) is outside this build's hot "
+                                      "path; pass ray_tracer=... or call render_hits with precomputed hits")
+        vids, bary, hit_ray_idxs = self.ray_tracer(camCv2world, K, obj_mask_1d=obj_mask_1d, H=self.H, W=self.W,
+                                                   distortion_coeffs=distortion_coeffs,
+                                                   distortion_type=distortion_type)
+        img = self.render_hits(vids, bary, hit_ray_idxs, obj_mask_1d, return_tensor=True)
+        if eval_render:
+            return img.cpu(), hit_ray_idxs
+        return img.cpu().numpy()

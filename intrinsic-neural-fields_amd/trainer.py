@@ -1,0 +1,301 @@
+"""Host mirror of the reference trainer.py (Trainer, trainer.py:18-337).
+
+Public behaviour is the reference's: the same epoch loop, train/val metrics and
+TensorBoard tags (Train_Loss, Train Epoch-PSNR, Val_Loss, Val Epoch-PSNR, Test Loss),
+best-model tracking starting at min_val_loss = 1.0, checkpoint files and keys
+(checkpoint.pt every `checkpoint_every` epochs from epoch 0, checkpoint_{199}.pt /
+best_model_checkpoint_{199}.pt, model.pt, model_last_epoch.pt) and resume.
+
+The inner loop is where it differs (trainer.py:248-256): with a TextureField, the HIP
+Adam and a tagged loss, every batch runs as ONE fused launch sequence (gather ->
+forward -> loss -> backward -> Adam, csrc/plan.hip inf_train_step); the full batches
+of an epoch replay a captured HIP graph, and the loss / squared-error sums stay on the
+device, read once per epoch instead of the reference's two host syncs per step.  Any
+other model / optimizer / loss falls back to the reference's autograd step.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import random
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from evaluation_metrics import epoch_psnr
+from utils import to_device
+
+
+class _JsonlWriter:
+    """Stand-in for tensorboardX.SummaryWriter (absent here): scalars to logs/scalars.jsonl."""
+
+    def __init__(self, log_dir):
+        os.makedirs(log_dir, exist_ok=True)
+        self.path = os.path.join(log_dir, "scalars.jsonl")
+
+    def add_scalar(self, tag, value, global_step=None):
+        with open(self.path, "a") as f:
+            f.write(json.dumps({"tag": tag, "value": float(value), "step": global_step}) + "\n")
+
+    def add_image(self, *args, **kwargs):
+        pass
+
+
+def _summary_writer(log_dir):
+    try:
+        from tensorboardX import SummaryWriter
+        return SummaryWriter(log_dir)
+    except ImportError:
+        return _JsonlWriter(log_dir)
+
+
+class _FusedEpoch:
+    """Replays one captured fused step per full batch of an epoch."""
+
+    def __init__(self, trainer):
+        self.t = trainer
+        self.graph = None
+        self.key = None
+        self.perm = None
+
+    def run(self, loader):
+        t = self.t
+        model, optim = t.model, t.optim
+        loss_type = t.loss_fn.loss_type
+        it = iter(loader)  # reshuffles like the reference (randperm on the device)
+        B, N, nb = loader.B, loader.N, len(loader)
+        full = N // B if nb * B > N else nb
+        rt = model.hip_runtime()
+        group = optim.fused_group_for(model)
+        rt.ensure_optimizer_arenas()
+        plan = model.hip_plan(B, loss_type)
+        use_graph = os.environ.get("INF_GRAPH", "1") != "0" and full >= 2
+        key = (id(plan), B, N, loss_type, id(loader.source))
+        if self.perm is None or self.perm.numel() != N or self.perm.device != rt.device:
+            self.perm = torch.empty(N, dtype=torch.int64, device=rt.device)
+        self.perm.copy_(loader.idxs)
+        plan.reset_epoch_sums()
+        total = 0
+        done = 0
+        if use_graph:
+            optim.sync_runtime_state(model, rt, plan, group)
+            if self.graph is None or self.key != key:
+                self._capture(plan, loader, B, loss_type)
+                self.key = key
+            optim.sync_runtime_state(model, rt, plan, group)
+            plan.reset_epoch_sums()
+            plan.set_batch_index(0)
+            for _ in range(full):
+                self.graph.replay()
+            optim.after_fused_steps(model, rt, group, full)
+            done = full
+            total = full * B
+        for i, batch in enumerate(it):
+            if i < done:
+                continue
+            model.fused_train_step(batch, optim, loss_type, want_pred=False)
+            total += batch.batch_size
+        c = plan.read_ctrl()
+        return c["epoch_loss"] / (3 * total), c["epoch_sse"] / total
+
+    def _capture(self, plan, loader, B, loss_type):
+        b = plan.make_batch(source=loader.source, ray_idx=self.perm, offset=0, batch=B, offset_from_ctrl=True,
+                            loss=loss_type)
+        self._batch = b
+        # one eager step settles the plan's per-batch tables before capture, then undo it
+        saved = [x.clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl)]
+        plan.set_batch_index(0)
+        plan.train_step(b, None, apply_adam=True)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                plan.train_step(b, None, apply_adam=True)
+                plan.ctrl_advance()
+        torch.cuda.current_stream().wait_stream(s)
+        for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
+            dst.copy_(src)
+        plan.sync_shadow()
+        self.graph = g
+
+
+class Trainer:
+    def __init__(self, model, optim, loss_fn, renderer, data, mesh, config, device):
+        self.model = model
+        self.optim = optim
+        self.loss_fn = loss_fn
+        self.renderer = renderer
+        self.mesh = mesh
+        self.config = config
+        self.use_lr_scheduler = config["training"].get("use_lr_scheduler", False)
+        self.lr_scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim, mode="min", factor=0.2)
+        self.dataset_type = self.config["data"].get("type")
+        self.H = config["data"]["img_height"]
+        self.W = config["data"]["img_width"]
+        self.train_data_loader = data["train"]
+        self.val_data_loader = data["val"]
+        if self.dataset_type is None:
+            self.val_render_infos = list(zip(config["data"].get("eval_render_input_paths", []),
+                                             config["data"].get("eval_render_img_names", [])))
+        self.test_data_loader = data.get("test", None)
+        self.out_dir = self.config["training"]["out_dir"]
+        log_dir = os.path.join(self.out_dir, "logs")
+        os.makedirs(log_dir, exist_ok=True)
+        self.writer = _summary_writer(log_dir)
+        self.render_every = self.config["training"]["render_every"]
+        self.print_every = self.config["training"]["print_every"]
+        self.epochs = self.config["training"]["epochs"]
+        self.checkpoint_every = self.config["training"].get("checkpoint_every")
+        if self.checkpoint_every is not None:
+            self.checkpoint_path = os.path.join(self.out_dir, "checkpoint.pt")
+        self.device = device
+        self.model_config = self.config["model"]
+        self.best_model_weights_path = os.path.join(self.out_dir, "model.pt")
+        self.best_model = None
+        self.model_last_epoch_path = os.path.join(self.out_dir, "model_last_epoch.pt")
+        self._fused_epoch = _FusedEpoch(self)
+        self._render_note = False
+
+    # ---- fused-path eligibility ----------------------------------------------------
+    def _can_fuse(self, batch=None):
+        from inf_optim import Adam
+        from model import TextureField
+        ok = isinstance(self.model, TextureField) and isinstance(self.optim, Adam) and \
+            getattr(self.loss_fn, "loss_type", None) is not None
+        if batch is not None:
+            ok = ok and hasattr(batch, "is_lazy_rays") and batch.is_lazy_rays()
+        return ok
+
+    def _train_step(self, batch):
+        """Reference trainer.py:71-84: returns (loss.item(), pred_rgbs)."""
+        if self._can_fuse(batch):
+            pred = self.model.fused_train_step(batch, self.optim, self.loss_fn.loss_type, want_pred=True)
+            plan = self.model._rt.plan
+            return plan.read_ctrl()["loss_sum"] / (3 * batch.batch_size), pred
+        pred_rgbs = self.model(batch)
+        loss = self.loss_fn(pred_rgbs, batch["expected_rgbs"])
+        self.optim.zero_grad(set_to_none=True)
+        loss.backward()
+        self.optim.step()
+        return loss.item(), pred_rgbs
+
+    @torch.no_grad()
+    def _eval_step(self, model, batch):
+        pred_rgbs = model(batch)
+        loss = self.loss_fn(pred_rgbs, batch["expected_rgbs"])
+        return loss, pred_rgbs
+
+    def evaluate(self, epoch=None):
+        """Reference trainer.py:164-187 (sums kept on the device, one sync)."""
+        self.model.eval()
+        acc_loss = torch.zeros((), dtype=torch.float64, device=self.device)
+        acc_l2 = torch.zeros((), dtype=torch.float64, device=self.device)
+        total = 0
+        for batch in self.val_data_loader:
+            batch = to_device(batch, device=self.device)
+            loss, pred_rgbs = self._eval_step(self.model, batch)
+            bs = batch["expected_rgbs"].size()[0]
+            acc_l2 += F.mse_loss(pred_rgbs, batch["expected_rgbs"], reduction="sum").double()
+            acc_loss += loss.double() * bs
+            total += bs
+        val_loss = float(acc_loss) / total
+        self.writer.add_scalar("Val_Loss", val_loss, epoch)
+        val_psnr = epoch_psnr(float(acc_l2) / total)
+        self.writer.add_scalar("Val Epoch-PSNR", val_psnr, epoch)
+        return val_loss, val_psnr
+
+    def test(self):
+        """Reference trainer.py:189-212 (no test loader is built, config.py:85)."""
+        if self.test_data_loader is None:
+            return
+        model = self.best_model if self.best_model is not None else self.model
+        model.eval()
+        acc, total = 0.0, 0
+        for batch in self.test_data_loader:
+            loss, _ = self._eval_step(model, batch)
+            bs = batch["expected_rgbs"].size()[0]
+            acc += loss.item() * bs
+            total += bs
+        test_loss = acc / total
+        self.writer.add_scalar("Test Loss", test_loss)
+        print(f"Test Loss: {test_loss}")
+        return test_loss
+
+    def _checkpoint_dict(self, epoch):
+        return {"epoch": epoch, "model_state_dict": self.model.state_dict(),
+                "optimizer_state_dict": self.optim.state_dict(),
+                "pytorch_random_state": torch.random.get_rng_state(), "python_random_state": random.getstate(),
+                "numpy_random_state": np.random.get_state()}
+
+    def _init_or_load_checkpoint(self):
+        """Reference trainer.py:214-230.  The checkpoint is this trainer's own file
+        (it holds Python/numpy RNG states, so it is not a weights-only file)."""
+        if self.checkpoint_every is None or not os.path.exists(self.checkpoint_path):
+            return 0
+        print("Restoring from checkpoint...")
+        checkpoint = torch.load(self.checkpoint_path, map_location="cpu", weights_only=False)
+        self.model.load_state_dict(checkpoint["model_state_dict"])
+        self.optim.load_state_dict(checkpoint["optimizer_state_dict"])
+        torch.random.set_rng_state(checkpoint["pytorch_random_state"])
+        random.setstate(checkpoint["python_random_state"])
+        np.random.set_state(checkpoint["numpy_random_state"])
+        print("Done.")
+        return checkpoint["epoch"] + 1
+
+    def _train_epoch(self):
+        if self._can_fuse() and hasattr(self.train_data_loader, "source"):
+            return self._fused_epoch.run(self.train_data_loader)
+        acc_loss, acc_l2, total = 0.0, 0.0, 0
+        for batch in self.train_data_loader:
+            batch = to_device(batch, device=self.device)
+            loss, pred_rgbs = self._train_step(batch)
+            bs = batch["expected_rgbs"].size()[0]
+            acc_l2 += F.mse_loss(pred_rgbs, batch["expected_rgbs"], reduction="sum").item()
+            acc_loss += loss * bs
+            total += bs
+        return acc_loss / total, acc_l2 / total
+
+    def train(self):
+        """Reference trainer.py:232-337."""
+        print("Starting training...")
+        epoch_start = self._init_or_load_checkpoint()
+        min_val_loss = 1.
+        for epoch in range(epoch_start, self.epochs):
+            self.model.train()
+            t0 = time.time()
+            train_loss, train_mse = self._train_epoch()
+            t1 = time.time()
+            self.writer.add_scalar("Train_Loss", train_loss, epoch)
+            train_psnr = epoch_psnr(train_mse)
+            self.writer.add_scalar("Train Epoch-PSNR", train_psnr, epoch)
+            val_loss, val_psnr = self.evaluate(epoch)
+            if val_loss < min_val_loss:
+                min_val_loss = val_loss
+                torch.save(self.model.state_dict(), self.best_model_weights_path)
+                self.best_model = copy.deepcopy(self.model)
+            if self.use_lr_scheduler:
+                self.lr_scheduler.step(val_loss)
+            if epoch == 0 or (epoch + 1) % self.print_every == 0:
+                print(f"Epoch: {epoch + 1} / {self.epochs}, Train Loss: {train_loss}, Train PSNR: {train_psnr}, "
+                      f"Val Loss: {val_loss}, Val PSNR: {val_psnr}"
+                      f"Epoch Time: {t1 - t0}s")
+            if (epoch == 0 or (epoch + 1) % self.render_every == 0) and not self._render_note:
+                print("Visualizing... skipped: view rendering needs ray casting (outside this build's hot path)")
+                self._render_note = True
+            if self.checkpoint_every is not None and epoch % self.checkpoint_every == 0:
+                print("Saving checkpoint...")
+                torch.save(self._checkpoint_dict(epoch), self.checkpoint_path)
+                print("Done.")
+            if epoch > 0 and (epoch + 1) == 200:
+                print(f"Persisting checkpoint at {epoch}...")
+                torch.save(self._checkpoint_dict(epoch), os.path.join(self.out_dir, f"checkpoint_{epoch}.pt"))
+                best = self.best_model if self.best_model is not None else self.model
+                torch.save(best.state_dict(), os.path.join(self.out_dir, f"best_model_checkpoint_{epoch}.pt"))
+                print("Done.")
+        self.test()
+        print("Done.")
+        torch.save(self.model.state_dict(), self.model_last_epoch_path)
