@@ -27,6 +27,8 @@ import torch  # noqa: E402
 
 PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0  # GB/s
+KERNEL_NAMES = {"dw_gemm": "gemm_nt_kernel<bf16,128,128> (grouped split-K weight-gradient GEMM)",
+                "chain": "chain_kernel (fused forward + loss + dX chain)"}
 
 
 def parse():
@@ -277,17 +279,24 @@ def main():
     ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
     value = world * args.batch / (ms * 1e-3)
 
-    from inf_hip import STAGE_DW_GEMM, STAGE_FWD_GEMM, STAGE_GATHER
-    # dominant kernel: the grouped split-K weight-gradient GEMM (one launch, all layers)
-    dw_ms, dw_flops, dw_bytes = time_stage(tr.plan, STAGE_DW_GEMM)
-    fwd_ms, fwd_flops, _ = time_stage(tr.plan, STAGE_FWD_GEMM, layer=1)
-    ga_ms, _, ga_bytes = time_stage(tr.plan, STAGE_GATHER, batch=tr.batch)
-    achieved = dw_flops / (dw_ms * 1e-3) / 1e12
+    from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
+    # per-kernel times (HIP events around repeated launches of one stage on its saved inputs)
+    stages = {}
+    stages["dw_gemm"] = time_stage(tr.plan, STAGE_DW_GEMM)
+    stages["gather"] = time_stage(tr.plan, STAGE_GATHER, batch=tr.batch)
+    stages["update"] = time_stage(tr.plan, STAGE_UPDATE)
+    if args.mode == "bf16" and not os.environ.get("INF_NO_CHAIN"):
+        stages["chain"] = time_stage(tr.plan, STAGE_CHAIN, batch=tr.batch)
+    mfma_stages = {k: v for k, v in stages.items() if k in ("dw_gemm", "chain")}
+    dom = max(mfma_stages, key=lambda k: mfma_stages[k][0])
+    dom_ms, dom_flops, _ = stages[dom]
+    achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+    dw_ms = stages["dw_gemm"][0]
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "dw_gemm_traffic.json")
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get(f"{args.mode}_B{args.batch}")
+            traffic = json.load(open(pmc_path)).get(f"{dom}_{args.mode}_B{args.batch}")
         except Exception:
             traffic = None
 
@@ -337,14 +346,15 @@ def main():
                        "rays_per_gpu_per_step": args.batch, "global_batch": args.batch * world,
                        "verts": args.verts, "parallelism": f"dp{world}", "graph": not args.no_graph},
             "model_tflops": flops_ray * value / 1e12,
-            "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel (grouped split-K weight-gradient GEMM)",
+            "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES[dom],
                          "achieved": achieved, "peak": PEAK[args.mode], "unit": "TFLOP/s",
                          "frac": achieved / PEAK[args.mode], "traffic": traffic,
-                         "avg_ms": dw_ms, "flops_per_launch": dw_flops},
-            "stages": {"fwd_gemm_layer1_ms": fwd_ms, "fwd_gemm_layer1_tflops": fwd_flops / (fwd_ms * 1e-3) / 1e12,
-                       "gather_ms": ga_ms, "gather_gbs": ga_bytes / (ga_ms * 1e-3) / 1e9,
-                       "gather_hbm_frac": ga_bytes / (ga_ms * 1e-3) / 1e9 / HBM_PEAK,
-                       "host_wall_ms_per_step": wall_ms},
+                         "avg_ms": dom_ms, "flops_per_launch": dom_flops},
+            "stages": {k: {"ms": v[0], "tflops": v[1] / (v[0] * 1e-3) / 1e12 if v[1] else None,
+                           "gbs": v[2] / (v[0] * 1e-3) / 1e9 if v[2] else None,
+                           "hbm_frac": v[2] / (v[0] * 1e-3) / 1e9 / HBM_PEAK if v[2] else None}
+                       for k, v in stages.items()},
+            "host_wall_ms_per_step": wall_ms,
             "large_batch": extra,
             "render": render,
             "cpu_baseline": cpu,

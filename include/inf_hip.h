@@ -173,10 +173,17 @@ int inf_render(inf_plan* plan, const inf_batch* batch, const int64_t* hit, const
  *   INF_STAGE_DW_GEMM  - the grouped split-K weight-gradient GEMM
  *   INF_STAGE_UPDATE   - the slab-reduction/Adam/packed-weight launch (reduce only:
  *                        parameters are not modified)
+ *   INF_STAGE_CHAIN    - the fused forward + loss + dX-chain kernel (bf16 mode)
  * *flops / *bytes receive the stage's algorithmic work per launch (unpadded). */
-enum { INF_STAGE_GATHER = 0, INF_STAGE_FWD_GEMM = 1, INF_STAGE_DW_GEMM = 2, INF_STAGE_UPDATE = 3 };
+enum { INF_STAGE_GATHER = 0, INF_STAGE_FWD_GEMM = 1, INF_STAGE_DW_GEMM = 2, INF_STAGE_UPDATE = 3,
+       INF_STAGE_CHAIN = 4 };
 int inf_run_stage(inf_plan* plan, const inf_batch* batch, int stage, int layer, double* flops, double* bytes,
                   inf_stream_t stream);
+
+/* Debug builds only (libinf_hip_dbg.so, -DINF_CHAIN_DEBUG): register the valid device
+ * byte ranges [lo, hi) (n pairs) and a result buffer; the fused chain then checks every
+ * global access against them and records violations instead of issuing them. */
+int inf_debug_ranges(inf_plan* plan, const uint64_t* ranges_dev, int n, unsigned long long* out_dev);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

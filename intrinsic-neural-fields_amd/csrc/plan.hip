@@ -8,11 +8,13 @@
 //   -> L-2 dX GEMMs (ReLU mask + bias-grad partials) -> ONE grouped split-K dW GEMM over
 //   all weight matrices -> ONE update launch (slab reduction + Adam + packed weights).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
 
 #include "adam.hpp"
+#include "chain.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
 
@@ -81,6 +83,10 @@ struct inf_plan {
   // saved forward
   int saved_batch = 0, saved_bp = 0;
   bool saved = false;
+  bool last_chain = false;  // the last training step ran the fused chain
+  const uint64_t* dbg_ranges = nullptr;
+  int dbg_n = 0;
+  unsigned long long* dbg_out = nullptr;
 
   template <typename T = char>
   T* W(int64_t off) const { return reinterpret_cast<T*>(ws + off); }
@@ -189,8 +195,9 @@ int build_layout(inf_plan* p) {
     const auto& g = p->segs[i];
     if (g.gemm) p->o_slab[i] = take((int64_t)S * g.R * g.c_pad * 4);
   }
-  p->o_hw = take((int64_t)p->grid_hb * 3 * H * 4);
-  p->o_hb = take((int64_t)p->grid_hb * 3 * 4);
+  const int64_t head_parts = std::max<int64_t>(p->grid_hb, Bp / 64);
+  p->o_hw = take(head_parts * 3 * H * 4);
+  p->o_hb = take(head_parts * 3 * 4);
 
   // update work list
   int64_t nitems = 0;
@@ -377,14 +384,19 @@ AdamArgs update_args(inf_plan* p, int Bp) {
 }
 
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
-int refresh_tables(inf_plan* p, int Bp, hipStream_t st) {
+int refresh_tables(inf_plan* p, int Bp, hipStream_t st, bool chain = false) {
   const int parts = Bp / 64;
   bool changed = false;
   for (size_t i = 0; i < p->segs.size(); ++i) {
     const ParamSeg& g = p->segs[i];
     AdamSeg& a = p->adam_segs[i];
-    if (g.kind == 1 && g.layer < p->L - 2 && a.nslab != parts) {
-      a.nslab = parts;
+    if (g.gemm) continue;
+    // hidden biases: one partial per 64 rays; the last hidden layer's and the output
+    // layer's come from head_bwd (grid_hb partials) on the layered path
+    const bool from_head = g.layer == p->L - 1 || (g.kind == 1 && g.layer == p->L - 2);
+    const int want = (from_head && !chain) ? p->grid_hb : parts;
+    if (a.nslab != want) {
+      a.nslab = want;
       changed = true;
     }
   }
@@ -461,6 +473,96 @@ int head_backward(inf_plan* p, int Bp, const float* dpred, bool count_step, hipS
   return launch_head_bwd(a, p->mode, st);
 }
 
+bool use_chain(const inf_plan* p) {
+  return p->mode == INF_MODE_BF16 && chain_supported(p->H) && p->L - 1 <= CHAIN_MAX_HIDDEN &&
+         std::getenv("INF_NO_CHAIN") == nullptr;
+}
+
+// Forward (train = 0) or fused forward + loss + backward chain (train = 1) of a padded
+// batch whose features are already in X0 (csrc/chain.hip).
+int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, const int64_t* hit,
+              const int64_t* pixel_map, float* img, hipStream_t st) {
+  const int H = p->H, L = p->L, s = p->s;
+  const int bm = chain_bm(Bp) <= Bp && Bp % chain_bm(Bp) == 0 ? chain_bm(Bp) : 64;
+  const int BK = chain_bk(bm);
+  ChainArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.L = L;
+  a.s = s;
+  a.H = H;
+  a.k_pad = p->k_pad;
+  a.rows = Bp;
+  a.batch = b->batch;
+  a.X = p->W<bf16>(p->o_x0);
+  int np = 0, steps = 0;
+  auto add = [&](const void* B, int ldb, int K, int a_src, int layer, int kind, int epi) {
+    ChainPhase& ph = a.ph[np++];
+    ph.B = reinterpret_cast<const bf16*>(B);
+    ph.ldb = ldb;
+    ph.ktiles = K / BK;
+    ph.a_src = a_src;
+    ph.layer = layer;
+    ph.kind = kind;
+    ph.epilogue = epi;
+    ph.step0 = steps;
+    steps += ph.ktiles;
+  };
+  for (int l = 0; l <= L - 2; ++l) {
+    const ParamSeg* w = p->weight_seg(l, 0);
+    if (l == 0) {
+      add(p->shadow + w->w_off, w->c_pad, p->k_pad, 1, l, 0, 1);
+    } else if (l == s) {
+      const ParamSeg* wy = p->weight_seg(l, 1);
+      add(p->shadow + w->w_off, w->c_pad, H, 0, l, 0, 0);
+      add(p->shadow + wy->w_off, wy->c_pad, p->k_pad, 1, l, 0, 1);
+    } else {
+      add(p->shadow + w->w_off, w->c_pad, H, 0, l, 0, 1);
+    }
+    a.bias[l] = p->params + p->bias_seg(l, 0)->off;
+    a.YT[l] = p->W<bf16>(p->o_yt[l]);
+    a.dZT[l] = p->W<bf16>(p->o_dZT[l]);
+    a.colsum[l] = p->W<float>(p->o_colsum[l]);
+  }
+  a.bias_y = p->params + p->bias_seg(s, 1)->off;
+  if (train) {
+    for (int l = L - 2; l >= 1; --l) {
+      const ParamSeg* w = p->weight_seg(l, 0);  // Lx at the skip layer
+      add(p->shadow + w->wt_off, w->R, H, 0, l, 1, 1);
+    }
+  }
+  a.nphase = np;
+  a.nsteps = steps;
+  a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
+  a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
+  a.hw_part = p->W<float>(p->o_hw);
+  a.hb_part = p->W<float>(p->o_hb);
+  a.ldt = Bp;
+  a.pred = pred;
+  a.ctrl = p->ctrl;
+  a.hit = hit;
+  a.pixel_map = pixel_map;
+  a.img = img;
+  a.dbg_ranges = p->dbg_ranges;
+  a.dbg_nranges = p->dbg_n;
+  a.dbg_out = p->dbg_out;
+  a.train = train ? 1 : 0;
+  a.save = train ? 1 : 0;
+  a.count_step = train ? 1 : 0;
+  if (train) {
+    INF_CHECK_ARG(b->rgb != nullptr, "training batch without target colours");
+    a.rgb = b->rgb;
+    a.ray_idx = b->ray_idx;
+    a.idx_dtype = b->idx_dtype;
+    a.idx_offset = b->idx_offset;
+    a.offset_from_ctrl = b->offset_from_ctrl;
+    a.loss = b->loss >= 0 ? b->loss : p->d.loss;
+    INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
+    const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
+    a.inv_count = (float)(1.0 / (double)cnt);
+  }
+  return launch_chain(a, bm, st);
+}
+
 int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool loss, const int64_t* hit,
                  const int64_t* pixel_map, float* img, hipStream_t st) {
   INF_CHECK_ARG(b != nullptr, "null batch");
@@ -468,6 +570,11 @@ int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool l
   int rc = pad_batch(p, b->batch, save, &Bp);
   if (rc) return rc;
   if ((rc = run_input(p, b, Bp, save, st))) return rc;
+  if (!save && use_chain(p)) {
+    if ((rc = run_chain(p, b, Bp, false, pred, hit, pixel_map, img, st))) return rc;
+    p->saved = false;
+    return INF_OK;
+  }
   if ((rc = run_forward_layers(p, Bp, save, st))) return rc;
   float* pred_ws = p->W<float>(p->o_pred);
   if ((rc = head_forward(p, b, Bp, save ? pred_ws : pred, loss, hit, pixel_map, img, st))) return rc;
@@ -668,11 +775,26 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int apply_a
   hipStream_t st = (hipStream_t)stream;
   INF_HIP_TRY(hipMemsetAsync(&p->ctrl->loss_sum, 0, 2 * sizeof(double), st));
   int rc;
-  if ((rc = forward_impl(p, batch, pred, true, true, nullptr, nullptr, nullptr, st))) return rc;
+  const bool chain = use_chain(p);
+  if (chain) {
+    int Bp = 0;
+    if ((rc = pad_batch(p, batch->batch, true, &Bp))) return rc;
+    if ((rc = run_input(p, batch, Bp, true, st))) return rc;
+    if ((rc = run_chain(p, batch, Bp, true, pred, nullptr, nullptr, nullptr, st))) return rc;
+    if ((rc = run_weight_grads(p, Bp, st))) return rc;
+    p->saved = false;
+    p->saved_batch = batch->batch;
+    p->saved_bp = Bp;
+    p->last_chain = true;
+  } else {
+    p->last_chain = false;
+    if ((rc = forward_impl(p, batch, pred, true, true, nullptr, nullptr, nullptr, st))) return rc;
+    const int Bp0 = p->saved_bp;
+    if ((rc = head_backward(p, Bp0, nullptr, true, st))) return rc;
+    if ((rc = run_backward_layers(p, Bp0, st))) return rc;
+  }
   const int Bp = p->saved_bp;
-  if ((rc = head_backward(p, Bp, nullptr, true, st))) return rc;
-  if ((rc = run_backward_layers(p, Bp, st))) return rc;
-  if ((rc = refresh_tables(p, Bp, st))) return rc;
+  if ((rc = refresh_tables(p, Bp, st, chain))) return rc;
   AdamArgs a = update_args(p, Bp);
   a.grad_src = GRAD_SLABS;
   if (apply_adam) {
@@ -710,7 +832,7 @@ int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const in
 
 int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double* flops, double* bytes,
                   inf_stream_t stream) {
-  if (p == nullptr || !p->bound || !p->saved) {
+  if (p == nullptr || !p->bound || !(p->saved || p->last_chain)) {
     set_error("run_stage needs a saved training step");
     return INF_ERR_STATE;
   }
@@ -745,8 +867,17 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
         }
       break;
     }
+    case INF_STAGE_CHAIN: {
+      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && use_chain(p), "chain stage needs a bf16 training batch");
+      // replay on the saved inputs; the step counter it advances is restored by the caller
+      rc = run_chain(p, b, Bp, true, nullptr, nullptr, nullptr, nullptr, st);
+      const double Lh = p->L;
+      f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+      by = B * (2.0 * p->k_pad * e + 2.0 * (Lh - 1) * H * e) + 2.0 * 4 * p->P;
+      break;
+    }
     case INF_STAGE_UPDATE: {
-      if ((rc = refresh_tables(p, Bp, st))) return rc;
+      if ((rc = refresh_tables(p, Bp, st, p->last_chain))) return rc;
       AdamArgs a = update_args(p, Bp);
       INF_CHECK_ARG(p->grads != nullptr, "update stage needs a bound grads arena");
       a.grad_src = GRAD_SLABS;  // reduce only into the grads arena: parameters unchanged
@@ -761,6 +892,14 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
   if (flops) *flops = f;
   if (bytes) *bytes = by;
   return rc;
+}
+
+int inf_debug_ranges(inf_plan* p, const uint64_t* ranges, int n, unsigned long long* out) {
+  INF_CHECK_ARG(p != nullptr && n >= 0, "debug ranges");
+  p->dbg_ranges = ranges;
+  p->dbg_n = n;
+  p->dbg_out = out;
+  return INF_OK;
 }
 
 int inf_ctrl_advance(inf_plan* p, inf_stream_t stream) {

@@ -131,8 +131,11 @@ class Plan:
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and h.value:
-            lib.inf_plan_destroy(h)
+        if h is not None and h.value and lib is not None:
+            try:
+                lib.inf_plan_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
             self.handle = None
 
     # ---- ctrl block -------------------------------------------------------------

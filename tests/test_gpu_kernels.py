@@ -222,3 +222,65 @@ def test_render_golden():
             pmap = torch.nonzero(torch.from_numpy(d["obj_mask"]).cuda()).reshape(-1)
         plan.render(plan.make_batch(source=src, batch=hit.shape[0]), hit, pmap, img)
         np.testing.assert_allclose(img.reshape(H, W, 3).cpu().numpy(), d[f"img_{tag}"], atol=1e-5)
+
+
+@pytest.mark.parametrize("name,B", [("B", 1024), ("A", 512), ("R", 256), ("B", 32768)])
+def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
+    """The fused bf16 chain (csrc/chain.hip) vs the layered bf16 kernels and the fp32
+    oracle: predictions within 2e-2, reduced gradients within 3e-2 of the largest element
+    (bf16 operands, fp32 accumulation)."""
+    rng = np.random.default_rng(21)
+    k, H, L, s = CFG[name]
+    w0 = weights(golden(f"g2_forward_{name}.npz"))
+    V, N = 2000, B
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (N, 3))
+    bary = rng.dirichlet([1, 1, 1], N).astype(np.float32)
+    rgb = rng.random((N, 3)).astype(np.float32)
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda())
+    out = {}
+    for tag in ("chain", "layered"):
+        if tag == "layered":
+            monkeypatch.setenv("INF_NO_CHAIN", "1")
+        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
+        c = plan.read_ctrl()
+        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"], c["step"])
+    _, cache = O.mlp_forward(w0, O.gather(E, vids, bary), L, s)
+    p_ref = cache["out"][-1]
+    g_ref = O.mlp_backward(w0, cache, O.loss_grad(p_ref, rgb, "L2"), L, s)
+    for tag in ("chain", "layered"):
+        p, g, lsum, step = out[tag]
+        assert step == 1
+        assert np.abs(p - p_ref).max() < 2e-2, tag
+        assert abs(lsum / (3 * B) - O.loss_value(p_ref, rgb, "L2")) < 2e-3, tag
+        for n in O.layer_names(L, s):
+            scale = max(np.abs(g_ref[n]).max(), 1e-12)
+            err = np.abs(g[n] - g_ref[n]).max() / scale
+            assert err < 3e-2, (tag, n, err)
+    # chain and layered bf16 paths agree much more tightly with each other
+    np.testing.assert_allclose(out["chain"][0], out["layered"][0], atol=1e-5)
+    for n in O.layer_names(L, s):
+        scale = max(np.abs(out["layered"][1][n]).max(), 1e-12)
+        assert np.abs(out["chain"][1][n] - out["layered"][1][n]).max() / scale < 1e-2, n
+
+
+def test_bf16_chain_render_matches_layered(monkeypatch):
+    d = golden("g7_render.npz")
+    H, W = int(d["H"]), int(d["W"])
+    E = torch.from_numpy(d["E"]).cuda()
+    imgs = {}
+    for tag in ("chain", "layered"):
+        if tag == "layered":
+            monkeypatch.setenv("INF_NO_CHAIN", "1")
+        plan, _, _ = make_plan("A", mode="bf16", max_batch=1024)
+        src = rt().RaySource(E, torch.from_numpy(d["vids_full"]).cuda(), torch.from_numpy(d["bary_full"]).cuda(), None)
+        hit = torch.from_numpy(d["hit_full"]).cuda()
+        img = torch.ones((H * W, 3), device="cuda")
+        plan.render(plan.make_batch(source=src, batch=hit.shape[0]), hit, None, img)
+        imgs[tag] = img.cpu().numpy()
+    np.testing.assert_allclose(imgs["chain"], imgs["layered"], atol=1e-5)
+    np.testing.assert_allclose(imgs["chain"].reshape(H, W, 3), d["img_full"], atol=2e-2)
