@@ -24,25 +24,40 @@ struct ModeTraits;
 template <>
 struct ModeTraits<bf16> {
   static constexpr int BK = 64;  // elements per k-tile (128 B rows)
-  static constexpr int CH = 8;   // elements per 16-byte chunk
+
 };
 template <>
 struct ModeTraits<float> {
   static constexpr int BK = 32;
-  static constexpr int CH = 4;
+
 };
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// 16-byte chunk `chunk` of 128-byte LDS row `row`.  The 16 lanes of a ds_read_b128 group
+// read 16 consecutive rows at one chunk: (row & 1, row >> 1) select distinct slots of the
+// 256-byte bank row pair, so the group is conflict-free.
+__device__ __forceinline__ int swz_slot(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + (swz_slot(row, chunk) << 4); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  // wait until at most N of this wave's vector-memory ops (direct-to-LDS loads) are in
+  // flight, then a workgroup barrier; one asm statement so no LDS access moves across
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 template <typename T, int BM, int BN>
 struct Tile {
   static constexpr int BK = ModeTraits<T>::BK;
-  static constexpr int CH = ModeTraits<T>::CH;
+
   static constexpr int A_CHUNKS = BM * 8 / 256;  // 16-byte chunks per thread per k-tile
   static constexpr int B_CHUNKS = BN * 8 / 256;
-  static constexpr int OPER_BYTES = 2 * (BM + BN) * 128;
+  static constexpr int STAGES = (BM == 128 && BN == 128) ? 3 : 4;
+  static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int OPER_BYTES = STAGES * STAGE_BYTES;
   static constexpr int CLD = BN + 4;  // fp32 C staging row stride
   static constexpr int C_BYTES = BM * CLD * 4;
   static constexpr int LDS_BYTES = OPER_BYTES > C_BYTES ? OPER_BYTES : C_BYTES;
@@ -106,10 +121,10 @@ __device__ __forceinline__ float ld_elem(const void* p, int64_t i) {
 }
 
 template <typename T, int BM, int BN>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const GemmBatch batch) {
+__global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) {
   using TL = Tile<T, BM, BN>;
-  constexpr int BK = TL::BK, CH = TL::CH;
-  __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
+  constexpr int BK = TL::BK;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // ---- locate problem / tile -----------------------------------------------------
   int pi = 0;
@@ -141,42 +156,37 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const GemmBatch batch) 
     t_end = t_begin + per;
   }
 
-  char* As_base = smem;
-  char* Bs_base = smem + 2 * BM * 128;
-
-  i32x4 ra[TL::A_CHUNKS], rb[TL::B_CHUNKS];
-
-  auto load_global = [&](int t) {
+  // ---- S-stage direct-to-LDS pipeline ------------------------------------------------
+  // Each 1 KiB wave-instruction fills 8 consecutive 128-byte rows of a stage image; lane
+  // L writes row L/8, slot L%8, so the source address carries the swizzle (the image is
+  // lane-linear).  Wave w fills A rows [w*BM/4, (w+1)*BM/4) and B rows likewise.
+  constexpr int STAGES = TL::STAGES;
+  constexpr int A_INS = BM / 32, B_INS = BN / 32;  // glds per wave per stage
+  constexpr int PER = A_INS + B_INS;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int lrow = lane >> 3, lslot = lane & 7;
+  auto issue = [&](int t) {
+    const int buf = (t - t_begin) % STAGES;
     const int seg = t < kt0 ? 0 : 1;
     const int k0 = (seg == 0 ? t : t - kt0) * BK;
-    const T* A = reinterpret_cast<const T*>(P.A[seg]);
-    const T* Bm = reinterpret_cast<const T*>(P.B[seg]);
-    const int64_t lda = P.lda[seg], ldb = P.ldb[seg];
+    const char* A = reinterpret_cast<const char*>(reinterpret_cast<const T*>(P.A[seg]) + k0);
+    const char* Bm = reinterpret_cast<const char*>(reinterpret_cast<const T*>(P.B[seg]) + k0);
+    const int64_t lda = P.lda[seg] * (int64_t)sizeof(T), ldb = P.ldb[seg] * (int64_t)sizeof(T);
+    char* As = smem + buf * TL::STAGE_BYTES;
+    char* Bs = As + BM * 128;
 #pragma unroll
-    for (int i = 0; i < TL::A_CHUNKS; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, ch = c & 7;
-      ra[i] = *reinterpret_cast<const i32x4*>(A + (int64_t)(m0 + row) * lda + k0 + ch * CH);
+    for (int i = 0; i < A_INS; ++i) {
+      const int r0 = wv * (BM / 4) + i * 8;
+      const int row = r0 + lrow;
+      const char* src = A + (int64_t)(m0 + row) * lda + (swz_slot(row, lslot) << 4);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(As + r0 * 128), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < TL::B_CHUNKS; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, ch = c & 7;
-      rb[i] = *reinterpret_cast<const i32x4*>(Bm + (int64_t)(n0 + row) * ldb + k0 + ch * CH);
-    }
-  };
-  auto store_lds = [&](int buf) {
-    char* As = As_base + buf * BM * 128;
-    char* Bs = Bs_base + buf * BN * 128;
-#pragma unroll
-    for (int i = 0; i < TL::A_CHUNKS; ++i) {
-      const int c = tid + 256 * i;
-      *reinterpret_cast<i32x4*>(As + swz(c >> 3, c & 7)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < TL::B_CHUNKS; ++i) {
-      const int c = tid + 256 * i;
-      *reinterpret_cast<i32x4*>(Bs + swz(c >> 3, c & 7)) = rb[i];
+    for (int i = 0; i < B_INS; ++i) {
+      const int r0 = wv * (BN / 4) + i * 8;
+      const int row = r0 + lrow;
+      const char* src = Bm + (int64_t)(n0 + row) * ldb + (swz_slot(row, lslot) << 4);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(Bs + r0 * 128), 16, 0, 0);
     }
   };
 
@@ -187,20 +197,22 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const GemmBatch batch) 
     for (int j = 0; j < TL::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (t_begin < t_end) {
-    load_global(t_begin);
-    store_lds(0);
-    __syncthreads();
-    int buf = 0;
+#pragma unroll
+    for (int q = 0; q < STAGES - 1; ++q)
+      if (t_begin + q < t_end) issue(t_begin + q);
 #pragma unroll 1
     for (int t = t_begin; t < t_end; ++t) {
-      const bool more = t + 1 < t_end;
-      if (more) load_global(t + 1);
-      compute_tile<T, BM, BN>(As_base + buf * BM * 128, Bs_base + buf * BN * 128, wm0, wn0, lane, acc);
-      if (more) store_lds(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
+      // stages issued after t that may stay in flight
+      const int ahead = min(STAGES - 2, t_end - 1 - t);
+      if (ahead >= 2) wait_vm_barrier<2 * PER>();
+      else if (ahead == 1) wait_vm_barrier<PER>();
+      else wait_vm_barrier<0>();
+      if (t + STAGES - 1 < t_end) issue(t + STAGES - 1);
+      const char* As = smem + ((t - t_begin) % STAGES) * TL::STAGE_BYTES;
+      compute_tile<T, BM, BN>(As, As + BM * 128, wm0, wn0, lane, acc);
     }
   }
+  __syncthreads();
 
   // ---- epilogue ------------------------------------------------------------------
   float* Cs = reinterpret_cast<float*>(smem);
@@ -291,7 +303,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const GemmBatch batch) 
 
 template <typename T, int BM, int BN>
 int launch_typed(const GemmBatch& b, hipStream_t stream) {
-  gemm_nt_kernel<T, BM, BN><<<dim3((unsigned)b.total_blocks), dim3(256), 0, stream>>>(b);
+  constexpr int lds = Tile<T, BM, BN>::LDS_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr = true;
+  }
+  gemm_nt_kernel<T, BM, BN><<<dim3((unsigned)b.total_blocks), dim3(256), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
