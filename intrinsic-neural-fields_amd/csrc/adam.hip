@@ -32,9 +32,146 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   p = p + s.step_neg * (m / denom);
 }
 
+// Matrix tile: ADAM_TILE_R (64) rows x ADAM_TILE_C (32) columns, 256 threads; thread
+// (rb, c4) owns rows rb and rb + 32 at columns 4*c4 .. 4*c4+3.  Every load of a phase is
+// issued before its first use (parameters + Adam state, then the split-K slabs eight at a
+// time) so each thread keeps 16-24 16-byte loads in flight.  VEC4: the tensor's rows are
+// 16-byte aligned in the flat arena (C % 4 == 0, offset % 4 == 0); otherwise the arena
+// side is accessed element-wise (slabs are always padded and aligned).
+template <typename T, bool VEC4>
+__device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
+                                            const Scalars& sc, float (*tile)[ADAM_TILE_R + 1]) {
+  const int tid = threadIdx.x;
+  const int c4 = tid & 7, rb = tid >> 3;
+  const int cl = 4 * c4;
+  const int gc = item.c0 + cl;
+  constexpr int NR = ADAM_TILE_R / 32;
+  bool ok[NR];
+  int64_t e[NR];
+  float w[NR][4], g[NR][4], m[NR][4], v[NR][4];
+  auto ld4 = [&](const float* base, int i, float (&dst)[4]) {
+    if (VEC4) {
+      const float4 t = ok[i] ? *reinterpret_cast<const float4*>(base + e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      dst[0] = t.x, dst[1] = t.y, dst[2] = t.z, dst[3] = t.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = (ok[i] && gc + j < seg.C) ? base[e[i] + j] : 0.f;
+    }
+  };
+  auto st4 = [&](float* base, int i, const float (&src)[4]) {
+    if (!ok[i]) return;
+    if (VEC4) {
+      *reinterpret_cast<float4*>(base + e[i]) = make_float4(src[0], src[1], src[2], src[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (gc + j < seg.C) base[e[i] + j] = src[j];
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int gr = item.r0 + rb + 32 * i;
+    ok[i] = gr < seg.R && gc < seg.C;
+    e[i] = seg.off + (int64_t)(ok[i] ? gr : 0) * seg.C + (ok[i] ? gc : 0);
+    ld4(a.params, i, w[i]);
+  }
+  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
+  if (adam) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      ld4(a.exp_avg, i, m[i]);
+      ld4(a.exp_avg_sq, i, v[i]);
+    }
+  }
+  if (a.grad_src == GRAD_FLAT) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) ld4(a.grads, i, g[i]);
+  } else if (a.grad_src == GRAD_SLABS) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[i][j] = 0.f;
+    const float* base = seg.slab + gc;
+    const int ns = seg.nslab;
+#pragma unroll 1
+    for (int k0 = 0; k0 < ns; k0 += 8) {
+      float4 t[8][NR];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float* sk = base + (int64_t)min(k0 + q, ns - 1) * seg.slab_stride;
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+          t[q][i] = ok[i] ? *reinterpret_cast<const float4*>(sk + (int64_t)(item.r0 + rb + 32 * i) * seg.slab_ld)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      // fixed order: partial 0, 1, ..., ns-1
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (k0 + q < ns) {
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            g[i][0] += t[q][i].x;
+            g[i][1] += t[q][i].y;
+            g[i][2] += t[q][i].z;
+            g[i][3] += t[q][i].w;
+          }
+        }
+      }
+    }
+  }
+  if (a.grad_src != GRAD_NONE) {
+    if (a.write_grads) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) st4(a.grads, i, g[i]);
+    }
+    if (adam) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) adam_elem(w[i][j], m[i][j], v[i][j], g[i][j], a, sc);
+        st4(a.params, i, w[i]);
+        st4(a.exp_avg, i, m[i]);
+        st4(a.exp_avg_sq, i, v[i]);
+      }
+    }
+  }
+  if (!a.write_shadow) return;
+  // packed row-major shadow: 4 consecutive columns per store (padded columns stay zero)
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = rb + 32 * i;
+    if (ok[i]) {
+      T* dst = reinterpret_cast<T*>(seg.W) + (int64_t)(item.r0 + r) * seg.ldw + gc;
+      if (VEC4) {
+        if constexpr (sizeof(T) == 2) {
+          const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
+          *reinterpret_cast<bf16x4*>(dst) = pk;
+        } else {
+          *reinterpret_cast<float4*>(dst) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (gc + j < seg.C) dst[j] = (T)w[i][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[cl + j][r] = w[i][j];
+  }
+  __syncthreads();
+  // packed transposed shadow: 64 consecutive rows of one column per wave
+#pragma unroll
+  for (int i = 0; i < ADAM_TILE_R * ADAM_TILE_C / 256; ++i) {
+    const int idx = tid + 256 * i;
+    const int cc = idx / ADAM_TILE_R, r = idx % ADAM_TILE_R;
+    const int gr = item.r0 + r, gcc = item.c0 + cc;
+    if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
-  __shared__ float tile[64][65];
+  __shared__ float tile[ADAM_TILE_C][ADAM_TILE_R + 1];
   __shared__ Scalars sc;
   const AdamItem item = a.items[blockIdx.x];
   const AdamSeg seg = a.segs[item.seg];
@@ -53,76 +190,10 @@ __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   if (a.do_adam) __syncthreads();
 
   if (seg.matrix) {
-    // 16 elements per thread; every load of a phase is issued before its first use so
-    // one thread keeps 16 (slab sum) or 48 (Adam state) loads in flight
-    const int r0 = item.r0, c0 = item.c0;
-    const int c = tid & 63;
-    const int rb = tid >> 6;  // rows rb, rb+4, ..., rb+60
-    const int gc = c0 + c;
-    bool ok[16];
-    int64_t e[16];
-    float w[16], g[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int gr = r0 + rb + 4 * i;
-      ok[i] = gr < seg.R && gc < seg.C;
-      e[i] = seg.off + (int64_t)(ok[i] ? gr : 0) * seg.C + (ok[i] ? gc : 0);
-      w[i] = ok[i] ? a.params[e[i]] : 0.f;
-    }
-    if (a.grad_src == GRAD_FLAT) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) g[i] = ok[i] ? a.grads[e[i]] : 0.f;
-    } else if (a.grad_src == GRAD_SLABS) {
-      const float* base = seg.slab + gc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) g[i] = ok[i] ? base[(int64_t)(r0 + rb + 4 * i) * seg.slab_ld] : 0.f;
-#pragma unroll 1
-      for (int k = 1; k < seg.nslab; ++k) {
-        const float* sk = base + (int64_t)k * seg.slab_stride;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (ok[i]) g[i] += sk[(int64_t)(r0 + rb + 4 * i) * seg.slab_ld];
-      }
-    }
-    if (a.grad_src != GRAD_NONE) {
-      if (a.write_grads) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (ok[i]) a.grads[e[i]] = g[i];
-      }
-      if (a.do_adam) {
-        float m[16], v[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          m[i] = ok[i] ? a.exp_avg[e[i]] : 0.f;
-          v[i] = ok[i] ? a.exp_avg_sq[e[i]] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (ok[i]) {
-            adam_elem(w[i], m[i], v[i], g[i], a, sc);
-            a.params[e[i]] = w[i];
-            a.exp_avg[e[i]] = m[i];
-            a.exp_avg_sq[e[i]] = v[i];
-          }
-        }
-      }
-    }
-    if (!a.write_shadow) return;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = rb + 4 * i;
-      if (ok[i]) reinterpret_cast<T*>(seg.W)[(int64_t)(r0 + r) * seg.ldw + gc] = (T)w[i];
-      tile[c][r] = w[i];
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int idx = tid + 256 * i;
-      const int cc = idx >> 6, r = idx & 63;
-      const int gr = r0 + r, gcc = c0 + cc;
-      if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
-    }
+    if (item.pad & ITEM_VEC4)
+      matrix_tile<T, true>(a, seg, item, sc, tile);
+    else
+      matrix_tile<T, false>(a, seg, item, sc, tile);
   } else {
     // vector chunk: 8 elements x 32 lanes
     const int el = tid >> 5, j = tid & 31;

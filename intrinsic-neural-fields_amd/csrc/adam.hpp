@@ -21,10 +21,15 @@ struct AdamSeg {
   int64_t ldwt;
 };
 
+// Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = 8 elements.
+constexpr int ADAM_TILE_R = 64;
+constexpr int ADAM_TILE_C = 32;
+constexpr int ITEM_VEC4 = 1;  // AdamItem.pad flag: 16-byte aligned rows in the arena
+
 struct AdamItem {
   int32_t seg;
   int32_t r0, c0;
-  int32_t pad;
+  int32_t pad;  // flags
 };
 
 struct AdamArgs {

@@ -201,7 +201,7 @@ int build_layout(inf_plan* p) {
 
   // update work list
   int64_t nitems = 0;
-  for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, 64) * ceil_div(g.C, 64) : ceil_div((int64_t)g.R * g.C, 8);
+  for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, ADAM_TILE_R) * ceil_div(g.C, ADAM_TILE_C) : ceil_div((int64_t)g.R * g.C, 8);
   p->table_bytes = align_up((int64_t)p->segs.size() * sizeof(AdamSeg)) + align_up(nitems * sizeof(AdamItem));
   p->o_tables = take(p->table_bytes);
   p->o_ws_end = w;
@@ -687,8 +687,9 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
       a.ldw = g.c_pad;
       a.WT = p->shadow + g.wt_off;
       a.ldwt = g.R;
-      for (int r = 0; r < g.R; r += 64)
-        for (int c = 0; c < g.C; c += 64) p->adam_items.push_back(AdamItem{(int32_t)i, r, c, 0});
+      const int flags = (g.C % 4 == 0 && g.off % 4 == 0) ? ITEM_VEC4 : 0;
+      for (int r = 0; r < g.R; r += ADAM_TILE_R)
+        for (int c = 0; c < g.C; c += ADAM_TILE_C) p->adam_items.push_back(AdamItem{(int32_t)i, r, c, flags});
     } else {
       a.R = 1;
       a.C = g.R * g.C;

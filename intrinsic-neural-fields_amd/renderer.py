@@ -80,11 +80,13 @@ class Renderer:
         bary = barycentric_coords.to(dev, torch.float32)
         hit = hit_ray_idxs.to(dev, torch.int64).contiguous()
         num_rays = hit.shape[0]
-        assert num_rays > 0
         M = self.H * self.W
         fill = 1.0 if self.background == "white" else 0.0
         assert self.background in ("white", "black")
         img = torch.full((M, 3), fill, dtype=torch.float32, device=dev)
+        if num_rays == 0:  # nothing hit: the reference's empty model call leaves the background
+            img = img.reshape(self.H, self.W, 3)
+            return img if return_tensor else img.cpu().numpy()
         pixel_map = None
         if obj_mask_1d is not None:
             assert obj_mask_1d.dtype == torch.bool

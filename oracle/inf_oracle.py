@@ -76,8 +76,8 @@ def _sigmoid(z):
 
 def mlp_forward(w: dict, x: np.ndarray, num_layers: int, skip: int):
     """model.py:98-112 TextureField.forward with layers.py:60-62 at the skip layer.
-    Returns (pred[B,3], cache) where cache holds each layer's input and output."""
-    cache = {"x": x, "in": [], "out": []}
+    Returns (pred[B,3], cache) where cache holds each layer's input, pre-activation and output."""
+    cache = {"x": x, "in": [], "z": [], "out": []}
     h = x
     for i in range(num_layers):
         cache["in"].append(h)
@@ -91,6 +91,7 @@ def mlp_forward(w: dict, x: np.ndarray, num_layers: int, skip: int):
         else:
             z = h @ w[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
             h = np.maximum(z, 0)
+        cache["z"].append(z)
         cache["out"].append(h)
     return h.astype(x.dtype, copy=False), cache
 

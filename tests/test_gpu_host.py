@@ -172,6 +172,10 @@ def test_renderer_render_hits_matches_reference():
     r.ray_tracer = lambda *a, **k: (torch.from_numpy(d["vids_full"]), torch.from_numpy(d["bary_full"]),
                                     torch.from_numpy(d["hit_full"]))
     np.testing.assert_allclose(r.render(None, None), d["img_full"], atol=1e-5)
+    # no hits: the background survives (the reference's model call on an empty batch)
+    empty = r.render_hits(torch.zeros((0, 3), dtype=torch.int64), torch.zeros((0, 3)),
+                          torch.zeros((0,), dtype=torch.int64))
+    assert empty.shape == (H, W, 3) and (empty == 1.0).all()
 
 
 def _g8_trainer(tmp_path, mode, epochs=12):

@@ -20,7 +20,7 @@ def short(name):
             tail = ""
             if key == "gemm_nt_kernel":
                 tail = "<128x128>" if ("128ELi128" in name or "128, 128" in name) else "<64x64>"
-                tail = ("<bf16" if ("DF16b" in name or "bf16" in name.lower()) else "<f32") + tail[1:] if tail else tail
+                tail = ("<bf16," if ("DF16b" in name or "bf16" in name.lower()) else "<f32,") + tail[1:] if tail else tail
             if key == "chain_kernel":
                 for t in ("256, 64, 64", "256, 128, 32", "128, 64, 64", "128, 128, 32", "Li256ELi64", "Li256ELi128",
                           "Li128ELi64", "Li128ELi128"):
@@ -32,7 +32,8 @@ def short(name):
 
 
 def stats(d):
-    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True) or \
+        glob.glob(os.path.join(d, "*kernel_stats.csv"))
     out = {}
     if not f:
         return out
@@ -59,7 +60,8 @@ def counters(d, counter):
 
 
 def main(root):
-    res = {"kernels": stats(os.path.join(root, "trace"))}
+    tdir = os.path.join(root, "trace")
+    res = {"kernels": stats(tdir if os.path.isdir(tdir) else root)}
     fetch = counters(os.path.join(root, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(root, "write"), "WRITE_SIZE")
     for k, e in res["kernels"].items():
