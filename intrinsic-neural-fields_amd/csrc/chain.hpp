@@ -62,9 +62,20 @@ struct ChainArgs {
 
 // Supported hidden widths of the fused chain (others use the layered path).
 inline bool chain_supported(int H) { return H == 128 || H == 256; }
-// Ray-tile height used for a padded batch.
-inline int chain_bm(int64_t rows) { return rows >= 32768 ? 128 : 64; }
-inline int chain_bk(int bm) { return bm == 128 ? 32 : 64; }
+// Ray-tile height for a padded batch: about one workgroup per CU while the batch is
+// small (every workgroup streams all weights, so more tiles = more CUs streaming), then
+// taller tiles that do more MFMA work per streamed weight byte.
+inline int chain_bm(int64_t rows) {
+  if (rows <= 4096) return 16;
+  if (rows <= 8192) return 32;
+  if (rows <= 16384) return 64;
+  return 128;
+}
+inline int chain_bk(int bm) { return bm >= 64 ? 32 : 64; }
+// Rays per bias-gradient / output-layer partial written by the chain.
+inline int chain_partial_rows(int bm) { return bm >= 64 ? 64 : bm; }
+// Upper bound on the chain's partial count for padded batches up to bp_max.
+inline int64_t chain_max_partials(int64_t bp_max) { return bp_max / 64 > 256 ? bp_max / 64 : 256; }
 
 int launch_chain(const ChainArgs& a, int bm, hipStream_t stream);
 

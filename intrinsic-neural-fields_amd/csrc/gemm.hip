@@ -55,7 +55,12 @@ struct Tile {
 
   static constexpr int A_CHUNKS = BM * 8 / 256;  // 16-byte chunks per thread per k-tile
   static constexpr int B_CHUNKS = BN * 8 / 256;
-  static constexpr int STAGES = (BM == 128 && BN == 128) ? 3 : 4;
+#ifndef INF_GEMM128_STAGES
+#define INF_GEMM128_STAGES 2
+#endif
+  // 128x128: 2 stages (64 KiB, under the 67.6 KiB C staging tile) keep two workgroups per
+  // CU; the 64x64 tile affords 4 stages (64 KiB) at the same occupancy
+  static constexpr int STAGES = (BM == 128 && BN == 128) ? INF_GEMM128_STAGES : 4;
   static constexpr int STAGE_BYTES = (BM + BN) * 128;
   static constexpr int OPER_BYTES = STAGES * STAGE_BYTES;
   static constexpr int CLD = BN + 4;  // fp32 C staging row stride

@@ -185,7 +185,7 @@ int build_layout(inf_plan* p) {
     p->o_yt.push_back(take(Bp * H * p->esz));
     p->o_dZ.push_back(take(Bp * H * p->esz));
     p->o_dZT.push_back(take(Bp * H * p->esz));
-    const int64_t parts = std::max<int64_t>(Bp / 64, p->grid_hb);
+    const int64_t parts = std::max<int64_t>(chain_max_partials(Bp), p->grid_hb);
     p->o_colsum.push_back(take(parts * H * 4));
   }
   p->o_dz = take(Bp * 3 * 4);
@@ -195,7 +195,7 @@ int build_layout(inf_plan* p) {
     const auto& g = p->segs[i];
     if (g.gemm) p->o_slab[i] = take((int64_t)S * g.R * g.c_pad * 4);
   }
-  const int64_t head_parts = std::max<int64_t>(p->grid_hb, Bp / 64);
+  const int64_t head_parts = std::max<int64_t>(p->grid_hb, chain_max_partials(Bp));
   p->o_hw = take(head_parts * 3 * H * 4);
   p->o_hb = take(head_parts * 3 * 4);
 
@@ -385,7 +385,7 @@ AdamArgs update_args(inf_plan* p, int Bp) {
 
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, bool chain = false) {
-  const int parts = Bp / 64;
+  const int parts = chain ? Bp / chain_partial_rows(chain_bm(Bp)) : Bp / 64;
   bool changed = false;
   for (size_t i = 0; i < p->segs.size(); ++i) {
     const ParamSeg& g = p->segs[i];
@@ -483,7 +483,7 @@ bool use_chain(const inf_plan* p) {
 int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, const int64_t* hit,
               const int64_t* pixel_map, float* img, hipStream_t st) {
   const int H = p->H, L = p->L, s = p->s;
-  const int bm = chain_bm(Bp) <= Bp && Bp % chain_bm(Bp) == 0 ? chain_bm(Bp) : 64;
+  const int bm = chain_bm(Bp);
   const int BK = chain_bk(bm);
   ChainArgs a;
   std::memset(&a, 0, sizeof(a));
