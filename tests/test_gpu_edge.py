@@ -88,7 +88,9 @@ def test_fp32_train_steps_any_architecture(k, H, L, s, B, loss):
                          torch.from_numpy(rgb).cuda())
     plan, params = plan_for(k, H, L, s, w0, "fp32", loss, B)
     plan.set_lr(5e-4)
-    perm = torch.randperm(N, device="cuda")
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(B)
+    perm = torch.randperm(N, device="cuda", generator=gen)
     pidx = perm.cpu().numpy()
     tr = O.OracleTrainer(w0, L, s, 5e-4, loss)
     kinks = 0
@@ -105,7 +107,10 @@ def test_fp32_train_steps_any_architecture(k, H, L, s, B, loss):
     got = arena_to_dict(params, w0, L, s)
     print("relu kinks", kinks)
     for n in O.layer_names(L, s):
-        assert_adam_close(got[n], tr.w[n], lr=5e-4, steps=3, name=n, frac=1e-3 if kinks == 0 else 2e-2)
+        if kinks == 0:
+            assert_adam_close(got[n], tr.w[n], lr=5e-4, steps=3, name=n)
+        else:  # a flipped kink shifts one ray's contribution: <= 2 % of elements off by > 10 % of a step
+            assert_adam_close(got[n], tr.w[n], lr=5e-4, steps=3, name=n, atol=5e-5, frac=2e-2)
 
 
 @pytest.mark.parametrize("k,H,L,s,B,loss", ARCHS)
