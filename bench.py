@@ -95,10 +95,12 @@ class Trainer:
         self.graphs = None
         self.i = 0
 
+    GRAPH_STEPS = 8  # steps per replayed graph on one GPU (divides nb)
+
     def _launch(self):
         if self.world == 1:
-            self.plan.train_step(self.batch, None, apply_adam=True)
-            self.plan.ctrl_advance()
+            # Adam + the batch-index advance ride in the step's update launch
+            self.plan.train_step(self.batch, None, apply_adam=True, advance=True)
         else:
             self.plan.train_step(self.batch, None, apply_adam=False)
 
@@ -113,14 +115,20 @@ class Trainer:
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1, stream=s):
                 self._launch()
-            g2 = None
+            g2 = gm = None
             if self.world > 1:
                 g2 = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g2, stream=s):
                     self.plan.adam(0, 0.0)
                     self.plan.ctrl_advance()
+            else:
+                # several steps per graph: one replay launch per GRAPH_STEPS steps
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm, stream=s):
+                    for _ in range(self.GRAPH_STEPS):
+                        self._launch()
         torch.cuda.current_stream().wait_stream(s)
-        self.graphs = (g1, g2)
+        self.graphs = (g1, g2, gm)
         self.plan.set_batch_index(0)
         self.i = 0
 
@@ -142,25 +150,36 @@ class Trainer:
         if self.graphs is None:
             return self.step_eager()
         self._wrap()
-        g1, g2 = self.graphs
+        g1, g2, _ = self.graphs
         g1.replay()
         if g2 is not None:
             torch.distributed.all_reduce(self.plan.grads)
             g2.replay()
         self.i += 1
 
+    def run(self, n):
+        """n training steps (multi-step graph replays where they fit the epoch)."""
+        gm = self.graphs[2] if self.graphs is not None else None
+        while n > 0:
+            self._wrap()
+            if gm is not None and n >= self.GRAPH_STEPS and self.i + self.GRAPH_STEPS <= self.nb:
+                gm.replay()
+                self.i += self.GRAPH_STEPS
+                n -= self.GRAPH_STEPS
+            else:
+                self.step()
+                n -= 1
+
 
 def time_steps(tr, steps, warmup, world):
-    for _ in range(warmup):
-        tr.step()
+    tr.run(warmup)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
-    for _ in range(steps):
-        tr.step()
+    tr.run(steps)
     e1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0

@@ -146,11 +146,15 @@ int inf_forward(inf_plan* plan, const inf_batch* batch, float* pred, int save, i
 int inf_backward(inf_plan* plan, const float* dpred, float* grads, inf_stream_t stream);
 
 /* Fused training step (trainer.py:71-84 + loss config.py:113-122):
- * gather -> forward -> loss -> backward -> gradient reduction, and, if
- * apply_adam != 0, the Adam update (torch.optim.Adam, config.py:108).  With
- * apply_adam == 0 the reduced gradient is left in `grads` for a cross-GPU
- * all-reduce followed by inf_adam().  pred may be NULL.  Loss sums go to ctrl. */
-int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int apply_adam,
+ * gather -> forward -> loss -> backward -> gradient reduction, and, with
+ * INF_STEP_ADAM in `flags`, the Adam update (torch.optim.Adam, config.py:108).
+ * Without it the reduced gradient is left in `grads` for a cross-GPU all-reduce
+ * followed by inf_adam().  INF_STEP_ADVANCE also advances ctrl->batch_index by one
+ * at the end of the step (a graph-replayed epoch; same as a following
+ * inf_ctrl_advance).  pred may be NULL.  The step's loss / SSE sums are stored in
+ * ctrl->loss_sum / sse_sum and added to the epoch sums. */
+enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2 };
+int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int flags,
                    inf_stream_t stream);
 
 /* Adam update from the bound `grads` arena (optim.step(), trainer.py:82).  step > 0
@@ -184,6 +188,12 @@ int inf_run_stage(inf_plan* plan, const inf_batch* batch, int stage, int layer, 
  * byte ranges [lo, hi) (n pairs) and a result buffer; the fused chain then checks every
  * global access against them and records violations instead of issuing them. */
 int inf_debug_ranges(inf_plan* plan, const uint64_t* ranges_dev, int n, unsigned long long* out_dev);
+
+/* Diagnostics: when `stamps_dev` is non-null, the fused chain of workgroups 0 and the last
+ * records the 100 MHz wall clock (s_memrealtime) at every flat k-step once its stage has
+ * landed: stamps_dev[w * (max_steps + 1) + s], w = 0 (first) / 1 (last), entry max_steps
+ * = the kernel's end.  Pass null to turn it off. */
+int inf_debug_timing(inf_plan* plan, unsigned long long* stamps_dev, int max_steps);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

@@ -169,11 +169,47 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
   }
 }
 
+// End-of-step item: loss / SSE partials (one per chain tile) summed in a fixed order, so
+// the epoch loss is bitwise reproducible (unlike per-tile atomics), then the step's sums
+// are stored and added to the epoch sums; optionally the replayed batch index advances.
+__device__ void finish_step(const AdamArgs& a) {
+  __shared__ double rl[256], rs[256];
+  const int tid = threadIdx.x;
+  double l = 0.0, s = 0.0;
+  for (int i = tid; i < a.nloss; i += 256) {
+    l += a.loss_part[2 * i];
+    s += a.loss_part[2 * i + 1];
+  }
+  rl[tid] = l;
+  rs[tid] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) {
+      rl[tid] += rl[tid + w];
+      rs[tid] += rs[tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (a.nloss > 0) {
+      a.ctrl->loss_sum = rl[0];
+      a.ctrl->sse_sum = rs[0];
+      a.ctrl->epoch_loss += rl[0];
+      a.ctrl->epoch_sse += rs[0];
+    }
+    if (a.advance) a.ctrl->batch_index += 1;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   __shared__ float tile[ADAM_TILE_C][ADAM_TILE_R + 1];
   __shared__ Scalars sc;
   const AdamItem item = a.items[blockIdx.x];
+  if (item.seg < 0) {
+    if ((a.nloss > 0 || a.advance) && a.ctrl != nullptr) finish_step(a);
+    return;
+  }
   const AdamSeg seg = a.segs[item.seg];
   const int tid = threadIdx.x;
 

@@ -46,7 +46,12 @@ struct AdamArgs {
   int32_t write_shadow;
   int32_t step_host;    // > 0: use this t, else ctrl->step
   float lr_host;        // > 0: use this lr, else ctrl->lr
-  const inf_ctrl* ctrl;
+  inf_ctrl* ctrl;
+  // end-of-step item (AdamItem.seg < 0): fixed-order sum of the fused chain's per-tile
+  // loss / SSE partials into ctrl, and the batch-index advance of a replayed epoch
+  const double* loss_part;  // [nloss][2]
+  int32_t nloss;
+  int32_t advance;
   double beta1_d, beta2_d;
   float one_minus_b1, beta2, one_minus_b2, eps;
 };

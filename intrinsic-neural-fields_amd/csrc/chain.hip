@@ -93,6 +93,14 @@ __device__ __forceinline__ int stage_off(int row, int c) {
   return row * (BK * 2) + ((c ^ stage_swz<BK>(row)) << 4);
 }
 
+// Y^T / dZ^T as the chain writes them: 16-ray blocks, element (col, ray b) at
+// (b / 16) * (H * 16) + col * 16 + b % 16 -- one 16-ray tile fills whole 128-byte lines
+// (the dW GEMM reads this layout through GemmProblem::a_kblk / b_kblk).
+template <int H>
+__device__ __forceinline__ int64_t tofs(int col, int b) {
+  return (int64_t)(b >> 4) * (H * 16) + col * 16 + (b & 15);
+}
+
 template <int H>
 __device__ __forceinline__ int act_off(int row, int col) {  // byte offset of element (row, col)
   return row * (H * 2) + (((col >> 3) ^ (row & 15)) << 4) + ((col & 7) << 1);
@@ -292,8 +300,8 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
             if (lane == 0) *mask_word(l, i, j, r) = bits;
           }
         }
-        if (yt != nullptr && GOK(yt + (int64_t)col * a.ldt + b0 + row, 8, 6))
-          *reinterpret_cast<u16x4*>(yt + (int64_t)col * a.ldt + b0 + row) = q;
+        if (yt != nullptr && GOK(yt + tofs<H>(col, b0 + row), 8, 6))
+          *reinterpret_cast<u16x4*>(yt + tofs<H>(col, b0 + row)) = q;
       }
     }
   };
@@ -318,8 +326,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
           q[r] = bf_bits(v);
           if (keep) *reinterpret_cast<unsigned short*>(act + act_off<H>(row + r, col)) = q[r];
         }
-        if (GOK(dzt + (int64_t)col * a.ldt + b0 + row, 8, 8))
-          *reinterpret_cast<u16x4*>(dzt + (int64_t)col * a.ldt + b0 + row) = q;
+        if (GOK(dzt + tofs<H>(col, b0 + row), 8, 8)) *reinterpret_cast<u16x4*>(dzt + tofs<H>(col, b0 + row)) = q;
       }
       cs += __shfl_xor(cs, 16, 64);
       cs += __shfl_xor(cs, 32, 64);
@@ -390,7 +397,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
         dzs[ray * 3 + part] = dz;
       }
     }
-    if (a.train && a.ctrl != nullptr) {
+    if (a.train && a.loss_part != nullptr) {
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) {
         lsum += __shfl_xor(lsum, o, 64);
@@ -406,16 +413,18 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
   // dZ_{L-2}, output-layer partial gradients, bias partials: one thread per column and
   // PR-row group
   auto head_bwd = [&]() {
-    if (a.ctrl != nullptr && tid == 0) {
+    // per-tile partials (summed in a fixed order by the update launch's end-of-step item:
+    // no same-address atomics from every workgroup, which the in-order vmcnt would wait on)
+    if (a.loss_part != nullptr && tid == 0) {
       double L_ = 0, S_ = 0;
       for (int w = 0; w < C::NW; ++w) {
         L_ += red[w];
         S_ += red[16 + w];
       }
-      if (GOK(&a.ctrl->epoch_sse, 8, 14)) atomicAdd(&a.ctrl->loss_sum, L_);
-      atomicAdd(&a.ctrl->sse_sum, S_);
-      atomicAdd(&a.ctrl->epoch_loss, L_);
-      atomicAdd(&a.ctrl->epoch_sse, S_);
+      if (GOK(a.loss_part + 2 * blockIdx.x + 1, 8, 14)) {
+        a.loss_part[2 * blockIdx.x] = L_;
+        a.loss_part[2 * blockIdx.x + 1] = S_;
+      }
     }
     if (tid < H * C::WR) {
       const int k = tid % H, rg = tid / H;
@@ -453,12 +462,14 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
       u16x8 v;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = *reinterpret_cast<const unsigned short*>(act + act_off<H>(q * 8 + e, k));
-      if (GOK(dzt + (int64_t)k * a.ldt + b0 + q * 8, 16, 18))
-        *reinterpret_cast<u16x8*>(dzt + (int64_t)k * a.ldt + b0 + q * 8) = v;
+      if (GOK(dzt + tofs<H>(k, b0 + q * 8), 16, 18)) *reinterpret_cast<u16x8*>(dzt + tofs<H>(k, b0 + q * 8)) = v;
     }
   };
 
   // ---- main loop over flat k-steps -------------------------------------------------------
+  unsigned long long* stamp = nullptr;
+  if (a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    stamp = a.stamps + (blockIdx.x == 0 ? 0 : a.stamp_steps + 1);
   zero_acc();
   const int nsteps = a.nsteps;
 #pragma unroll
@@ -473,6 +484,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
     int n = 0;
     for (int d = 1; d <= ahead; ++d) n += C::W_INS + (((xbits >> ((step + d) % NS)) & 1u) ? xw : 0);
     wait_vm_barrier<C::MAXWAIT>(n);
+    if (stamp != nullptr && step < a.stamp_steps) stamp[step] = wall_clock64();
     if (step + NS - 1 < nsteps) issue(step + NS - 1);
     const ChainPhase& P = a.ph[p];
     compute(step % NS, P.a_src != 0, step - P.step0);
@@ -498,6 +510,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
       ++p;
     }
   }
+  if (stamp != nullptr) stamp[a.stamp_steps] = wall_clock64();
 }
 
 template <int H, int BM, int BK, int NS>

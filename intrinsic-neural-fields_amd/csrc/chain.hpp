@@ -47,6 +47,7 @@ struct ChainArgs {
   int32_t loss;
   float inv_count;
   inf_ctrl* ctrl;
+  double* loss_part;              // [rows/BM][2] per-tile loss / SSE sums (train)
   const int64_t* hit;
   const int64_t* pixel_map;
   float* img;
@@ -58,6 +59,9 @@ struct ChainArgs {
   const uint64_t* dbg_ranges;
   int32_t dbg_nranges;
   unsigned long long* dbg_out;  // [0] count, then (site, address) pairs
+  // diagnostics (any build): per-step wall-clock stamps of the first and last workgroup
+  unsigned long long* stamps;
+  int32_t stamp_steps;
 };
 
 // Supported hidden widths of the fused chain (others use the layered path).

@@ -174,23 +174,29 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
     const int buf = (t - t_begin) % STAGES;
     const int seg = t < kt0 ? 0 : 1;
     const int k0 = (seg == 0 ? t : t - kt0) * BK;
-    const char* A = reinterpret_cast<const char*>(reinterpret_cast<const T*>(P.A[seg]) + k0);
-    const char* Bm = reinterpret_cast<const char*>(reinterpret_cast<const T*>(P.B[seg]) + k0);
-    const int64_t lda = P.lda[seg] * (int64_t)sizeof(T), ldb = P.ldb[seg] * (int64_t)sizeof(T);
     char* As = smem + buf * TL::STAGE_BYTES;
     char* Bs = As + BM * 128;
+    // byte offset of 16-byte chunk c (element k0 + c*EPC) of operand row r
+    constexpr int EPC = 16 / sizeof(T);
+    auto chunk_off = [&](int64_t ld, bool kblk, int64_t r, int c) -> int64_t {
+      const int64_t k = k0 + c * EPC;
+      return (kblk ? (k >> 4) * ld + r * 16 + (k & 15) : r * ld + k) * (int64_t)sizeof(T);
+    };
+    const bool akb = seg == 0 && P.a_kblk, bkb = seg == 0 && P.b_kblk;
+    const char* A = reinterpret_cast<const char*>(P.A[seg]);
+    const char* Bm = reinterpret_cast<const char*>(P.B[seg]);
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
       const int r0 = wv * (BM / 4) + i * 8;
       const int row = r0 + lrow;
-      const char* src = A + (int64_t)(m0 + row) * lda + (swz_slot(row, lslot) << 4);
+      const char* src = A + chunk_off(P.lda[seg], akb, m0 + row, swz_slot(row, lslot));
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(As + r0 * 128), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       const int r0 = wv * (BN / 4) + i * 8;
       const int row = r0 + lrow;
-      const char* src = Bm + (int64_t)(n0 + row) * ldb + (swz_slot(row, lslot) << 4);
+      const char* src = Bm + chunk_off(P.ldb[seg], bkb, n0 + row, swz_slot(row, lslot));
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(Bs + r0 * 128), 16, 0, 0);
     }
   };

@@ -21,6 +21,10 @@ struct GemmProblem {
   const void* B[2];
   int64_t lda[2];
   int64_t ldb[2];
+  // K-blocked operand (segment 0 only): element (row, k) at (k/16) * ld + row * 16 + k % 16,
+  // i.e. ld = rows * 16 -- the layout the fused chain writes Y^T / dZ^T in (whole 128-byte
+  // lines per 16-ray tile).  0: plain row-major row * ld + k.
+  int32_t a_kblk, b_kblk;
   int32_t K[2];  // per segment, multiple of the k-tile
   int32_t nseg;
   int32_t M, N;  // multiples of the block tile

@@ -64,6 +64,7 @@ struct inf_plan {
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
   std::vector<int64_t> o_slab;                            // per param segment (weights)
   int64_t o_hw = 0, o_hb = 0;                             // head partials
+  int64_t o_loss = 0;                                     // chain per-tile loss partials
   int64_t table_bytes = 0;
 
   // bound buffers
@@ -87,6 +88,8 @@ struct inf_plan {
   const uint64_t* dbg_ranges = nullptr;
   int dbg_n = 0;
   unsigned long long* dbg_out = nullptr;
+  unsigned long long* stamps = nullptr;
+  int stamp_steps = 0;
 
   template <typename T = char>
   T* W(int64_t off) const { return reinterpret_cast<T*>(ws + off); }
@@ -198,9 +201,10 @@ int build_layout(inf_plan* p) {
   const int64_t head_parts = std::max<int64_t>(p->grid_hb, chain_max_partials(Bp));
   p->o_hw = take(head_parts * 3 * H * 4);
   p->o_hb = take(head_parts * 3 * 4);
+  p->o_loss = take(std::max<int64_t>(Bp / 16, 1) * 2 * 8);
 
   // update work list
-  int64_t nitems = 0;
+  int64_t nitems = 1;  // + the end-of-step item
   for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, ADAM_TILE_R) * ceil_div(g.C, ADAM_TILE_C) : ceil_div((int64_t)g.R * g.C, 8);
   p->table_bytes = align_up((int64_t)p->segs.size() * sizeof(AdamSeg)) + align_up(nitems * sizeof(AdamItem));
   p->o_tables = take(p->table_bytes);
@@ -292,7 +296,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
   return INF_OK;
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st);
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, bool chain = false);
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
@@ -327,7 +331,8 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
   return run_weight_grads(p, Bp, st);
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st) {
+// chain: Y^T / dZ^T were written by the fused chain in its 16-ray blocked layout
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, bool chain) {
   const int H = p->H, s = p->s;
   // weight gradients: one grouped split-K launch (chunks of GEMM_MAX_PROBLEMS)
   std::vector<GemmProblem> probs;
@@ -337,10 +342,12 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st) {
     GemmProblem q = blank_problem();
     const int l = g.layer;
     q.A[0] = p->W(p->o_dZT[l]);
-    q.lda[0] = Bp;
+    q.lda[0] = chain ? (int64_t)H * 16 : Bp;
+    q.a_kblk = chain ? 1 : 0;
     const bool from_input = (l == 0) || (l == s && g.sub == 1);
     q.B[0] = from_input ? (const void*)p->W(p->o_x0t) : (const void*)p->W(p->o_yt[l - 1]);
-    q.ldb[0] = Bp;
+    q.ldb[0] = (chain && !from_input) ? (int64_t)H * 16 : Bp;
+    q.b_kblk = (chain && !from_input) ? 1 : 0;
     q.K[0] = Bp;
     q.M = g.R;
     q.N = g.c_pad;
@@ -539,12 +546,15 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
   a.ldt = Bp;
   a.pred = pred;
   a.ctrl = p->ctrl;
+  a.loss_part = train ? p->W<double>(p->o_loss) : nullptr;
   a.hit = hit;
   a.pixel_map = pixel_map;
   a.img = img;
   a.dbg_ranges = p->dbg_ranges;
   a.dbg_nranges = p->dbg_n;
   a.dbg_out = p->dbg_out;
+  a.stamps = p->stamps;
+  a.stamp_steps = p->stamp_steps;
   a.train = train ? 1 : 0;
   a.save = train ? 1 : 0;
   a.count_step = train ? 1 : 0;
@@ -707,6 +717,7 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
     }
     p->adam_segs.push_back(a);
   }
+  p->adam_items.push_back(AdamItem{-1, 0, 0, 0});  // end-of-step: loss sums, batch advance
   const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
   INF_CHECK_ARG(seg_bytes + (int64_t)(p->adam_items.size() * sizeof(AdamItem)) <= p->table_bytes, "table size");
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
@@ -765,29 +776,35 @@ int inf_backward(inf_plan* p, const float* dpred, float* grads, inf_stream_t str
   return launch_update(a, p->mode, st);
 }
 
-int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int apply_adam, inf_stream_t stream) {
+int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, inf_stream_t stream) {
   if (p == nullptr || !p->bound) {
     set_error("plan not bound");
     return INF_ERR_STATE;
   }
+  const bool apply_adam = (flags & INF_STEP_ADAM) != 0;
+  INF_CHECK_ARG((flags & ~(INF_STEP_ADAM | INF_STEP_ADVANCE)) == 0, "train_step: unknown flags");
   INF_CHECK_ARG(batch != nullptr && batch->rgb != nullptr, "train_step: batch with target colours required");
   INF_CHECK_ARG(p->grads != nullptr || apply_adam, "train_step: grads not bound");
   INF_CHECK_ARG(!apply_adam || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr), "train_step: Adam state");
   hipStream_t st = (hipStream_t)stream;
-  INF_HIP_TRY(hipMemsetAsync(&p->ctrl->loss_sum, 0, 2 * sizeof(double), st));
   int rc;
   const bool chain = use_chain(p);
+  int nloss = 0;
   if (chain) {
+    // the chain leaves per-tile loss partials; the update launch stores their sum
     int Bp = 0;
     if ((rc = pad_batch(p, batch->batch, true, &Bp))) return rc;
     if ((rc = run_input(p, batch, Bp, true, st))) return rc;
     if ((rc = run_chain(p, batch, Bp, true, pred, nullptr, nullptr, nullptr, st))) return rc;
-    if ((rc = run_weight_grads(p, Bp, st))) return rc;
+    if ((rc = run_weight_grads(p, Bp, st, true))) return rc;
     p->saved = false;
     p->saved_batch = batch->batch;
     p->saved_bp = Bp;
     p->last_chain = true;
+    nloss = Bp / chain_bm(Bp);
   } else {
+    // the layered head accumulates the step's sums with atomics: clear them first
+    INF_HIP_TRY(hipMemsetAsync(&p->ctrl->loss_sum, 0, 2 * sizeof(double), st));
     p->last_chain = false;
     if ((rc = forward_impl(p, batch, pred, true, true, nullptr, nullptr, nullptr, st))) return rc;
     const int Bp0 = p->saved_bp;
@@ -804,6 +821,9 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int apply_a
   } else {
     a.write_grads = 1;
   }
+  a.loss_part = p->W<double>(p->o_loss);
+  a.nloss = nloss;
+  a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
   return launch_update(a, p->mode, st);
 }
 
@@ -860,7 +880,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       break;
     }
     case INF_STAGE_DW_GEMM: {
-      rc = run_weight_grads(p, Bp, st);
+      rc = run_weight_grads(p, Bp, st, p->last_chain);
       for (const auto& g : p->segs)
         if (g.gemm) {
           f += 2.0 * g.R * g.C * B;
@@ -900,6 +920,13 @@ int inf_debug_ranges(inf_plan* p, const uint64_t* ranges, int n, unsigned long l
   p->dbg_ranges = ranges;
   p->dbg_n = n;
   p->dbg_out = out;
+  return INF_OK;
+}
+
+int inf_debug_timing(inf_plan* p, unsigned long long* stamps, int max_steps) {
+  INF_CHECK_ARG(p != nullptr && max_steps >= 0, "debug timing");
+  p->stamps = stamps;
+  p->stamp_steps = max_steps;
   return INF_OK;
 }
 

@@ -21,6 +21,7 @@ LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
 LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
+STEP_ADAM, STEP_ADVANCE = 1, 2  # inf_train_step flags
 
 c_void_p, c_int, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int32,
                                                         ctypes.c_int64, ctypes.c_float, ctypes.c_double)
@@ -73,6 +74,7 @@ _SIGNATURES = {
     "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "inf_debug_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "inf_run_stage": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_int, ctypes.POINTER(c_double),
                               ctypes.POINTER(c_double), c_void_p]),
 }

@@ -11,7 +11,7 @@ import ctypes
 import torch
 
 from . import (CTRL_BYTES, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, LOSS_CODES, MODE_BF16, MODE_CODES, Batch,
-               MlpDesc, PlanInfo, c_int64, c_void_p, check, lib)
+               STEP_ADAM, STEP_ADVANCE, MlpDesc, PlanInfo, c_int64, c_void_p, check, lib)
 
 _TORCH_DTYPE = {DTYPE_F32: torch.float32, DTYPE_BF16: torch.bfloat16}
 _CODE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.int32: DTYPE_I32, torch.int64: DTYPE_I64}
@@ -221,9 +221,10 @@ class Plan:
     def backward(self, dpred: torch.Tensor, grads: torch.Tensor):
         check(lib.inf_backward(self.handle, ptr(dpred), ptr(grads), stream_handle()), "backward")
 
-    def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool):
-        check(lib.inf_train_step(self.handle, ctypes.byref(b), ptr(pred), 1 if apply_adam else 0, stream_handle()),
-              "train_step")
+    def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool, advance: bool = False):
+        """inf_train_step; advance=True also moves ctrl.batch_index on (graph-replayed epochs)."""
+        flags = (STEP_ADAM if apply_adam else 0) | (STEP_ADVANCE if advance else 0)
+        check(lib.inf_train_step(self.handle, ctypes.byref(b), ptr(pred), flags, stream_handle()), "train_step")
 
     def adam(self, step: int = 0, lr: float = 0.0):
         check(lib.inf_adam(self.handle, int(step), float(lr), stream_handle()), "adam")

@@ -53,13 +53,16 @@ def _summary_writer(log_dir):
 
 
 class _FusedEpoch:
-    """Replays one captured fused step per full batch of an epoch."""
+    """Replays captured fused steps (GRAPH_STEPS per graph launch, then single steps) over
+    the full batches of an epoch; the batch index advances on the device."""
 
     def __init__(self, trainer):
         self.t = trainer
         self.graph = None
         self.key = None
         self.perm = None
+
+    GRAPH_STEPS = 8
 
     def run(self, loader):
         t = self.t
@@ -88,8 +91,11 @@ class _FusedEpoch:
             optim.sync_runtime_state(model, rt, plan, group)
             plan.reset_epoch_sums()
             plan.set_batch_index(0)
-            for _ in range(full):
-                self.graph.replay()
+            g1, gm = self.graph
+            for _ in range(full // self.GRAPH_STEPS):
+                gm.replay()
+            for _ in range(full % self.GRAPH_STEPS):
+                g1.replay()
             optim.after_fused_steps(model, rt, group, full)
             done = full
             total = full * B
@@ -111,16 +117,19 @@ class _FusedEpoch:
         plan.train_step(b, None, apply_adam=True)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
+        g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                plan.train_step(b, None, apply_adam=True)
-                plan.ctrl_advance()
+            # the step's update launch also advances ctrl.batch_index (INF_STEP_ADVANCE)
+            with torch.cuda.graph(g1, stream=s):
+                plan.train_step(b, None, apply_adam=True, advance=True)
+            with torch.cuda.graph(gm, stream=s):  # GRAPH_STEPS steps per replay launch
+                for _ in range(self.GRAPH_STEPS):
+                    plan.train_step(b, None, apply_adam=True, advance=True)
         torch.cuda.current_stream().wait_stream(s)
         for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
             dst.copy_(src)
         plan.sync_shadow()
-        self.graph = g
+        self.graph = (g1, gm)
 
 
 class Trainer:
