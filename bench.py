@@ -193,6 +193,7 @@ def time_steps(tr, steps, warmup, world):
 
 
 def time_stage(plan, stage, reps=20, batch=None, layer=0):
+    plan.set_batch_index(0)  # stage replays read batch 0 of the epoch
     plan.run_stage(stage, layer, batch)  # warm
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

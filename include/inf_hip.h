@@ -84,6 +84,9 @@ typedef struct inf_batch {
   int32_t batch;         /* rays in this batch (<= max_batch)                         */
   int64_t loss_count;    /* elements of the loss mean (3 x global batch); 0 = 3*batch */
   int32_t loss;          /* INF_LOSS_* of a training call; -1 = the plan's desc.loss   */
+  int64_t num_rays;      /* entries of ray_idx (rows of vids/bary/rgb when ray_idx is  */
+                         /* null); rays past it read as zero features / targets.       */
+                         /* 0 = unchecked.  Vertex ids >= num_vertices read as zero.   */
 } inf_batch;
 
 /* Device-resident step state (lets a captured HIP graph replay a whole epoch). */

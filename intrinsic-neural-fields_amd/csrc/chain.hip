@@ -185,7 +185,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
     for (int i = tid; i < BM * 3; i += C::THREADS) {
       const int b = b0 + i / 3;
       float t = 0.f;
-      if (b < a.batch && a.rgb != nullptr) {
+      if (b < a.batch && a.rgb != nullptr && ray_in_range(offset, b, a.num_rays)) {
         const void* ip = a.idx_dtype == INF_DTYPE_I64 ? (const void*)((const int64_t*)a.ray_idx + offset + b)
                                                       : (const void*)((const int32_t*)a.ray_idx + offset + b);
         (void)ip;

@@ -56,6 +56,11 @@ __host__ __device__ constexpr inline int64_t round_up(int64_t x, int64_t m) { re
 __host__ __device__ constexpr inline int64_t ceil_div(int64_t x, int64_t m) { return (x + m - 1) / m; }
 
 // Index of ray b of a batch: ray_idx[offset + b] (int32/int64) or offset + b.
+// Ray b of a batch starting at entry `offset` exists (num_rays 0 = unchecked).
+__device__ __forceinline__ bool ray_in_range(int64_t offset, int b, int64_t num_rays) {
+  return num_rays <= 0 || (offset + b >= 0 && offset + b < num_rays);
+}
+
 __device__ __forceinline__ int64_t ray_row(const void* ray_idx, int idx_dtype, int64_t offset, int b) {
   if (ray_idx == nullptr) return offset + b;
   if (idx_dtype == INF_DTYPE_I64) return reinterpret_cast<const int64_t*>(ray_idx)[offset + b];
@@ -70,7 +75,7 @@ __device__ __forceinline__ int64_t vid_at(const void* vids, int vid_dtype, int64
 // ---- kernel launch wrappers (defined in the .hip files) --------------------------
 int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
                   int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
-                  const int32_t* ctrl_batch_index, int64_t ctrl_stride, int batch, void* out, int out_dtype,
+                  const int32_t* ctrl_batch_index, int64_t num_rays, int batch, void* out, int out_dtype,
                   int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream);
 
 // Pack fp32 features [B][ld_in] into the GEMM dtype [rows_out][ld_out] (+ transposed copy).

@@ -75,7 +75,8 @@ template <typename TabT, typename OutT, bool VEC>
 __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
     const TabT* __restrict__ table, int64_t V, int k, int64_t table_ld, const void* __restrict__ vids,
     int vid_dtype, const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype,
-    int64_t idx_offset, const int32_t* __restrict__ ctrl_batch_index, int batch, OutT* __restrict__ out,
+    int64_t idx_offset, const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int batch,
+    OutT* __restrict__ out,
     int64_t ld_out, int rows_out, OutT* __restrict__ out_t, int64_t ld_out_t) {
   __shared__ float tile[GT_COLS][GT_ROWS + 1];
 
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 
-  if (b < batch) {
+  if (b < batch && ray_in_range(offset, b, num_rays)) {
     const int64_t row = ray_row(ray_idx, idx_dtype, offset, b);
     const float w0 = bary[3 * row + 0];
     const float w1 = bary[3 * row + 1];
@@ -100,7 +101,10 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
     const int64_t v0 = vid_at(vids, vid_dtype, 3 * row + 0);
     const int64_t v1 = vid_at(vids, vid_dtype, 3 * row + 1);
     const int64_t v2 = vid_at(vids, vid_dtype, 3 * row + 2);
-    if (VEC) {
+    const bool vok = (uint64_t)v0 < (uint64_t)V && (uint64_t)v1 < (uint64_t)V && (uint64_t)v2 < (uint64_t)V;
+    if (!vok) {
+      // an out-of-range vertex id reads as a zero feature row (never outside the table)
+    } else if (VEC) {
       if (c0 < k) {  // k is a multiple of 16 on this path
         float e0[16], e1[16], e2[16];
         load16<TabT>(table + v0 * table_ld + c0, e0);
@@ -162,20 +166,20 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
 template <typename TabT, typename OutT>
 int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const void* vids, int vid_dtype,
                  const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_bi,
-                 int batch, void* out, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t,
-                 hipStream_t stream) {
+                 int64_t num_rays, int batch, void* out, int64_t ld_out, int rows_out, void* out_t,
+                 int64_t ld_out_t, hipStream_t stream) {
   dim3 grid((unsigned)ceil_div(rows_out, GT_ROWS), (unsigned)ceil_div(ld_out, GT_COLS));
   const bool vec = (k % 16 == 0) && (table_ld % 16 == 0) && (ld_out % 16 == 0) &&
                    (out_t == nullptr || ld_out_t % 16 == 0) && ((uintptr_t)table % 16 == 0) &&
                    ((uintptr_t)out % 16 == 0) && ((uintptr_t)out_t % 16 == 0);
   if (vec) {
     gather_kernel<TabT, OutT, true><<<grid, GT_THREADS, 0, stream>>>(
-        (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, batch,
-        (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
+        (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, num_rays,
+        batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
   } else {
     gather_kernel<TabT, OutT, false><<<grid, GT_THREADS, 0, stream>>>(
-        (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, batch,
-        (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
+        (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, num_rays,
+        batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
   }
   INF_LAUNCH_CHECK();
   return INF_OK;
@@ -185,7 +189,7 @@ int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const vo
 
 int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
                   int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
-                  const int32_t* ctrl_batch_index, int64_t /*ctrl_stride*/, int batch, void* out, int out_dtype,
+                  const int32_t* ctrl_batch_index, int64_t num_rays, int batch, void* out, int out_dtype,
                   int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
   INF_CHECK_ARG(table != nullptr && vids != nullptr && bary != nullptr, "gather: null input");
   INF_CHECK_ARG(k > 0 && table_ld >= k && V > 0, "gather: bad table shape");
@@ -201,15 +205,19 @@ int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t 
   INF_CHECK_ARG(of || out_dtype == INF_DTYPE_BF16, "gather: out dtype must be f32/bf16");
   if (tf && of)
     return launch_typed<float, float>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                      ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+                                      ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                      stream);
   if (tf && !of)
     return launch_typed<float, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                     ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+                                     ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                      stream);
   if (!tf && of)
     return launch_typed<bf16, float>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                     ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+                                     ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                      stream);
   return launch_typed<bf16, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                  ctrl_batch_index, batch, out, ld_out, rows_out, out_t, ld_out_t, stream);
+                                  ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                      stream);
 }
 
 // Features given by the caller (model(batch) with batch["eigenfunctions"], model.py:104):

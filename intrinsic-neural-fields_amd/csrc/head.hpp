@@ -22,6 +22,7 @@ struct HeadFwdArgs {
   const void* ray_idx;
   int32_t idx_dtype;
   int64_t idx_offset;
+  int64_t num_rays;     // bound on idx_offset + b (0 = unchecked)
   int32_t offset_from_ctrl;
   int32_t loss;
   float inv_count;      // 1 / (elements of the loss mean)

@@ -236,7 +236,7 @@ int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStrea
     const int64_t k_table = p->k_pad;  // device tables are packed with k_pad zero-filled columns
     return launch_gather(b->table, b->table_dtype, b->num_vertices, (int)k_table, k_table, b->vids, b->vid_dtype,
                          b->bary, b->ray_idx, b->idx_dtype, b->idx_offset,
-                         b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr, 0, b->batch, x0, dtype_of(p),
+                         b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr, b->num_rays, b->batch, x0, dtype_of(p),
                          p->k_pad, Bp, x0t, Bp, st);
   }
   INF_CHECK_ARG(b->features != nullptr, "batch has neither a table nor features");
@@ -441,6 +441,7 @@ int head_forward(inf_plan* p, const inf_batch* b, int Bp, float* pred, bool loss
     a.ray_idx = b->ray_idx;
     a.idx_dtype = b->idx_dtype;
     a.idx_offset = b->idx_offset;
+    a.num_rays = b->num_rays;
     a.offset_from_ctrl = b->offset_from_ctrl;
     a.loss = b->loss >= 0 ? b->loss : p->d.loss;
     INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
@@ -564,6 +565,7 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
     a.ray_idx = b->ray_idx;
     a.idx_dtype = b->idx_dtype;
     a.idx_offset = b->idx_offset;
+    a.num_rays = b->num_rays;
     a.offset_from_ctrl = b->offset_from_ctrl;
     a.loss = b->loss >= 0 ? b->loss : p->d.loss;
     INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");

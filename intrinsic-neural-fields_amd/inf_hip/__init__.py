@@ -43,7 +43,7 @@ class Batch(ctypes.Structure):
                 ("vids", c_void_p), ("vid_dtype", c_int32), ("bary", c_void_p), ("rgb", c_void_p),
                 ("ray_idx", c_void_p), ("idx_dtype", c_int32), ("idx_offset", c_int64),
                 ("offset_from_ctrl", c_int32), ("features", c_void_p), ("ld_features", c_int64),
-                ("batch", c_int32), ("loss_count", c_int64), ("loss", c_int32)]
+                ("batch", c_int32), ("loss_count", c_int64), ("loss", c_int32), ("num_rays", c_int64)]
 
 
 class Ctrl(ctypes.Structure):

@@ -206,6 +206,9 @@ class Plan:
             if ray_idx is not None:
                 b.ray_idx = ray_idx.data_ptr()
                 b.idx_dtype = dtype_code(ray_idx)
+                b.num_rays = ray_idx.numel()  # the kernels never read past the permutation
+            else:
+                b.num_rays = src.vids32.shape[0]
             b.idx_offset = int(offset)
             b.offset_from_ctrl = 1 if offset_from_ctrl else 0
             b.batch = int(batch)

@@ -171,3 +171,31 @@ def test_plan_rejects_bad_architectures():
     for args in [(64, 100, 4, 2), (64, 128, 2, 1), (64, 128, 4, 3), (64, 1024, 4, 2), (0, 128, 4, 2)]:
         with pytest.raises(RuntimeError):
             rt().Plan(*args, "fp32", "L2", 64, params)
+
+
+def test_out_of_range_rays_and_vertices_read_as_zero():
+    """inf_batch.num_rays bounds the permutation window and vertex ids are checked against
+    the table: a window running past the permutation (a stale replayed batch index) or a
+    bad vertex id yields zero feature rows / targets instead of a device fault."""
+    k, H, L, s = 64, 128, 4, 2
+    w0 = init_weights(k, H, L, s, seed=9)
+    N, B = 100, 64
+    E, vids, bary, rgb = synth_rays(k, 50, N, seed=3)
+    vids[5] = [0, 10_000, 1]  # out-of-range vertex id
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda())
+    perm = torch.arange(N, device="cuda")
+    for mode in ("fp32", "bf16"):
+        plan, _ = plan_for(k, H, L, s, w0, mode, "L2", B)
+        pred = torch.empty((B, 3), device="cuda")
+        plan.forward(plan.make_batch(source=src, ray_idx=perm, offset=N - 10, batch=B), pred, save=False)
+        x = np.zeros((B, k), np.float32)
+        x[:10] = O.gather(E, vids[N - 10:], bary[N - 10:])
+        p_ref, _ = O.mlp_forward(w0, x, L, s)
+        tol = 1e-5 if mode == "fp32" else 2e-2
+        assert np.abs(pred.cpu().numpy() - p_ref).max() < tol, mode
+        plan.forward(plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B), pred, save=False)
+        x = O.gather(E, np.clip(vids[:B], 0, 49), bary[:B])
+        x[5] = 0.0
+        p_ref, _ = O.mlp_forward(w0, x, L, s)
+        assert np.abs(pred.cpu().numpy() - p_ref).max() < tol, mode
