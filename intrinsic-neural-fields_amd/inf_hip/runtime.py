@@ -251,12 +251,15 @@ class RaySource:
     """Device-resident rays + eigenfunction table (ray_dataloader.py:58-98 moves the same
     arrays to the device once).  Keeps int32 vertex ids and packed GEMM-dtype tables."""
 
-    def __init__(self, E: torch.Tensor, vids: torch.Tensor, bary: torch.Tensor, rgbs: torch.Tensor | None):
+    def __init__(self, E: torch.Tensor, vids: torch.Tensor, bary: torch.Tensor, rgbs: torch.Tensor | None,
+                 validate: bool = True):
         require_hip(E, vids, bary, rgbs)
         self.E = E
         self.vids = vids
         V = E.shape[0]
-        if vids.numel() and (int(vids.min()) < 0 or int(vids.max()) >= V):
+        # the reference's E[vids] raises IndexError on a bad id (mesh.py:319); the kernels
+        # additionally read such rows as zero (validate=False exercises that guard)
+        if validate and vids.numel() and (int(vids.min()) < 0 or int(vids.max()) >= V):
             raise ValueError("vertex id out of range of the eigenfunction table")
         self.vids32 = vids.to(torch.int32).contiguous()
         self.bary = bary.to(torch.float32).contiguous()
