@@ -19,6 +19,12 @@ struct AdamSeg {
   int64_t ldw;
   void* WT;             // packed [C_pad][ldwt] transposed weight
   int64_t ldwt;
+  // bf16 weight images in MFMA fragment order for the register-streamed chain (chain3.hip),
+  // hidden H x H weights only (else null): 1 KiB per (32-deep k block kb, 16-column tile t)
+  // at (kb * (H/16) + t) KiB, lane l's 8 elements at 16 l bytes: lane l = n % 16 + 16 (k % 32 / 8)
+  // holds k = 32 kb + 8 (l / 16) + e of column n = 16 t + l % 16
+  void* WF;             // forward: n = output row r, k = input column c
+  void* WTF;            // backward (dX): n = input column c, k = output row r
 };
 
 // Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = 8 elements.

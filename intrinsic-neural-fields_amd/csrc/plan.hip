@@ -15,6 +15,7 @@
 
 #include "adam.hpp"
 #include "chain.hpp"
+#include "chain3.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
 
@@ -37,6 +38,7 @@ struct ParamSeg {
   int32_t gemm = 0;
   int32_t c_pad = 0;
   int64_t w_off = 0, wt_off = 0;  // bytes into shadow
+  int64_t f_off = -1, ft_off = -1;  // MFMA-fragment images (hidden H x H weights, bf16)
 };
 
 constexpr int64_t ALIGN = 256;
@@ -61,6 +63,7 @@ struct inf_plan {
 
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_ws_end = 0;
+  int64_t o_zy = 0;  // skip layer's data term X W_y^T + b_y (f32), register-streamed chain
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
   std::vector<int64_t> o_slab;                            // per param segment (weights)
   int64_t o_hw = 0, o_hb = 0;                             // head partials
@@ -84,7 +87,7 @@ struct inf_plan {
   // saved forward
   int saved_batch = 0, saved_bp = 0;
   bool saved = false;
-  bool last_chain = false;  // the last training step ran the fused chain
+  int last_chain = 0;  // fused chain of the last training step: 0 none, 2 LDS ring, 3 registers
   const uint64_t* dbg_ranges = nullptr;
   int dbg_n = 0;
   unsigned long long* dbg_out = nullptr;
@@ -162,6 +165,16 @@ int build_layout(inf_plan* p) {
     const int bt = (H % 128 == 0) ? 128 : 64;
     gemm_tiles += (g.R / bt) * (g.c_pad / bt);
   }
+  // fragment images of the hidden H x H weights for the register-streamed chain
+  if (p->mode == INF_MODE_BF16 && (H == 128 || H == 256)) {
+    for (auto& g : p->segs) {
+      if (!g.gemm || g.layer < 1 || g.layer > L - 2 || g.sub != 0 || g.R != H || g.C != H) continue;
+      g.f_off = sh;
+      sh = align_up(sh + (int64_t)H * H * 2);
+      g.ft_off = sh;
+      sh = align_up(sh + (int64_t)H * H * 2);
+    }
+  }
   p->shadow_bytes = sh;
 
   // ---- split-K factor of the weight-gradient GEMMs and batch padding ----
@@ -183,14 +196,16 @@ int build_layout(inf_plan* p) {
   };
   p->o_x0 = take(Bp * p->k_pad * p->esz);
   p->o_x0t = take((int64_t)p->k_pad * Bp * p->esz);
+  const int64_t max_parts =
+      std::max<int64_t>({chain_max_partials(Bp), std::min<int64_t>(Bp, CHAIN3_MAX_ROWS) / 16, (int64_t)p->grid_hb});
   for (int l = 0; l < L - 1; ++l) {
     p->o_y.push_back(take(Bp * H * p->esz));
     p->o_yt.push_back(take(Bp * H * p->esz));
     p->o_dZ.push_back(take(Bp * H * p->esz));
     p->o_dZT.push_back(take(Bp * H * p->esz));
-    const int64_t parts = std::max<int64_t>(chain_max_partials(Bp), p->grid_hb);
-    p->o_colsum.push_back(take(parts * H * 4));
+    p->o_colsum.push_back(take(max_parts * H * 4));
   }
+  p->o_zy = take(std::min<int64_t>(Bp, CHAIN3_MAX_ROWS) * H * 4);
   p->o_dz = take(Bp * 3 * 4);
   p->o_pred = take(Bp * 3 * 4);
   p->o_slab.assign(p->segs.size(), 0);
@@ -198,9 +213,8 @@ int build_layout(inf_plan* p) {
     const auto& g = p->segs[i];
     if (g.gemm) p->o_slab[i] = take((int64_t)S * g.R * g.c_pad * 4);
   }
-  const int64_t head_parts = std::max<int64_t>(p->grid_hb, chain_max_partials(Bp));
-  p->o_hw = take(head_parts * 3 * H * 4);
-  p->o_hb = take(head_parts * 3 * 4);
+  p->o_hw = take(max_parts * 3 * H * 4);
+  p->o_hb = take(max_parts * 3 * 4);
   p->o_loss = take(std::max<int64_t>(Bp / 16, 1) * 2 * 8);
 
   // update work list
@@ -296,7 +310,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
   return INF_OK;
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, bool chain = false);
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0);
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
@@ -331,8 +345,9 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
   return run_weight_grads(p, Bp, st);
 }
 
-// chain: Y^T / dZ^T were written by the fused chain in its 16-ray blocked layout
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, bool chain) {
+// chain (2, 3): Y^T / dZ^T were written by the fused chain in its 16-ray blocked layout;
+// with the register-streamed chain (3) Y_0^T comes plain from the input GEMM
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
   const int H = p->H, s = p->s;
   // weight gradients: one grouped split-K launch (chunks of GEMM_MAX_PROBLEMS)
   std::vector<GemmProblem> probs;
@@ -345,9 +360,10 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, bool chain) {
     q.lda[0] = chain ? (int64_t)H * 16 : Bp;
     q.a_kblk = chain ? 1 : 0;
     const bool from_input = (l == 0) || (l == s && g.sub == 1);
+    const bool b_blocked = chain && !from_input && !(chain == 3 && l == 1);
     q.B[0] = from_input ? (const void*)p->W(p->o_x0t) : (const void*)p->W(p->o_yt[l - 1]);
-    q.ldb[0] = (chain && !from_input) ? (int64_t)H * 16 : Bp;
-    q.b_kblk = (chain && !from_input) ? 1 : 0;
+    q.ldb[0] = b_blocked ? (int64_t)H * 16 : Bp;
+    q.b_kblk = b_blocked ? 1 : 0;
     q.K[0] = Bp;
     q.M = g.R;
     q.N = g.c_pad;
@@ -391,8 +407,8 @@ AdamArgs update_args(inf_plan* p, int Bp) {
 }
 
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
-int refresh_tables(inf_plan* p, int Bp, hipStream_t st, bool chain = false) {
-  const int parts = chain ? Bp / chain_partial_rows(chain_bm(Bp)) : Bp / 64;
+int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
+  const int parts = chain == 3 ? Bp / chain3_bm(Bp) : chain ? Bp / chain_partial_rows(chain_bm(Bp)) : Bp / 64;
   bool changed = false;
   for (size_t i = 0; i < p->segs.size(); ++i) {
     const ParamSeg& g = p->segs[i];
@@ -575,6 +591,95 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
   return launch_chain(a, bm, st);
 }
 
+bool use_chain3(const inf_plan* p, int Bp) {
+  const ParamSeg* w1 = p->weight_seg(1, 0);
+  return use_chain(p) && chain3_supported(p->H, p->L, Bp) && w1 != nullptr && w1->f_off >= 0 &&
+         std::getenv("INF_NO_CHAIN3") == nullptr;
+}
+
+// Input GEMM of the register-streamed chain, one grouped launch over X (the gathered
+// features, already in X0):  Y_0 = relu(X W_0^T + b_0)  (+ Y_0^T for the dW GEMM) and
+// Z_y = X W_y^T + b_y, the skip layer's data term in f32 (model.py:43-56, layers.py:60-62).
+int run_input_gemm(inf_plan* p, int Bp, hipStream_t st) {
+  const int H = p->H, s = p->s;
+  GemmBatch gb;
+  std::memset(&gb, 0, sizeof(gb));
+  gb.nprob = 2;
+  for (int i = 0; i < 2; ++i) {
+    GemmProblem& q = gb.p[i];
+    q = blank_problem();
+    const ParamSeg* w = i == 0 ? p->weight_seg(0, 0) : p->weight_seg(s, 1);
+    const ParamSeg* bs = i == 0 ? p->bias_seg(0, 0) : p->bias_seg(s, 1);
+    q.A[0] = p->W(p->o_x0);
+    q.lda[0] = p->k_pad;
+    q.B[0] = p->shadow + w->w_off;
+    q.ldb[0] = w->c_pad;
+    q.K[0] = p->k_pad;
+    q.bias0 = p->params + bs->off;
+    q.M = Bp;
+    q.N = H;
+    if (i == 0) {
+      q.relu = 1;
+      q.C = p->W(p->o_y[0]);
+      q.ldc = H;
+      q.CT = p->W(p->o_yt[0]);
+      q.ldct = Bp;
+    } else {
+      q.C = p->W(p->o_zy);
+      q.ldc = H;
+      q.c_f32 = 1;
+    }
+  }
+  return launch_gemm(gb, p->mode, pick_tile(p, Bp, 2 * H), st);
+}
+
+int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
+  const int H = p->H, L = p->L, s = p->s;
+  Chain3Args a;
+  std::memset(&a, 0, sizeof(a));
+  a.L = L;
+  a.s = s;
+  a.H = H;
+  a.rows = Bp;
+  a.batch = b->batch;
+  a.Y0 = p->W<bf16>(p->o_y[0]);
+  a.Zy = p->W<float>(p->o_zy);
+  a.nphase = 2 * (L - 2);
+  for (int ph = 0; ph < a.nphase; ++ph) {
+    const bool fwd = ph < L - 2;
+    const int l = fwd ? ph + 1 : (L - 2) - (ph - (L - 2));
+    const ParamSeg* w = p->weight_seg(l, 0);
+    INF_CHECK_ARG(w != nullptr && w->f_off >= 0, "chain3: fragment image missing");
+    a.img[ph] = reinterpret_cast<const bf16*>(p->shadow + (fwd ? w->f_off : w->ft_off));
+  }
+  for (int l = 0; l <= L - 2; ++l) {
+    a.bias[l] = p->params + p->bias_seg(l, 0)->off;
+    a.YT[l] = p->W<bf16>(p->o_yt[l]);
+    a.dZT[l] = p->W<bf16>(p->o_dZT[l]);
+    a.colsum[l] = p->W<float>(p->o_colsum[l]);
+  }
+  a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
+  a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
+  a.hw_part = p->W<float>(p->o_hw);
+  a.hb_part = p->W<float>(p->o_hb);
+  a.loss_part = p->W<double>(p->o_loss);
+  a.pred = pred;
+  INF_CHECK_ARG(b->rgb != nullptr, "training batch without target colours");
+  a.rgb = b->rgb;
+  a.ray_idx = b->ray_idx;
+  a.idx_dtype = b->idx_dtype;
+  a.idx_offset = b->idx_offset;
+  a.num_rays = b->num_rays;
+  a.offset_from_ctrl = b->offset_from_ctrl;
+  a.loss = b->loss >= 0 ? b->loss : p->d.loss;
+  INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
+  const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
+  a.inv_count = (float)(1.0 / (double)cnt);
+  a.ctrl = p->ctrl;
+  a.count_step = 1;
+  return launch_chain3(a, chain3_bm(Bp), st);
+}
+
 int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool loss, const int64_t* hit,
                  const int64_t* pixel_map, float* img, hipStream_t st) {
   INF_CHECK_ARG(b != nullptr, "null batch");
@@ -699,6 +804,8 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
       a.ldw = g.c_pad;
       a.WT = p->shadow + g.wt_off;
       a.ldwt = g.R;
+      a.WF = g.f_off >= 0 ? p->shadow + g.f_off : nullptr;
+      a.WTF = g.ft_off >= 0 ? p->shadow + g.ft_off : nullptr;
       const int flags = (g.C % 4 == 0 && g.off % 4 == 0) ? ITEM_VEC4 : 0;
       for (int r = 0; r < g.R; r += ADAM_TILE_R)
         for (int c = 0; c < g.C; c += ADAM_TILE_C) p->adam_items.push_back(AdamItem{(int32_t)i, r, c, flags});
@@ -792,7 +899,22 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   int rc;
   const bool chain = use_chain(p);
   int nloss = 0;
-  if (chain) {
+  int ck = 0;
+  int Bp3 = 0;
+  if ((rc = pad_batch(p, batch->batch, true, &Bp3))) return rc;
+  if (use_chain3(p, Bp3)) {
+    // gather -> input GEMM -> register-streamed chain -> dW GEMM (-> update below)
+    const int Bp = Bp3;
+    if ((rc = run_input(p, batch, Bp, true, st))) return rc;
+    if ((rc = run_input_gemm(p, Bp, st))) return rc;
+    if ((rc = run_chain3(p, batch, Bp, pred, st))) return rc;
+    if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
+    p->saved = false;
+    p->saved_batch = batch->batch;
+    p->saved_bp = Bp;
+    ck = 3;
+    nloss = Bp / chain3_bm(Bp);
+  } else if (chain) {
     // the chain leaves per-tile loss partials; the update launch stores their sum
     int Bp = 0;
     if ((rc = pad_batch(p, batch->batch, true, &Bp))) return rc;
@@ -802,19 +924,19 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     p->saved = false;
     p->saved_batch = batch->batch;
     p->saved_bp = Bp;
-    p->last_chain = true;
+    ck = 2;
     nloss = Bp / chain_bm(Bp);
   } else {
     // the layered head accumulates the step's sums with atomics: clear them first
     INF_HIP_TRY(hipMemsetAsync(&p->ctrl->loss_sum, 0, 2 * sizeof(double), st));
-    p->last_chain = false;
     if ((rc = forward_impl(p, batch, pred, true, true, nullptr, nullptr, nullptr, st))) return rc;
     const int Bp0 = p->saved_bp;
     if ((rc = head_backward(p, Bp0, nullptr, true, st))) return rc;
     if ((rc = run_backward_layers(p, Bp0, st))) return rc;
   }
+  p->last_chain = ck;
   const int Bp = p->saved_bp;
-  if ((rc = refresh_tables(p, Bp, st, chain))) return rc;
+  if ((rc = refresh_tables(p, Bp, st, ck))) return rc;
   AdamArgs a = update_args(p, Bp);
   a.grad_src = GRAD_SLABS;
   if (apply_adam) {
@@ -893,10 +1015,25 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
     case INF_STAGE_CHAIN: {
       INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && use_chain(p), "chain stage needs a bf16 training batch");
       // replay on the saved inputs; the step counter it advances is restored by the caller
-      rc = run_chain(p, b, Bp, true, nullptr, nullptr, nullptr, nullptr, st);
       const double Lh = p->L;
-      f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
-      by = B * (2.0 * p->k_pad * e + 2.0 * (Lh - 1) * H * e) + 2.0 * 4 * p->P;
+      if (p->last_chain == 3) {
+        rc = run_chain3(p, b, Bp, nullptr, st);
+        f = 2.0 * 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+        // hidden weights streamed by every workgroup + Y_0 / Z_y tiles in, Y^T / dZ^T out
+        by = (double)(Bp / chain3_bm(Bp)) * 2.0 * (Lh - 2) * H * H * e + B * H * (e + 4.0) +
+             B * (2.0 * Lh - 5) * H * e;
+      } else {
+        rc = run_chain(p, b, Bp, true, nullptr, nullptr, nullptr, nullptr, st);
+        f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+        by = B * (2.0 * p->k_pad * e + 2.0 * (Lh - 1) * H * e) + 2.0 * 4 * p->P;
+      }
+      break;
+    }
+    case INF_STAGE_INPUT_GEMM: {
+      INF_CHECK_ARG(p->last_chain == 3, "input GEMM stage needs a register-chain training step");
+      rc = run_input_gemm(p, Bp, st);
+      f = 2.0 * B * 2.0 * k * H;
+      by = B * p->k_pad * e + 2.0 * H * p->k_pad * e + B * H * (2.0 * e + 4.0);
       break;
     }
     case INF_STAGE_UPDATE: {

@@ -227,8 +227,10 @@ def test_render_golden():
 @pytest.mark.parametrize("name,B", [("B", 1024), ("A", 512), ("R", 256), ("B", 4096), ("B", 8192), ("A", 16384),
                                     ("B", 32768)])
 def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
-    """The fused bf16 chain (csrc/chain.hip) vs the layered bf16 kernels and the fp32
-    oracle: predictions within 2e-2; reduced gradients within 0.25 of each tensor's max.
+    """The fused bf16 chains (csrc/chain3.hip: batches up to 8192 rays, register-streamed
+    weights after the input GEMM; csrc/chain.hip: the LDS-ring chain) vs the layered bf16
+    kernels and the fp32 oracle: predictions within 2e-2; reduced gradients within 0.25
+    of each tensor's max.
     bf16 rounding of activations and of dZ compounds backwards through the ReLU layers:
     PyTorch's own bf16 autocast of the reference on this exact problem (config B, 1024
     rays) is off by 0.135 (layers.0 weight) / 0.10 (Ly) / 0.005 (head) of max, and this
@@ -246,7 +248,10 @@ def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
     src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
                          torch.from_numpy(rgb).cuda())
     out = {}
-    for tag in ("chain", "layered"):
+    tags = ("chain3", "chain", "layered")
+    for tag in tags:
+        if tag == "chain":
+            monkeypatch.setenv("INF_NO_CHAIN3", "1")
         if tag == "layered":
             monkeypatch.setenv("INF_NO_CHAIN", "1")
         plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
@@ -258,7 +263,7 @@ def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
     p_ref = cache["out"][-1]
     g_ref = O.mlp_backward(w0, cache, O.loss_grad(p_ref, rgb, "L2"), L, s)
     errs = {}
-    for tag in ("chain", "layered"):
+    for tag in tags:
         p, g, lsum, step = out[tag]
         assert step == 1
         assert np.abs(p - p_ref).max() < 2e-2, tag
@@ -271,11 +276,15 @@ def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
         assert err < 0.25, (tag, n, err)
         if n.startswith(f"layers.{L - 1}."):
             assert err < 1e-2, (tag, n, err)  # the output layer sees no bf16 backward chain
-    # chain and layered bf16 paths agree much more tightly with each other
+    # the chains and the layered bf16 path agree much more tightly with each other (the
+    # register chain sums the skip layer's two K segments in a different order, so a
+    # bf16 activation can round the other way: 5e-4, seen 1.5e-4 on 2 of 12288 at 4096 rays)
     np.testing.assert_allclose(out["chain"][0], out["layered"][0], atol=1e-5)
-    for n in O.layer_names(L, s):
-        scale = max(np.abs(out["layered"][1][n]).max(), 1e-12)
-        assert np.abs(out["chain"][1][n] - out["layered"][1][n]).max() / scale < 1e-2, n
+    np.testing.assert_allclose(out["chain3"][0], out["layered"][0], atol=5e-4)
+    for tag in ("chain", "chain3"):
+        for n in O.layer_names(L, s):
+            scale = max(np.abs(out["layered"][1][n]).max(), 1e-12)
+            assert np.abs(out[tag][1][n] - out["layered"][1][n]).max() / scale < 1e-2, (tag, n)
 
 
 def test_bf16_chain_render_matches_layered(monkeypatch):
