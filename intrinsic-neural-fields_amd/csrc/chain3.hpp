@@ -37,6 +37,10 @@ struct Chain3Args {
   float inv_count;
   inf_ctrl* ctrl;
   int32_t count_step;
+  // diagnostics: per-phase wall-clock stamps (100 MHz) of wave 0 of the first and the last
+  // workgroup: [2][nphase * 3 + 6] = entry, {phase start, MFMAs done, epilogue done} ..., end,
+  // loads issued, Y_0 tile written, barrier 0 passed
+  unsigned long long* stamps;
 };
 
 // Rays per workgroup.  One 16-row MFMA tile: every CU streams the whole weight set per

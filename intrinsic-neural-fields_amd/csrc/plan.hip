@@ -677,6 +677,7 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.inv_count = (float)(1.0 / (double)cnt);
   a.ctrl = p->ctrl;
   a.count_step = 1;
+  a.stamps = p->stamps;
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
