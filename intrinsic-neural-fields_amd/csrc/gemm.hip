@@ -13,6 +13,8 @@
 // over all bank slots of a 256-byte bank row pair (2-way at worst).
 // Epilogue: accumulators -> padded fp32 LDS tile -> bias / ReLU / ReLU-mask ->
 // coalesced row-major store, transposed store and per-tile column sums.
+#include <cstdlib>
+
 #include "gemm.hpp"
 
 namespace inf {
@@ -49,6 +51,18 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// wait until at most n * PER direct-to-LDS loads of this wave are in flight (n <= N,
+// wave-uniform; vmcnt takes an immediate), then the workgroup barrier
+template <int N, int PER>
+__device__ __forceinline__ void wait_ahead_barrier(int n) {
+  if constexpr (N <= 0) {
+    wait_vm_barrier<0>();
+  } else {
+    if (n >= N) wait_vm_barrier<N * PER>();
+    else wait_ahead_barrier<N - 1, PER>(n);
+  }
+}
+
 template <typename T, int BM, int BN>
 struct Tile {
   static constexpr int BK = ModeTraits<T>::BK;
@@ -58,9 +72,13 @@ struct Tile {
 #ifndef INF_GEMM128_STAGES
 #define INF_GEMM128_STAGES 2
 #endif
+#ifndef INF_GEMM64_STAGES
+#define INF_GEMM64_STAGES 4
+#endif
   // 128x128: 2 stages (64 KiB, under the 67.6 KiB C staging tile) keep two workgroups per
   // CU; the 64x64 tile affords 4 stages (64 KiB) at the same occupancy
-  static constexpr int STAGES = (BM == 128 && BN == 128) ? INF_GEMM128_STAGES : 4;
+  static constexpr int STAGES =
+      (BM == 128 && BN == 128) ? INF_GEMM128_STAGES : ((BM == 64 && BN == 64) ? INF_GEMM64_STAGES : 4);
   static constexpr int STAGE_BYTES = (BM + BN) * 128;
   static constexpr int OPER_BYTES = STAGES * STAGE_BYTES;
   static constexpr int CLD = BN + 4;  // fp32 C staging row stride
@@ -132,12 +150,16 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // ---- locate problem / tile -----------------------------------------------------
+  // XCD-aware order (batch.xcd_remap): blocks b, b + 8, b + 16, ... are dealt to one
+  // XCD, so they take consecutive tiles (same row panel, n fastest) and share its L2
+  int bid = (int)blockIdx.x;
+  if (batch.xcd_remap && batch.total_blocks % 8 == 0) bid = (bid & 7) * (batch.total_blocks >> 3) + (bid >> 3);
   int pi = 0;
 #pragma unroll 1
   for (int i = 1; i < batch.nprob; ++i)
-    if ((int)blockIdx.x >= batch.p[i].block_begin) pi = i;
+    if (bid >= batch.p[i].block_begin) pi = i;
   const GemmProblem& P = batch.p[pi];
-  int local = (int)blockIdx.x - P.block_begin;
+  int local = bid - P.block_begin;
   const int tiles = P.tiles_m * P.tiles_n;
   const int split = local / tiles;
   local -= split * tiles;
@@ -215,9 +237,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
     for (int t = t_begin; t < t_end; ++t) {
       // stages issued after t that may stay in flight
       const int ahead = min(STAGES - 2, t_end - 1 - t);
-      if (ahead >= 2) wait_vm_barrier<2 * PER>();
-      else if (ahead == 1) wait_vm_barrier<PER>();
-      else wait_vm_barrier<0>();
+      wait_ahead_barrier<STAGES - 2, PER>(ahead);
       if (t + STAGES - 1 < t_end) issue(t + STAGES - 1);
       const char* As = smem + ((t - t_begin) % STAGES) * TL::STAGE_BYTES;
       compute_tile<T, BM, BN>(As, As + BM * 128, wm0, wn0, lane, acc);
@@ -352,11 +372,14 @@ int launch_gemm(GemmBatch& b, int mode, GemmTile tile, hipStream_t stream) {
     blocks += p.tiles_m * p.tiles_n * p.splits;
   }
   b.total_blocks = blocks;
+  b.xcd_remap = std::getenv("INF_NO_XCD_REMAP") == nullptr ? 1 : 0;
   if (mode == INF_MODE_BF16) {
     if (tile == TILE_128x128) return launch_typed<bf16, 128, 128>(b, stream);
+    if (tile == TILE_128x64) return launch_typed<bf16, 128, 64>(b, stream);
     return launch_typed<bf16, 64, 64>(b, stream);
   }
   if (tile == TILE_128x128) return launch_typed<float, 128, 128>(b, stream);
+  if (tile == TILE_128x64) return launch_typed<float, 128, 64>(b, stream);
   return launch_typed<float, 64, 64>(b, stream);
 }
 

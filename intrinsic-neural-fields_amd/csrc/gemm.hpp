@@ -51,11 +51,12 @@ struct GemmBatch {
   GemmProblem p[GEMM_MAX_PROBLEMS];
   int32_t nprob;
   int32_t total_blocks;
+  int32_t xcd_remap;  // 1: XCD-aware block -> tile order (set by launch_gemm)
 };
 
 // Tile configuration selector.
-enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1 };
-inline int tile_bm(GemmTile t) { return t == TILE_128x128 ? 128 : 64; }
+enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_128x64 = 2 };
+inline int tile_bm(GemmTile t) { return t == TILE_64x64 ? 64 : 128; }
 inline int tile_bn(GemmTile t) { return t == TILE_128x128 ? 128 : 64; }
 
 // Fills tiles_m/tiles_n/block_begin/total_blocks and launches.  mode = INF_MODE_*.

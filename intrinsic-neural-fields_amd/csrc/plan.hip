@@ -8,6 +8,7 @@
 //   -> L-2 dX GEMMs (ReLU mask + bias-grad partials) -> ONE grouped split-K dW GEMM over
 //   all weight matrices -> ONE update launch (slab reduction + Adam + packed weights).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -181,6 +182,10 @@ int build_layout(inf_plan* p) {
   int S = 1;
   const int64_t mb = round_up(std::max(p->max_batch, 1), 128);
   while (gemm_tiles * S < 512 && S < 16 && mb / (S * 2) >= 512) S *= 2;
+  if (const char* e = std::getenv("INF_DW_SPLITS")) {  // tuning experiments
+    const int want = std::atoi(e);
+    if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 128) S = want;
+  }
   p->dw_splits = S;
   p->train_unit = (int)std::max<int64_t>(128, (int64_t)S * 64);
   p->bp_max = (int)round_up(p->max_batch, p->train_unit);
@@ -224,6 +229,18 @@ int build_layout(inf_plan* p) {
   p->o_tables = take(p->table_bytes);
   p->o_ws_end = w;
   return INF_OK;
+}
+
+// Tile override for tuning experiments: INF_TILE_<WHAT>=128x128|128x64|64x64.
+bool tile_override(const char* what, GemmTile* t) {
+  char name[64];
+  std::snprintf(name, sizeof(name), "INF_TILE_%s", what);
+  const char* v = std::getenv(name);
+  if (v == nullptr) return false;
+  if (!std::strcmp(v, "128x128")) *t = TILE_128x128;
+  else if (!std::strcmp(v, "128x64")) *t = TILE_128x64;
+  else *t = TILE_64x64;
+  return true;
 }
 
 GemmTile pick_tile(const inf_plan* p, int64_t M, int64_t N) {
@@ -373,7 +390,8 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
     q.slab_stride = (int64_t)g.R * g.c_pad;
     probs.push_back(q);
   }
-  const GemmTile wtile = (H % 128 == 0) ? TILE_128x128 : TILE_64x64;
+  GemmTile wtile = (H % 128 == 0) ? TILE_128x128 : TILE_64x64;
+  tile_override("DW", &wtile);
   for (size_t i0 = 0; i0 < probs.size(); i0 += GEMM_MAX_PROBLEMS) {
     GemmBatch gb;
     std::memset(&gb, 0, sizeof(gb));
@@ -630,7 +648,9 @@ int run_input_gemm(inf_plan* p, int Bp, hipStream_t st) {
       q.c_f32 = 1;
     }
   }
-  return launch_gemm(gb, p->mode, pick_tile(p, Bp, 2 * H), st);
+  GemmTile tile = pick_tile(p, Bp, 2 * H);
+  tile_override("INPUT", &tile);
+  return launch_gemm(gb, p->mode, tile, st);
 }
 
 int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
