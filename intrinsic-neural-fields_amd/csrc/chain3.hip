@@ -38,6 +38,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr float C3_CAUCHY_C2 = (20.f / 255.f) * (20.f / 255.f);
 constexpr int C3_THREADS = 320;  // 4 compute waves + 1 store wave
 constexpr int C3_LDS_CAP = 160 * 1024;
+#ifndef C3_DEPTH
+#define C3_DEPTH 4
+#endif
 
 template <int H, int TM>
 struct L3 {
@@ -83,6 +86,13 @@ __device__ __forceinline__ int act_off3(int row, int col) {
 template <int H>
 __device__ __forceinline__ int box_off(int col, int r) {
   return (((r >> 4) * H + col) * 16 + (r & 15)) * 2;
+}
+
+// element (col, ray r < 16) of a workgroup's dZ^T box: the fragment image the dW GEMM
+// streams (lgemm.hip operand B: rows = columns of dZ, k = rays): per 16-column tile one
+// 512-byte piece = the workgroup's half (16 of 32 rays) of that tile's 1 KiB k-block
+__device__ __forceinline__ int frag_box_off(int col, int r) {
+  return (col >> 4) * 512 + ((col & 15) + 16 * (r >> 3)) * 16 + (r & 7) * 2;
 }
 
 __device__ __forceinline__ unsigned short bf_bits3(float x) {
@@ -171,7 +181,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const int c = tid + 256 * q, row = c / (H / 8), ch = c % (H / 8);
       yv[q] = *reinterpret_cast<const u16x8*>(a.Y0 + (int64_t)(b0 + row) * H + ch * 8);
     }
-    bf16x8 fr[UPL][TN];
+    // fragment ring: D k-blocks (D * TN KiB per wave) in flight; 16 KiB per wave kept the
+    // L2 -> CU stream at its best rate in tools/microbench/l2ring (32 KiB: -35 %)
+    constexpr int D = C3_DEPTH < UPL ? C3_DEPTH : UPL;
+    bf16x8 fr[D][TN];
     // byte offset of this lane's 16 bytes in a wave's TN KiB of one k block; the block
     // base stays uniform (SGPR) so every load is saddr + lane offset + immediate
     // buffer loads: descriptor per image in SGPRs, k-block offset in soffset, tile offset
@@ -187,7 +200,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     {
       const __amdgpu_buffer_rsrc_t rs0 = rsrc_of(a.img[0]);
 #pragma unroll
-      for (int kb = 0; kb < UPL; ++kb) {
+      for (int kb = 0; kb < D; ++kb) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) fr[kb][j] = frag(rs0, kb, j);
         // keep block order: the loop's waits assume block kb was issued before kb + 1
@@ -214,8 +227,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 #pragma unroll 1
     for (int p = 0; p < nphase; ++p) {
       stamp(1 + 3 * p);
-      // ---- MFMAs of phase p; slot kb refilled with phase p+1 (the last phase reloads
-      // itself: a few harmless extra loads keep every wait exact)
+      // ---- MFMAs of phase p; slot kb % D refilled with k-block kb + D of this phase or
+      // of phase p+1 (the last phase reloads itself: harmless extra loads keep every wait
+      // exact)
+      const __amdgpu_buffer_rsrc_t crs = rsrc_of(a.img[p]);
       const __amdgpu_buffer_rsrc_t nrs = rsrc_of(a.img[p + 1 < nphase ? p + 1 : p]);
 #pragma unroll
       for (int kb = 0; kb < UPL; ++kb) {
@@ -229,9 +244,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], fr[kb][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], fr[kb % D][j], acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fr[kb][j] = frag(nrs, kb, j);
+        for (int j = 0; j < TN; ++j)
+          fr[kb % D][j] = kb + D < UPL ? frag(crs, kb + D, j) : frag(nrs, kb + D - UPL, j);
         __builtin_amdgcn_sched_barrier(0);
       }
 
@@ -401,7 +417,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
                 g1 = fmaf(d1, h, g1);
                 g2 = fmaf(d2, h, g2);
               }
-              *reinterpret_cast<u16x4*>(box + box_off<H>(col, row0)) = q;
+              *reinterpret_cast<u16x4*>(box + frag_box_off(col, row0)) = q;
             }
             cs = col_sum4(cs);
             g0 = col_sum4(g0);
@@ -436,7 +452,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               q[r] = bf_bits3(v);
               if (keep_act) *reinterpret_cast<unsigned short*>(act + act_off3<H>(row0 + r, col)) = q[r];
             }
-            *reinterpret_cast<u16x4*>(box + box_off<H>(col, row0)) = q;
+            *reinterpret_cast<u16x4*>(box + frag_box_off(col, row0)) = q;
           }
           cs = col_sum4(cs);
           if (g4 == 0) csb[col] = cs;
@@ -531,6 +547,14 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       for (int c = lane * 16; c < bytes; c += 64 * 16)
         *reinterpret_cast<u16x8*>(d + c) = *reinterpret_cast<const u16x8*>(src + c);
     };
+    // dZ^T box -> fragment image: piece t (512 B) to k-block b0 / 32, tile t, half
+    // (b0 / 16) % 2 of its 1 KiB
+    const int64_t frag_base = (int64_t)(b0 >> 5) * (H / 16) * 1024 + ((b0 >> 4) & 1) * 512;
+    auto copy_frag = [&](const char* src, bf16* dst) {
+      char* d = reinterpret_cast<char*>(dst) + frag_base;
+      for (int c = lane; c < C::TILE_BYTES / 16; c += 64)
+        *reinterpret_cast<u16x8*>(d + (c >> 5) * 1024 + (c & 31) * 16) = *reinterpret_cast<const u16x8*>(src + c * 16);
+    };
 #pragma unroll 1
     for (int p = 0; p < nphase; ++p) {
       lbar();  // B1
@@ -543,7 +567,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         const int l = p + 1;
         if (l <= L - 3) copy_out(box, a.YT[l] + tile_elems, C::TILE_BYTES);
         if (head_phase) {
-          copy_out(box, a.dZT[L - 2] + tile_elems, C::TILE_BYTES);
+          copy_frag(box, a.dZT[L - 2]);
           copy_out(csb, a.colsum[L - 2] + (int64_t)blockIdx.x * H, H * 4);
           copy_out(reinterpret_cast<const char*>(hws), a.hw_part + (int64_t)blockIdx.x * 3 * H, 3 * H * 4);
           if (lane < 3) a.hb_part[(int64_t)blockIdx.x * 3 + lane] = hbs[lane];
@@ -554,7 +578,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       } else {
         const int l = (L - 2) - (p - nfwd);
-        copy_out(box, a.dZT[l - 1] + tile_elems, C::TILE_BYTES);
+        copy_frag(box, a.dZT[l - 1]);
         copy_out(csb, a.colsum[l - 1] + (int64_t)blockIdx.x * H, H * 4);
       }
     }

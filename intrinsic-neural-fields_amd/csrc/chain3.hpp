@@ -21,7 +21,8 @@ struct Chain3Args {
   const float* W7;                       // [3][H] fp32 output layer
   const float* b7;
   bf16* YT[CHAIN_MAX_HIDDEN];      // 16-ray blocked Y_l^T, l = 1..L-3
-  bf16* dZT[CHAIN_MAX_HIDDEN];     // 16-ray blocked dZ_l^T, l = 0..L-2
+  bf16* dZT[CHAIN_MAX_HIDDEN];     // dZ_l^T as fragment images (H/16 tiles x rows/32 k-blocks,
+                                   // lgemm.hpp operand B), l = 0..L-2
   float* colsum[CHAIN_MAX_HIDDEN]; // [rows/BM][H] bias-gradient partials
   float* hw_part;                  // [rows/BM][3][H]
   float* hb_part;                  // [rows/BM][3]

@@ -1,0 +1,269 @@
+// Grouped bf16 GEMM for the small-batch training step: A shared through LDS, B streamed
+// from an MFMA-fragment-order image straight into registers.
+//
+// Block = BM rows x 128 columns, 4 waves; wave w owns columns [32 w, 32 w + 32) (two
+// 16-column MFMA tiles) for all BM rows.  Per 32-deep k block ("unit") a wave needs
+// one A fragment per 16-row tile (shared by the 4 waves: LDS) and two B fragments (its
+// own: two coalesced 1 KiB loads of the fragment image, no LDS).
+//
+// Why.  The LDS-DMA GEMM (gemm.hip) stages both operands through LDS: at 64x64 / 128x128
+// tiles every k-step costs each wave 4-8 direct-to-LDS issues (~100+ cycles each) for
+// 8-32 MFMAs, and those issues, not HBM or the MFMAs, set its time.  Here the per-unit
+// traffic a wave issues is two 1 KiB register loads plus a quarter of the shared A tile
+// (register-staged: global_load_dwordx4 -> ds_write_b128, 16 bytes per thread per
+// 64-deep stage at BM = 64), and everything stays in flight: D = 8 units of B fragments
+// and RA = 4 stages of A per wave.  All vector-memory instructions are register loads,
+// so the compiler's vmcnt waits are exact; the per-stage barrier is an LDS hand-off that
+// never drains vmcnt.
+//
+// Epilogues: bias + ReLU into row-major C (bf16 / f32) and a plain transposed copy
+// (input GEMM), or the transposed f32 tile into a split-K slab (weight gradients: the
+// block computes dW^T, the slab holds dW as the update kernel reads it).
+#include <algorithm>
+
+#include "lgemm.hpp"
+
+namespace inf {
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef LG_DEPTH
+#define LG_DEPTH 4
+#endif
+
+template <int BM>
+struct LG {
+  static constexpr int TM = BM / 16, TN = 2;
+  static constexpr int D = LG_DEPTH;  // B units in flight per wave (fragment register ring)
+  static constexpr int RA = 4;  // A stages (64 deep) in flight in registers
+  static constexpr int ACH = BM * 8 / 256;  // 16-byte A chunks per thread per stage
+  static constexpr int A_STAGE = BM * 128;  // bytes: BM rows x 64 bf16
+  static constexpr int CLD = LG_BN + 4;     // f32 staging row stride
+  static constexpr int LDS = std::max(2 * A_STAGE, BM * CLD * 4);
+  static_assert(ACH >= 1 && BM * 8 % 256 == 0, "A stage must split over 256 threads");
+};
+
+// 16-byte chunk c of 128-byte LDS row `row` (the gemm.hip swizzle: a ds_read_b128 lane
+// group of 16 rows at one chunk is conflict-free)
+__device__ __forceinline__ int lswz(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int BM>
+__global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
+  using C = LG<BM>;
+  constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // ---- block -> problem / split / tile (XCD-aware order, gemm.hip) --------------------
+  int bid = (int)blockIdx.x;
+  if (batch.total_blocks % 8 == 0) bid = (bid & 7) * (batch.total_blocks >> 3) + (bid >> 3);
+  int pi = 0;
+#pragma unroll 1
+  for (int i = 1; i < batch.nprob; ++i)
+    if (bid >= batch.p[i].block_begin) pi = i;
+  const LgemmProblem& P = batch.p[pi];
+  int local = bid - P.block_begin;
+  const int tiles = P.tiles_m * P.tiles_n;
+  const int split = local / tiles;
+  local -= split * tiles;
+  const int tm = local / P.tiles_n;
+  const int tn = local - tm * P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * LG_BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wc = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+
+  const int kper = P.K / P.splits;  // multiple of 256
+  const int k_begin = split * kper;
+  const int nst = kper / 64;        // A stages, multiple of 4
+  const int nun = kper / 32;        // units
+
+  // ---- A: buffer descriptor at this split's first k; per-thread chunk offsets ---------
+  const bool akb = P.a_kblk != 0;
+  const char* a_base = reinterpret_cast<const char*>(P.A) + (akb ? (int64_t)(k_begin >> 4) * P.lda : k_begin) * 2;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a_base), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int a_step = akb ? (int)(4 * P.lda * 2) : 128;  // bytes per 64-deep stage
+  unsigned aoff[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int q = tid + 256 * i, row = q >> 3, c = q & 7;
+    aoff[i] = (unsigned)((akb ? (int64_t)(c >> 1) * P.lda + (int64_t)(m0 + row) * 16 + 8 * (c & 1)
+                              : (int64_t)(m0 + row) * P.lda + 8 * c) * 2);
+  }
+  // ---- B: fragment image; this wave's two 16-row tiles ---------------------------------
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(P.Bf), (short)0, 0x7FFFFFFF, 0x00020000);
+  const unsigned boff = (unsigned)((((P.b_row0 + n0) >> 4) + 2 * wc) * 64 + lane) * 16u;
+  const int bstep = P.b_tiles * 1024;  // bytes per unit
+  const int kb0 = k_begin >> 5;
+
+  auto loadA = [&](int st, u32x4 (&dst)[ACH]) {
+    st = min(st, nst - 1);  // past the end: reload the last stage (never stored)
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) dst[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, aoff[i], st * a_step, 0);
+  };
+  auto storeA = [&](int buf, const u32x4 (&src)[ACH]) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int q = tid + 256 * i;
+      *reinterpret_cast<u32x4*>(smem + buf * C::A_STAGE + lswz(q >> 3, q & 7)) = src[i];
+    }
+  };
+  auto loadB = [&](int u, bf16x8 (&dst)[TN]) {
+    u = min(u, nun - 1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      dst[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + j * 1024, (kb0 + u) * bstep, 0));
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ar[RA][ACH];
+  bf16x8 fr[D][TN];
+#pragma unroll
+  for (int q = 0; q < RA; ++q) {
+    loadA(q, ar[q]);
+    __builtin_amdgcn_sched_barrier(0);  // issue order = wait order
+  }
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    loadB(q, fr[q]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  storeA(0, ar[0]);
+  loadA(RA, ar[0]);
+  lg_bar();
+
+#pragma unroll 1
+  for (int s0 = 0; s0 < nst; s0 += 4) {
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss) {
+      const int s = s0 + ss;
+      const int nxt = (ss + 1) % RA;  // compile-time after unrolling
+      if (s + 1 < nst) storeA((s + 1) & 1, ar[nxt]);
+      loadA(s + 1 + RA, ar[nxt]);
+      const char* As = smem + (s & 1) * C::A_STAGE;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int slot = (2 * ss + kk) % D;
+        bf16x8 av[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(As + lswz(i * 16 + r16, kk * 4 + g4));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], fr[slot][j], acc[i][j], 0, 0, 0);
+        loadB(2 * s + kk + D, fr[slot]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      lg_bar();
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue: accumulators -> f32 LDS tile ------------------------------------------
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int CLD = C::CLD;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(i * 16 + g4 * 4 + r) * CLD + wc * 32 + j * 16 + r16] = acc[i][j][r];
+  __syncthreads();
+
+  if (P.slab != nullptr) {
+    // dW^T tile -> slab [n][m]: four consecutive m per 16-byte store
+    float* dst = P.slab + (int64_t)split * P.slab_stride;
+    constexpr int MQ = BM / 4;
+#pragma unroll 4
+    for (int q = tid; q < LG_BN * MQ; q += 256) {
+      const int col = q / MQ, mq = q - col * MQ;
+      const f32x4 v = {Cs[(mq * 4 + 0) * CLD + col], Cs[(mq * 4 + 1) * CLD + col], Cs[(mq * 4 + 2) * CLD + col],
+                       Cs[(mq * 4 + 3) * CLD + col]};
+      *reinterpret_cast<f32x4*>(dst + (int64_t)(n0 + col) * P.slab_ld + m0 + mq * 4) = v;
+    }
+    return;
+  }
+  constexpr int NQ = LG_BN / 4;
+#pragma unroll 4
+  for (int q = tid; q < BM * NQ; q += 256) {
+    const int row = q / NQ, c4 = q - row * NQ;
+    const int m = m0 + row, n = n0 + c4 * 4;
+    f32x4 v = *reinterpret_cast<const f32x4*>(Cs + row * CLD + c4 * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (P.bias != nullptr) x += P.bias[n + e];
+      if (P.relu) x = fmaxf(x, 0.f);
+      v[e] = x;
+    }
+    if (P.CT != nullptr) *reinterpret_cast<f32x4*>(Cs + row * CLD + c4 * 4) = v;
+    if (P.c_f32) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + (int64_t)m * P.ldc + n) = v;
+    } else {
+      const bf16x4 h = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(P.C) + (int64_t)m * P.ldc + n) = h;
+    }
+  }
+  if (P.CT == nullptr) return;
+  __syncthreads();
+  constexpr int MQ = BM / 4;
+#pragma unroll 4
+  for (int q = tid; q < LG_BN * MQ; q += 256) {
+    const int col = q / MQ, mq = q - col * MQ;
+    const bf16x4 h = {(bf16)Cs[(mq * 4 + 0) * CLD + col], (bf16)Cs[(mq * 4 + 1) * CLD + col],
+                      (bf16)Cs[(mq * 4 + 2) * CLD + col], (bf16)Cs[(mq * 4 + 3) * CLD + col]};
+    *reinterpret_cast<bf16x4*>(P.CT + (int64_t)(n0 + col) * P.ldct + m0 + mq * 4) = h;
+  }
+}
+
+template <int BM>
+int launch_typed(const LgemmBatch& b, hipStream_t stream) {
+  constexpr int lds = LG<BM>::LDS;
+  static bool attr = false;
+  if (!attr) {
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr = true;
+  }
+  lgemm_kernel<BM><<<dim3((unsigned)b.total_blocks), dim3(256), lds, stream>>>(b);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
+
+}  // namespace
+
+int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
+  INF_CHECK_ARG(bm == 32 || bm == 64, "lgemm: rows per block");
+  INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= LGEMM_MAX_PROBLEMS, "lgemm: problem count");
+  int blocks = 0;
+  for (int i = 0; i < b.nprob; ++i) {
+    LgemmProblem& p = b.p[i];
+    if (p.splits < 1) p.splits = 1;
+    INF_CHECK_ARG(p.A != nullptr && p.Bf != nullptr, "lgemm: null operand");
+    INF_CHECK_ARG(p.M > 0 && p.M % bm == 0 && p.N > 0 && p.N % LG_BN == 0, "lgemm: M/N not tile multiples");
+    INF_CHECK_ARG(p.K > 0 && p.K % (256 * p.splits) == 0, "lgemm: K per split must be a multiple of 256");
+    INF_CHECK_ARG(p.lda % 8 == 0 && p.b_row0 % 16 == 0 && p.b_row0 + p.N <= 16 * p.b_tiles, "lgemm: operand layout");
+    INF_CHECK_ARG(p.splits == 1 || p.slab != nullptr, "lgemm: split-K needs a slab");
+    INF_CHECK_ARG(p.slab != nullptr || p.C != nullptr, "lgemm: no output");
+    p.tiles_m = p.M / bm;
+    p.tiles_n = p.N / LG_BN;
+    p.block_begin = blocks;
+    blocks += p.tiles_m * p.tiles_n * p.splits;
+  }
+  b.total_blocks = blocks;
+  if (bm == 64) return launch_typed<64>(b, stream);
+  return launch_typed<32>(b, stream);
+}
+
+}  // namespace inf

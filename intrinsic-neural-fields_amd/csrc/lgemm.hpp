@@ -1,0 +1,55 @@
+// Grouped bf16 GEMM with one operand shared through LDS and the other streamed from an
+// MFMA-fragment-order image straight into registers (see lgemm.hip).
+//
+//   C[m][n] = epilogue( sum_k A[m][k] * B[n][k] )
+//
+//   input GEMM   A = X [rays][k_pad]          B = W_0 / W_y fragment images (adam.hip WF)
+//   dW GEMM      A = In^T [n_in][rays]        B = dZ_l^T fragment image (chain3.hip),
+//                C = dW^T, stored transposed into the split-K slab [n_out][n_in]
+#pragma once
+
+#include "common.hpp"
+
+namespace inf {
+
+constexpr int LGEMM_MAX_PROBLEMS = 12;
+constexpr int LG_BN = 128;  // columns per block: 4 waves x 32
+
+struct LgemmProblem {
+  // A: M rows, K-contiguous: row-major (element (r, k) at r * lda + k) or 16-blocked
+  // (at (k / 16) * lda + r * 16 + k % 16, gemm.hpp a_kblk)
+  const bf16* A;
+  int64_t lda;
+  int32_t a_kblk;
+  // B: fragment image of an R x K matrix: 1 KiB per (32-deep k block kb, 16-row tile t)
+  // at (kb * b_tiles + t) KiB, lane l's 16 bytes at 16 l (row 16 t + l % 16, k = 32 kb +
+  // 8 (l / 16) + e); rows [b_row0, b_row0 + N) of the image are this problem's columns
+  const bf16* Bf;
+  int32_t b_tiles;  // R / 16
+  int32_t b_row0;
+  int32_t M, N, K;  // M % BM == 0, N % 128 == 0, (K / splits) % 256 == 0
+  int32_t splits;
+  // epilogue (non-split): + bias[n], ReLU, row-major C and/or plain transposed CT
+  const float* bias;
+  int32_t relu;
+  void* C;
+  int64_t ldc;
+  int32_t c_f32;
+  bf16* CT;  // [N][ldct]
+  int64_t ldct;
+  // epilogue (split-K): C^T of split s at slab + s * slab_stride + n * slab_ld + m (f32)
+  float* slab;
+  int64_t slab_ld, slab_stride;
+  int32_t tiles_m, tiles_n, block_begin;
+};
+
+struct LgemmBatch {
+  LgemmProblem p[LGEMM_MAX_PROBLEMS];
+  int32_t nprob;
+  int32_t total_blocks;
+};
+
+// Rows per block for an M: 64 (the shapes of config B) or 32.
+int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream);
+
+}  // namespace inf

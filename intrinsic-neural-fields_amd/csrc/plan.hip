@@ -19,6 +19,7 @@
 #include "chain3.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
+#include "lgemm.hpp"
 
 namespace inf {
 
@@ -166,14 +167,20 @@ int build_layout(inf_plan* p) {
     const int bt = (H % 128 == 0) ? 128 : 64;
     gemm_tiles += (g.R / bt) * (g.c_pad / bt);
   }
-  // fragment images of the hidden H x H weights for the register-streamed chain
+  // fragment images (bf16 mode): the hidden H x H weights, forward and transposed, for
+  // the register-streamed chain; W_0 and W_y (forward) for the input GEMM (lgemm.hip)
   if (p->mode == INF_MODE_BF16 && (H == 128 || H == 256)) {
     for (auto& g : p->segs) {
-      if (!g.gemm || g.layer < 1 || g.layer > L - 2 || g.sub != 0 || g.R != H || g.C != H) continue;
+      if (!g.gemm) continue;
+      const bool hidden = g.layer >= 1 && g.layer <= L - 2 && g.sub == 0 && g.R == H && g.C == H;
+      const bool input = (g.layer == 0 && g.sub == 0) || (g.layer == s && g.sub == 1);
+      if (!hidden && !input) continue;
       g.f_off = sh;
-      sh = align_up(sh + (int64_t)H * H * 2);
-      g.ft_off = sh;
-      sh = align_up(sh + (int64_t)H * H * 2);
+      sh = align_up(sh + (int64_t)g.R * g.c_pad * 2);
+      if (hidden) {
+        g.ft_off = sh;
+        sh = align_up(sh + (int64_t)H * H * 2);
+      }
     }
   }
   p->shadow_bytes = sh;
@@ -182,6 +189,10 @@ int build_layout(inf_plan* p) {
   int S = 1;
   const int64_t mb = round_up(std::max(p->max_batch, 1), 128);
   while (gemm_tiles * S < 512 && S < 16 && mb / (S * 2) >= 512) S *= 2;
+  // bf16 steps of the register-streamed chain reduce their weight gradients with lgemm
+  // (896-block grid at 4096 rays already): fewer, longer splits halve the slab traffic
+  // the update launch reads (4096 rays: dW + update 30.8 -> 25.2 us at 4 splits vs 8)
+  if (d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
   if (const char* e = std::getenv("INF_DW_SPLITS")) {  // tuning experiments
     const int want = std::atoi(e);
     if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 128) S = want;
@@ -366,6 +377,42 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
 // with the register-streamed chain (3) Y_0^T comes plain from the input GEMM
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
   const int H = p->H, s = p->s;
+  if (chain == 3) {
+    // register-streamed chain: dZ_l^T is a fragment image (chain3.hip); one lgemm launch
+    // computes every dW^T tile with the layer input (X^T, Y_0^T plain, Y_l^T 16-ray
+    // blocked) through LDS, into the split-K slabs the update launch reduces
+    LgemmBatch lb;
+    std::memset(&lb, 0, sizeof(lb));
+    for (size_t i = 0; i < p->segs.size(); ++i) {
+      const ParamSeg& g = p->segs[i];
+      if (!g.gemm) continue;
+      INF_CHECK_ARG(lb.nprob < LGEMM_MAX_PROBLEMS, "lgemm: too many weight matrices");
+      LgemmProblem& q = lb.p[lb.nprob++];
+      const int l = g.layer;
+      const bool from_input = (l == 0) || (l == s && g.sub == 1);
+      if (from_input) {
+        q.A = p->W<bf16>(p->o_x0t);
+        q.lda = Bp;
+      } else if (l == 1) {
+        q.A = p->W<bf16>(p->o_yt[0]);
+        q.lda = Bp;
+      } else {
+        q.A = p->W<bf16>(p->o_yt[l - 1]);
+        q.lda = (int64_t)H * 16;
+        q.a_kblk = 1;
+      }
+      q.Bf = p->W<bf16>(p->o_dZT[l]);
+      q.b_tiles = H / 16;
+      q.M = g.c_pad;
+      q.N = g.R;
+      q.K = Bp;
+      q.splits = p->dw_splits;
+      q.slab = p->W<float>(p->o_slab[i]);
+      q.slab_ld = g.c_pad;
+      q.slab_stride = (int64_t)g.R * g.c_pad;
+    }
+    return launch_lgemm(lb, 64, st);
+  }
   // weight gradients: one grouped split-K launch (chunks of GEMM_MAX_PROBLEMS)
   std::vector<GemmProblem> probs;
   for (size_t i = 0; i < p->segs.size(); ++i) {
@@ -611,8 +658,9 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
 
 bool use_chain3(const inf_plan* p, int Bp) {
   const ParamSeg* w1 = p->weight_seg(1, 0);
+  // the dW lgemm streams K = Bp / dw_splits rays per block in 256-ray steps
   return use_chain(p) && chain3_supported(p->H, p->L, Bp) && w1 != nullptr && w1->f_off >= 0 &&
-         std::getenv("INF_NO_CHAIN3") == nullptr;
+         (Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0 && std::getenv("INF_NO_CHAIN3") == nullptr;
 }
 
 // Input GEMM of the register-streamed chain, one grouped launch over X (the gathered
@@ -620,6 +668,40 @@ bool use_chain3(const inf_plan* p, int Bp) {
 // Z_y = X W_y^T + b_y, the skip layer's data term in f32 (model.py:43-56, layers.py:60-62).
 int run_input_gemm(inf_plan* p, int Bp, hipStream_t st) {
   const int H = p->H, s = p->s;
+  const ParamSeg* w0 = p->weight_seg(0, 0);
+  const ParamSeg* wy = p->weight_seg(s, 1);
+  if (p->k_pad % 256 == 0 && Bp % 64 == 0 && H % LG_BN == 0 && w0->f_off >= 0 && wy->f_off >= 0 &&
+      std::getenv("INF_NO_LGEMM") == nullptr) {
+    // X via LDS, W_0 / W_y fragment images via registers (lgemm.hip)
+    LgemmBatch lb;
+    std::memset(&lb, 0, sizeof(lb));
+    lb.nprob = 2;
+    for (int i = 0; i < 2; ++i) {
+      LgemmProblem& q = lb.p[i];
+      const ParamSeg* w = i == 0 ? w0 : wy;
+      q.A = p->W<bf16>(p->o_x0);
+      q.lda = p->k_pad;
+      q.Bf = reinterpret_cast<const bf16*>(p->shadow + w->f_off);
+      q.b_tiles = H / 16;
+      q.M = Bp;
+      q.N = H;
+      q.K = p->k_pad;
+      q.splits = 1;
+      q.bias = p->params + (i == 0 ? p->bias_seg(0, 0) : p->bias_seg(s, 1))->off;
+      q.ldc = H;
+      if (i == 0) {
+        q.relu = 1;
+        q.C = p->W(p->o_y[0]);
+        q.CT = p->W<bf16>(p->o_yt[0]);
+        q.ldct = Bp;
+      } else {
+        q.C = p->W(p->o_zy);
+        q.c_f32 = 1;
+      }
+    }
+    const char* bm = std::getenv("INF_LGEMM_BM");  // tuning experiments
+    return launch_lgemm(lb, (bm != nullptr && std::atoi(bm) == 64) ? 64 : 32, st);
+  }
   GemmBatch gb;
   std::memset(&gb, 0, sizeof(gb));
   gb.nprob = 2;
