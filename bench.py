@@ -29,8 +29,7 @@ PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.m
 HBM_PEAK = 8000.0  # GB/s
 KERNEL_NAMES = {"dw_gemm": "gemm_nt_kernel<bf16,128,128> (grouped split-K weight-gradient GEMM)",
                 "chain": "chain_kernel (fused forward + loss + dX chain, LDS weight ring)",
-                "chain3": "chain3_kernel (fused hidden forward + loss + dX chain, register-streamed weights)",
-                "input_gemm": "gemm_nt_kernel<bf16,64,64> (layer 0 + skip data term, grouped)"}
+                "chain3": "chain3_kernel (fused gather + forward + loss + dX chain, register-streamed weights)"}
 
 
 def parse():
@@ -301,20 +300,21 @@ def main():
     ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
     value = world * args.batch / (ms * 1e-3)
 
-    from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_INPUT_GEMM, STAGE_UPDATE
+    from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
     # per-kernel times (HIP events around repeated launches of one stage on its saved inputs)
     stages = {}
     stages["dw_gemm"] = time_stage(tr.plan, STAGE_DW_GEMM)
-    stages["gather"] = time_stage(tr.plan, STAGE_GATHER, batch=tr.batch)
     stages["update"] = time_stage(tr.plan, STAGE_UPDATE)
     chain3 = (args.mode == "bf16" and args.batch <= 8192 and args.hidden in (128, 256)
               and not os.environ.get("INF_NO_CHAIN") and not os.environ.get("INF_NO_CHAIN3"))
     if chain3:
-        stages["input_gemm"] = time_stage(tr.plan, STAGE_INPUT_GEMM)
+        # the gather runs inside the fused chain
         stages["chain3"] = time_stage(tr.plan, STAGE_CHAIN, batch=tr.batch)
-    elif args.mode == "bf16" and not os.environ.get("INF_NO_CHAIN"):
-        stages["chain"] = time_stage(tr.plan, STAGE_CHAIN, batch=tr.batch)
-    mfma_stages = {k: v for k, v in stages.items() if k in ("dw_gemm", "chain", "chain3", "input_gemm")}
+    else:
+        stages["gather"] = time_stage(tr.plan, STAGE_GATHER, batch=tr.batch)
+        if args.mode == "bf16" and not os.environ.get("INF_NO_CHAIN"):
+            stages["chain"] = time_stage(tr.plan, STAGE_CHAIN, batch=tr.batch)
+    mfma_stages = {k: v for k, v in stages.items() if k in ("dw_gemm", "chain", "chain3")}
     dom = max(mfma_stages, key=lambda k: mfma_stages[k][0])
     dom_ms, dom_flops, _ = stages[dom]
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12

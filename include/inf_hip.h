@@ -180,12 +180,11 @@ int inf_render(inf_plan* plan, const inf_batch* batch, const int64_t* hit, const
  *   INF_STAGE_DW_GEMM  - the grouped split-K weight-gradient GEMM
  *   INF_STAGE_UPDATE   - the slab-reduction/Adam/packed-weight launch (reduce only:
  *                        parameters are not modified)
- *   INF_STAGE_CHAIN    - the fused forward + loss + dX-chain kernel (bf16 mode)
- *   INF_STAGE_INPUT_GEMM - layer 0 and the skip layer's data term as one grouped GEMM
- *                        (bf16 steps of <= 8192 rays, register-streamed chain)
+ *   INF_STAGE_CHAIN    - the fused forward + loss + dX-chain kernel (bf16 mode; at
+ *                        <= 8192 rays with the gather fused in)
  * *flops / *bytes receive the stage's algorithmic work per launch (unpadded). */
 enum { INF_STAGE_GATHER = 0, INF_STAGE_FWD_GEMM = 1, INF_STAGE_DW_GEMM = 2, INF_STAGE_UPDATE = 3,
-       INF_STAGE_CHAIN = 4, INF_STAGE_INPUT_GEMM = 5 };
+       INF_STAGE_CHAIN = 4 };
 int inf_run_stage(inf_plan* plan, const inf_batch* batch, int stage, int layer, double* flops, double* bytes,
                   inf_stream_t stream);
 

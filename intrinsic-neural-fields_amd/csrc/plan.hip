@@ -65,7 +65,6 @@ struct inf_plan {
 
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_ws_end = 0;
-  int64_t o_zy = 0;  // skip layer's data term X W_y^T + b_y (f32), register-streamed chain
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
   std::vector<int64_t> o_slab;                            // per param segment (weights)
   int64_t o_hw = 0, o_hb = 0;                             // head partials
@@ -221,7 +220,7 @@ int build_layout(inf_plan* p) {
     p->o_dZT.push_back(take(Bp * H * p->esz));
     p->o_colsum.push_back(take(max_parts * H * 4));
   }
-  p->o_zy = take(std::min<int64_t>(Bp, CHAIN3_MAX_ROWS) * H * 4);
+
   p->o_dz = take(Bp * 3 * 4);
   p->o_pred = take(Bp * 3 * 4);
   p->o_slab.assign(p->segs.size(), 0);
@@ -390,17 +389,10 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
       LgemmProblem& q = lb.p[lb.nprob++];
       const int l = g.layer;
       const bool from_input = (l == 0) || (l == s && g.sub == 1);
-      if (from_input) {
-        q.A = p->W<bf16>(p->o_x0t);
-        q.lda = Bp;
-      } else if (l == 1) {
-        q.A = p->W<bf16>(p->o_yt[0]);
-        q.lda = Bp;
-      } else {
-        q.A = p->W<bf16>(p->o_yt[l - 1]);
-        q.lda = (int64_t)H * 16;
-        q.a_kblk = 1;
-      }
+      // layer inputs as the chain wrote them: 16-ray blocked X^T / Y_{l-1}^T
+      q.A = from_input ? p->W<bf16>(p->o_x0t) : p->W<bf16>(p->o_yt[l - 1]);
+      q.lda = (int64_t)(from_input ? p->k_pad : H) * 16;
+      q.a_kblk = 1;
       q.Bf = p->W<bf16>(p->o_dZT[l]);
       q.b_tiles = H / 16;
       q.M = g.c_pad;
@@ -656,116 +648,37 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
   return launch_chain(a, bm, st);
 }
 
-bool use_chain3(const inf_plan* p, int Bp) {
+bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   const ParamSeg* w1 = p->weight_seg(1, 0);
-  // the dW lgemm streams K = Bp / dw_splits rays per block in 256-ray steps
-  return use_chain(p) && chain3_supported(p->H, p->L, Bp) && w1 != nullptr && w1->f_off >= 0 &&
+  const ParamSeg* w0 = p->weight_seg(0, 0);
+  // the fused gather reads a device-resident bf16 table; the dW lgemm streams
+  // K = Bp / dw_splits rays per block in 256-ray steps
+  return use_chain(p) && chain3_supported(p->H, p->L, p->k_pad, Bp) && w1 != nullptr && w1->f_off >= 0 &&
+         w0->f_off >= 0 && b->table != nullptr && b->table_dtype == INF_DTYPE_BF16 &&
          (Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0 && std::getenv("INF_NO_CHAIN3") == nullptr;
 }
 
-// Input GEMM of the register-streamed chain, one grouped launch over X (the gathered
-// features, already in X0):  Y_0 = relu(X W_0^T + b_0)  (+ Y_0^T for the dW GEMM) and
-// Z_y = X W_y^T + b_y, the skip layer's data term in f32 (model.py:43-56, layers.py:60-62).
-int run_input_gemm(inf_plan* p, int Bp, hipStream_t st) {
-  const int H = p->H, s = p->s;
-  const ParamSeg* w0 = p->weight_seg(0, 0);
-  const ParamSeg* wy = p->weight_seg(s, 1);
-  if (p->k_pad % 256 == 0 && Bp % 64 == 0 && H % LG_BN == 0 && w0->f_off >= 0 && wy->f_off >= 0 &&
-      std::getenv("INF_NO_LGEMM") == nullptr) {
-    // X via LDS, W_0 / W_y fragment images via registers (lgemm.hip)
-    LgemmBatch lb;
-    std::memset(&lb, 0, sizeof(lb));
-    lb.nprob = 2;
-    for (int i = 0; i < 2; ++i) {
-      LgemmProblem& q = lb.p[i];
-      const ParamSeg* w = i == 0 ? w0 : wy;
-      q.A = p->W<bf16>(p->o_x0);
-      q.lda = p->k_pad;
-      q.Bf = reinterpret_cast<const bf16*>(p->shadow + w->f_off);
-      q.b_tiles = H / 16;
-      q.M = Bp;
-      q.N = H;
-      q.K = p->k_pad;
-      q.splits = 1;
-      q.bias = p->params + (i == 0 ? p->bias_seg(0, 0) : p->bias_seg(s, 1))->off;
-      q.ldc = H;
-      if (i == 0) {
-        q.relu = 1;
-        q.C = p->W(p->o_y[0]);
-        q.CT = p->W<bf16>(p->o_yt[0]);
-        q.ldct = Bp;
-      } else {
-        q.C = p->W(p->o_zy);
-        q.c_f32 = 1;
-      }
-    }
-    const char* bm = std::getenv("INF_LGEMM_BM");  // tuning experiments
-    return launch_lgemm(lb, (bm != nullptr && std::atoi(bm) == 64) ? 64 : 32, st);
-  }
-  GemmBatch gb;
-  std::memset(&gb, 0, sizeof(gb));
-  gb.nprob = 2;
-  for (int i = 0; i < 2; ++i) {
-    GemmProblem& q = gb.p[i];
-    q = blank_problem();
-    const ParamSeg* w = i == 0 ? p->weight_seg(0, 0) : p->weight_seg(s, 1);
-    const ParamSeg* bs = i == 0 ? p->bias_seg(0, 0) : p->bias_seg(s, 1);
-    q.A[0] = p->W(p->o_x0);
-    q.lda[0] = p->k_pad;
-    q.B[0] = p->shadow + w->w_off;
-    q.ldb[0] = w->c_pad;
-    q.K[0] = p->k_pad;
-    q.bias0 = p->params + bs->off;
-    q.M = Bp;
-    q.N = H;
-    if (i == 0) {
-      q.relu = 1;
-      q.C = p->W(p->o_y[0]);
-      q.ldc = H;
-      q.CT = p->W(p->o_yt[0]);
-      q.ldct = Bp;
-    } else {
-      q.C = p->W(p->o_zy);
-      q.ldc = H;
-      q.c_f32 = 1;
-    }
-  }
-  GemmTile tile = pick_tile(p, Bp, 2 * H);
-  tile_override("INPUT", &tile);
-  return launch_gemm(gb, p->mode, tile, st);
-}
-
+// Fused gather + forward + loss + dX chain of a bf16 training batch (csrc/chain3.hip).
+// Weight stream: layer 0 over X (k_pad / 32 k-blocks of W_0), the hidden layers (the skip
+// layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
 int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
   const int H = p->H, L = p->L, s = p->s;
+  const int upl = H / 32;
+  const int nx = p->k_pad / (32 * upl);  // stream blocks of X
   Chain3Args a;
   std::memset(&a, 0, sizeof(a));
   a.L = L;
   a.s = s;
   a.H = H;
+  a.k_pad = p->k_pad;
   a.rows = Bp;
   a.batch = b->batch;
-  a.Y0 = p->W<bf16>(p->o_y[0]);
-  a.Zy = p->W<float>(p->o_zy);
-  a.nphase = 2 * (L - 2);
-  for (int ph = 0; ph < a.nphase; ++ph) {
-    const bool fwd = ph < L - 2;
-    const int l = fwd ? ph + 1 : (L - 2) - (ph - (L - 2));
-    const ParamSeg* w = p->weight_seg(l, 0);
-    INF_CHECK_ARG(w != nullptr && w->f_off >= 0, "chain3: fragment image missing");
-    a.img[ph] = reinterpret_cast<const bf16*>(p->shadow + (fwd ? w->f_off : w->ft_off));
-  }
-  for (int l = 0; l <= L - 2; ++l) {
-    a.bias[l] = p->params + p->bias_seg(l, 0)->off;
-    a.YT[l] = p->W<bf16>(p->o_yt[l]);
-    a.dZT[l] = p->W<bf16>(p->o_dZT[l]);
-    a.colsum[l] = p->W<float>(p->o_colsum[l]);
-  }
-  a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
-  a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
-  a.hw_part = p->W<float>(p->o_hw);
-  a.hb_part = p->W<float>(p->o_hb);
-  a.loss_part = p->W<double>(p->o_loss);
-  a.pred = pred;
+  INF_CHECK_ARG(b->table != nullptr && b->table_dtype == INF_DTYPE_BF16, "chain3: bf16 table batch required");
+  a.table = reinterpret_cast<const bf16*>(b->table);
+  a.num_vertices = b->num_vertices;
+  a.vids = b->vids;
+  a.vid_dtype = b->vid_dtype;
+  a.bary = b->bary;
   INF_CHECK_ARG(b->rgb != nullptr, "training batch without target colours");
   a.rgb = b->rgb;
   a.ray_idx = b->ray_idx;
@@ -773,6 +686,48 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.idx_offset = b->idx_offset;
   a.num_rays = b->num_rays;
   a.offset_from_ctrl = b->offset_from_ctrl;
+  auto img = [&](const ParamSeg* w, bool fwd) -> const bf16* {
+    const int64_t off = fwd ? w->f_off : w->ft_off;
+    return off >= 0 ? reinterpret_cast<const bf16*>(p->shadow + off) : nullptr;
+  };
+  auto add = [&](const bf16* im, int kb0, int a_x, int ak0, int phase, int last) -> int {
+    INF_CHECK_ARG(im != nullptr, "chain3: fragment image missing");
+    INF_CHECK_ARG(a.nblk < C3_MAX_BLOCKS, "chain3: too many weight-stream blocks");
+    C3Block& blk = a.blk[a.nblk++];
+    blk.img = im;
+    blk.kb0 = kb0;
+    blk.a_x = a_x;
+    blk.ak0 = ak0;
+    blk.phase = phase;
+    blk.last = last;
+    return INF_OK;
+  };
+  int rc;
+  for (int i = 0; i < nx; ++i)
+    if ((rc = add(img(p->weight_seg(0, 0), true), i * upl, 1, i * upl, 0, i == nx - 1))) return rc;
+  for (int l = 1; l <= L - 2; ++l) {
+    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, l != s))) return rc;
+    if (l == s)
+      for (int i = 0; i < nx; ++i)
+        if ((rc = add(img(p->weight_seg(s, 1), true), i * upl, 1, i * upl, l, i == nx - 1))) return rc;
+  }
+  for (int l = L - 2; l >= 1; --l)
+    if ((rc = add(img(p->weight_seg(l, 0), false), 0, 0, 0, (L - 1) + (L - 2 - l), 1))) return rc;
+  a.nphase = 2 * L - 3;
+  for (int l = 0; l <= L - 2; ++l) {
+    a.bias[l] = p->params + p->bias_seg(l, 0)->off;
+    a.YT[l] = p->W<bf16>(p->o_yt[l]);
+    a.dZT[l] = p->W<bf16>(p->o_dZT[l]);
+    a.colsum[l] = p->W<float>(p->o_colsum[l]);
+  }
+  a.bias_y = p->params + p->bias_seg(s, 1)->off;
+  a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
+  a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
+  a.XT = p->W<bf16>(p->o_x0t);
+  a.hw_part = p->W<float>(p->o_hw);
+  a.hb_part = p->W<float>(p->o_hb);
+  a.loss_part = p->W<double>(p->o_loss);
+  a.pred = pred;
   a.loss = b->loss >= 0 ? b->loss : p->d.loss;
   INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
   const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
@@ -1005,11 +960,9 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   int ck = 0;
   int Bp3 = 0;
   if ((rc = pad_batch(p, batch->batch, true, &Bp3))) return rc;
-  if (use_chain3(p, Bp3)) {
-    // gather -> input GEMM -> register-streamed chain -> dW GEMM (-> update below)
+  if (use_chain3(p, batch, Bp3)) {
+    // fused gather + chain -> dW GEMM (-> update below)
     const int Bp = Bp3;
-    if ((rc = run_input(p, batch, Bp, true, st))) return rc;
-    if ((rc = run_input_gemm(p, Bp, st))) return rc;
     if ((rc = run_chain3(p, batch, Bp, pred, st))) return rc;
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
     p->saved = false;
@@ -1121,22 +1074,16 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       const double Lh = p->L;
       if (p->last_chain == 3) {
         rc = run_chain3(p, b, Bp, nullptr, st);
-        f = 2.0 * 2.0 * B * ((Lh - 2) * H * H + 3 * H);
-        // hidden weights streamed by every workgroup + Y_0 / Z_y tiles in, Y^T / dZ^T out
-        by = (double)(Bp / chain3_bm(Bp)) * 2.0 * (Lh - 2) * H * H * e + B * H * (e + 4.0) +
-             B * (2.0 * Lh - 5) * H * e;
+        f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+        // every workgroup streams W_0, W_y and the hidden weights twice over (L2 -> CU);
+        // three table rows per ray in; X^T, Y^T, dZ^T out
+        by = (double)(Bp / chain3_bm(Bp)) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * e +
+             B * (3.0 * p->k_pad * e + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * e;
       } else {
         rc = run_chain(p, b, Bp, true, nullptr, nullptr, nullptr, nullptr, st);
         f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
         by = B * (2.0 * p->k_pad * e + 2.0 * (Lh - 1) * H * e) + 2.0 * 4 * p->P;
       }
-      break;
-    }
-    case INF_STAGE_INPUT_GEMM: {
-      INF_CHECK_ARG(p->last_chain == 3, "input GEMM stage needs a register-chain training step");
-      rc = run_input_gemm(p, Bp, st);
-      f = 2.0 * B * 2.0 * k * H;
-      by = B * p->k_pad * e + 2.0 * H * p->k_pad * e + B * H * (2.0 * e + 4.0);
       break;
     }
     case INF_STAGE_UPDATE: {

@@ -20,7 +20,7 @@ MODE_FP32, MODE_BF16 = 0, 1
 LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
 LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
-STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN, STAGE_INPUT_GEMM = 0, 1, 2, 3, 4, 5
+STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
 STEP_ADAM, STEP_ADVANCE = 1, 2  # inf_train_step flags
 
 c_void_p, c_int, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int32,

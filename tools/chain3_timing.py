@@ -31,8 +31,8 @@ b = plan.make_batch(source=src, batch=B)
 for _ in range(3):
     plan.train_step(b, None, apply_adam=True)
 torch.cuda.synchronize()
-nphase = 2 * (L - 2)
-names = [f"fwd{l}" for l in range(1, L - 1)] + [f"bwd{l}" for l in range(L - 2, 0, -1)]
+nphase = 2 * L - 3
+names = [f"fwd{l}" for l in range(0, L - 1)] + [f"bwd{l}" for l in range(L - 2, 0, -1)]
 
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
@@ -42,7 +42,7 @@ ev1.record()
 torch.cuda.synchronize()
 print(f"chain3 stage: {ev0.elapsed_time(ev1) / 50 * 1e3:.1f} us  (B={B}, {nphase} phases)")
 
-n1 = 3 * nphase + 6
+n1 = 5 * nphase + 6
 stamps = torch.zeros(2 * n1, dtype=torch.int64, device="cuda")
 lib.inf_debug_timing(plan.handle, ctypes.c_void_p(stamps.data_ptr()), nphase)
 for _ in range(5):
@@ -55,11 +55,14 @@ for w, name in enumerate(("first", "last")):
     t = st[w] - st[w][0]
     e = 3 * nphase + 3
     print(f"workgroup {name}: entry -> end {t[e - 1]:.2f} us, startup {t[1]:.2f} us "
-          f"(issued {t[e]:.2f}, Y0 tile in LDS {t[e + 1]:.2f}, barrier 0 {t[e + 2]:.2f})")
+          f"(fragments issued {t[e]:.2f}, feature tile gathered {t[e + 1]:.2f}, barrier 0 {t[e + 2]:.2f})")
     rows = []
     for p in range(nphase):
         mm = t[2 + 3 * p] - t[1 + 3 * p]
         ep = t[3 + 3 * p] - t[2 + 3 * p]
-        rows.append(f"{names[p]}: mfma {mm:.2f} epi {ep:.2f}")
+        b1 = t[3 * nphase + 6 + p] - t[2 + 3 * p]
+        body = t[4 * nphase + 6 + p] - t[3 * nphase + 6 + p]
+        b2 = t[3 + 3 * p] - t[4 * nphase + 6 + p]
+        rows.append(f"{names[p]}: mfma {mm:.2f} epi {ep:.2f} (B1 wait {b1:.2f}, body {body:.2f}, B2 wait {b2:.2f})")
     print("   " + "\n   ".join(rows))
 print("entry skew last-first:", (st[1][0] - st[0][0]), "us")
