@@ -27,7 +27,7 @@ import torch  # noqa: E402
 
 PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0  # GB/s
-KERNEL_NAMES = {"dw_gemm": "gemm_nt_kernel<bf16,128,128> (grouped split-K weight-gradient GEMM)",
+KERNEL_NAMES = {"dw_gemm": "lgemm_kernel (grouped split-K weight-gradient GEMM, fragment-image B operand)",
                 "chain": "chain_kernel (fused forward + loss + dX chain, LDS weight ring)",
                 "chain3": "chain3_kernel (fused gather + forward + loss + dX chain, register-streamed weights)"}
 
@@ -320,7 +320,9 @@ def main():
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     dw_ms = stages["dw_gemm"][0]
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "dw_gemm_traffic.json")
+    # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of
+    # this same command (tools/profile.sh: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md)
+    pmc_path = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(pmc_path):
         try:
             traffic = json.load(open(pmc_path)).get(f"{dom}_{args.mode}_B{args.batch}")

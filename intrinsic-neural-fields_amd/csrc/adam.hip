@@ -159,10 +159,13 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
     for (int j = 0; j < 4; ++j) tile[cl + j][r] = w[i][j];
     if constexpr (sizeof(T) == 2) {
       if (seg.WF != nullptr && ok[i]) {
-        // forward fragment image: 4 consecutive k of one lane's 8 (gc % 4 == 0)
+        // forward fragment image: 4 consecutive k of one lane's 8 (gc % 4 == 0), in natural
+        // or accumulator k order (adam.hpp wf_acc_order)
         const int gr = item.r0 + r;
-        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * ((gc & 31) >> 3)) * 8 +
-                          (gc & 7);
+        const int kk = gc & 31;
+        const int slot = seg.wf_acc_order ? (kk & 15) >> 2 : kk >> 3;
+        const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
+        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
         const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
       }
@@ -171,14 +174,15 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
   __syncthreads();
   if constexpr (sizeof(T) == 2) {
     if (seg.WTF != nullptr) {
-      // backward fragment image: thread (column c, 8-row group) stores one lane's 16 bytes
-      const int cc = tid >> 3, rg = tid & 7;
-      const int gcc = item.c0 + cc, gr = item.r0 + rg * 8;
-      if (gcc < seg.C && gr + 7 < seg.R) {
+      // backward fragment image, accumulator k order: thread (column c, 32-row block kbl,
+      // row group g) stores one lane's 16 bytes = rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3
+      const int cc = tid >> 3, kbl = (tid >> 2) & 1, g = tid & 3;
+      const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
+      if (gcc < seg.C && gr + 31 < seg.R) {
         bf16x8 v;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][rg * 8 + e];
-        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * ((gr & 31) >> 3)) * 8;
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
+        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
         *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
       }
     }

@@ -20,11 +20,16 @@ struct AdamSeg {
   void* WT;             // packed [C_pad][ldwt] transposed weight
   int64_t ldwt;
   // bf16 weight images in MFMA fragment order for the register-streamed chain (chain3.hip),
-  // hidden H x H weights only (else null): 1 KiB per (32-deep k block kb, 16-column tile t)
-  // at (kb * (H/16) + t) KiB, lane l's 8 elements at 16 l bytes: lane l = n % 16 + 16 (k % 32 / 8)
-  // holds k = 32 kb + 8 (l / 16) + e of column n = 16 t + l % 16
+  // W_0, W_y (forward) and the hidden H x H weights (both): 1 KiB per (32-deep k block kb,
+  // 16-row tile t) at (kb * (rows/16) + t) KiB, lane l's 8 elements at 16 l bytes: lane
+  // l = n % 16 + 16 g holds 8 k of block kb (slot g, see wf_acc_order) of row n = 16 t + l % 16
   void* WF;             // forward: n = output row r, k = input column c
   void* WTF;            // backward (dX): n = input column c, k = output row r
+  // k order inside a 32-deep block: 0 = natural (slot g, element e <-> k = 8 g + e: the input
+  // layers, fed the gathered features), 1 = accumulator order (k = 16 (e / 4) + 4 g + e % 4:
+  // fed activations straight from 16x16x32 accumulators, chain3.hip).  WTF: always 1.
+  int32_t wf_acc_order;
+  int32_t pad_;
 };
 
 // Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = 8 elements.

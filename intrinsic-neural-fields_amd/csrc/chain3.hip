@@ -13,21 +13,32 @@
 // and leaves what the weight-gradient GEMM needs: X^T, Y_l^T, dZ_l^T, bias partials.
 //
 // Why registers, not an LDS ring.  At 16 rays per workgroup every weight element feeds
-// exactly one wave (the 4 waves split the output columns), so staging weights through
-// LDS buys no reuse; what bounds the kernel is the L2 -> CU weight stream.  The packed
-// weights are stored in MFMA fragment order (adam.hip: 1 KiB per 16 columns x 32 k,
-// lane l's 16 bytes at 16 l), so a wave's B operand for one 32-deep k block is TN
-// coalesced 1 KiB loads straight into VGPRs.  The weight stream is a list of blocks
-// (C3Block: UPL k-blocks each, one hidden layer's K); each wave keeps a ring of D k-blocks
-// of fragments in flight and refills a slot right after its MFMAs consumed it -- across
-// block, phase and epilogue boundaries, with no per-k-step barrier.  After the gather the
-// only vector-memory instructions of the compute waves are these loads, so the
-// compiler's vmcnt waits are exact (each waits for one k-block).
+// exactly one wave (the 8 compute waves split the output features), so staging weights
+// through LDS buys no reuse; what bounds the kernel is the L2 -> CU weight stream.  The
+// packed weights are stored in MFMA fragment order (adam.hip: 1 KiB per 16 rows x 32 k,
+// lane l's 16 bytes at 16 l), so a wave's operand for one 32-deep k block is TN coalesced
+// 1 KiB loads straight into VGPRs.  The weight stream is a list of blocks (C3Block: UPL
+// k-blocks each, one hidden layer's K); each wave keeps a ring of D k-blocks of fragments
+// in flight and refills a slot right after its MFMAs consumed it -- across block, phase
+// and epilogue boundaries, with no per-k-step barrier.  After the gather the only
+// vector-memory instructions of the compute waves are these loads, so the compiler's
+// vmcnt waits are exact (each waits for one k-block).  Eight compute waves (two per SIMD)
+// keep twice the loads of four in flight: the L2 -> CU stream rate grows with them
+// (tools/microbench/l2ring.hip).
+//
+// Orientation.  The weights are the A operand and the 16 rays the B operand, so a wave's
+// accumulators hold Z^T: lane l has ray l % 16 and features 16 t + 4 (l / 16) + r.  Eight
+// such values of a tile pair (2q, 2q + 1) are exactly the lane's B operand of k block q of
+// the next layer, with the k order inside the block permuted (slot (g, e) = feature
+// 16 (e / 4) + 4 g + e % 4); the weight images of the layers fed by activations are written
+// in that order (adam.hip, wf_acc_order).  An epilogue therefore stores each lane's
+// activations to the LDS tile with one 16-byte write per k block, and nothing has to be
+// transposed on the compute waves' critical path.
 //
 // Stores.  Every global output (X^T, Y^T, dZ^T, bias / output-layer partials, loss, pred)
-// is written into LDS by the compute waves and copied out by a fifth "store" wave that
-// mirrors the compute waves' barriers.  Stores in the compute waves would join the
-// in-order vmcnt queue and make the next fragment wait for their completion.
+// is copied to HBM by a ninth "store" wave that mirrors the compute waves' barriers and
+// does the ray-major -> feature-major transposes from the LDS tile.  Stores in the compute
+// waves would join the in-order vmcnt queue and make the next fragment wait for them.
 #include "chain3.hpp"
 
 namespace inf {
@@ -36,9 +47,12 @@ namespace {
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4x8 __attribute__((ext_vector_type(8)));
 
 constexpr float C3_CAUCHY_C2 = (20.f / 255.f) * (20.f / 255.f);
-constexpr int C3_THREADS = 320;  // 4 compute waves + 1 store wave
+constexpr int C3_CW = 8;                      // compute waves
+constexpr int C3_CT = C3_CW * 64;             // compute threads
+constexpr int C3_THREADS = C3_CT + 64;        // + the store wave
 constexpr int C3_LDS_CAP = 160 * 1024;
 #ifndef C3_DEPTH
 #define C3_DEPTH 4
@@ -48,34 +62,33 @@ constexpr int C3BM = 16;  // rays per workgroup
 template <int H>
 struct L3 {
   static constexpr int BM = C3BM;
-  static constexpr int TN = H / 64;   // 16-column tiles per wave (a wave owns H/4 columns)
-  static constexpr int WN = H / 4;
-  static constexpr int UPL = H / 32;  // 32-deep k blocks per hidden layer (= per stream block)
-  static constexpr int NT = H / 16;   // 16-row tiles per k block of a weight image
-  static constexpr int ACT_ROW = H * 2;
-  static constexpr int TILE_BYTES = BM * H * 2;
-  static constexpr int BOX_BYTES = TILE_BYTES + H * 4;  // Y^T / dZ^T tile + bias partial
-  static constexpr int OFF_ACT = 0;
-  static constexpr int OFF_BOX = OFF_ACT + BM * ACT_ROW;
-  static constexpr int OFF_HW = OFF_BOX + 2 * BOX_BYTES;  // [3][H] output-layer weight grad
+  static constexpr int TN = H / (16 * C3_CW);  // 16-feature tiles per wave (2: H = 256, 1: H = 128)
+  static constexpr int WN = H / C3_CW;          // features per wave
+  static constexpr int UPL = H / 32;            // 32-deep k blocks per hidden layer (= per stream block)
+  static constexpr int NT = H / 16;             // 16-row tiles per k block of a weight image
+  static constexpr int ACT_BYTES = BM * H * 2;
+  static constexpr int OFF_ACT = 0;                       // activation / dZ tile (act_off layout)
+  static constexpr int OFF_CS = OFF_ACT + ACT_BYTES;      // [H] bias-gradient partial of a phase
+  static constexpr int OFF_HW = OFF_CS + H * 4;           // [3][H] output-layer weight grad
   static constexpr int OFF_HB = OFF_HW + 3 * H * 4;       // [4]
   static constexpr int OFF_LS = OFF_HB + 16;              // [2] f64 loss / SSE
   static constexpr int OFF_PRED = OFF_LS + 16;            // [BM][3]
-  static constexpr int OFF_DZ = OFF_PRED + BM * 12;       // [4 waves][BM][3] head gradient
-  static constexpr int OFF_TGT = OFF_DZ + 4 * BM * 12;    // [BM][3] targets
-  static constexpr int OFF_ZP = OFF_TGT + BM * 12;        // [4 waves][BM][3] head partial sums
-  static constexpr int OFF_RAY = OFF_ZP + 4 * BM * 12;    // [BM][4] vertex ids, [BM][3] ok
+  static constexpr int OFF_DZ = OFF_PRED + BM * 12;       // [waves][BM][3] head gradient
+  static constexpr int OFF_TGT = OFF_DZ + C3_CW * BM * 12;  // [BM][3] targets
+  static constexpr int OFF_ZP = OFF_TGT + BM * 12;        // [waves][BM][3] head partial sums
+  static constexpr int OFF_RAY = OFF_ZP + C3_CW * BM * 12;  // [BM][4] vertex ids, [BM][3] ok
   static constexpr int OFF_RBARY = OFF_RAY + BM * 16 + BM * 12 + 16;  // [BM][3] barycentrics
   static constexpr int OFF_W7 = OFF_RBARY + BM * 12 + 16;  // [3][H] then b7[3]
   static constexpr int OFF_VEC = OFF_W7 + 3 * H * 4 + 16;  // biases [L-1][H], then Ly.bias [H]
   // ReLU bits: per layer one 32-bit word per compute lane, bit j*4 + r for accumulator
   // element (j, r) of that lane
-  static constexpr int MASK_BYTES = 256 * 4;
+  static constexpr int MASK_BYTES = C3_CT * 4;
   __host__ __device__ static int off_mask(int L) { return OFF_VEC + L * H * 4; }
   __host__ __device__ static int off_x(int L) { return off_mask(L) + (L - 2) * MASK_BYTES; }
   __host__ __device__ static int off_stamp(int L, int k_pad) { return off_x(L) + BM * k_pad * 2; }
-  static int lds_bytes(int L, int k_pad) { return off_stamp(L, k_pad) + (5 * C3_MAX_PHASES + 8) * 8; }
-  static_assert(TN * 4 <= 32, "ReLU bits of a lane must fit one word");
+  static int lds_bytes(int L, int k_pad) { return off_stamp(L, k_pad) + (7 * C3_MAX_PHASES + 8) * 8; }
+  static_assert(TN >= 1 && TN * 4 <= 32, "ReLU bits of a lane must fit one word");
+  static_assert(OFF_LS % 8 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
 
 // byte offset of element (row, col) of a bf16 LDS tile with `rowb`-byte rows: 16-byte
@@ -85,16 +98,15 @@ __device__ __forceinline__ int tile_off(int rowb, int row, int col) {
   return row * rowb + (((col >> 3) ^ (row & 15)) << 4) + ((col & 7) << 1);
 }
 
-// element (col, ray r) of a Y^T box: the 16-ray blocked layout of the dW GEMM's A operand
-// (lgemm a_kblk), the whole tile contiguous in global memory
-__device__ __forceinline__ int box_off(int col, int r) { return (col * 16 + r) * 2; }
-
-// element (col, ray r < 16) of a dZ^T box: the fragment image the dW GEMM streams
-// (lgemm operand B: rows = columns of dZ, k = rays): per 16-column tile one 512-byte
-// piece = the workgroup's half (16 of 32 rays) of that tile's 1 KiB k-block
-__device__ __forceinline__ int frag_box_off(int col, int r) {
-  return (col >> 4) * 512 + ((col & 15) + 16 * (r >> 3)) * 16 + (r & 7) * 2;
-}
+// The activation tile: per 32-feature k block q one 1 KiB block of B-operand fragments,
+// slot (ray, g) = the 16 bytes of lane ray + 16 g, element e = feature 32 q + 16 (e / 4) +
+// 4 g + e % 4 (accumulator order).  The slot of (ray, g) sits at ray ^ act_swz(q, g): the
+// store wave's transposing reads (one ray of 16 row groups x 2 halves per 32-lane half)
+// then hit 32 distinct 8-byte bank pairs, and the MFMA operand reads stay conflict-free
+// (act_swz(q, g) ^ act_swz(q, g ^ 1) = 12 keeps the two row groups of every ds_read_b128
+// lane group on complementary ray sets).
+__device__ __forceinline__ int act_swz(int q, int g) { return ((q & 3) << 1) ^ ((g & 1) * 12) ^ (g >> 1); }
+__device__ __forceinline__ int act_off(int q, int ray, int g) { return q * 1024 + (((ray ^ act_swz(q, g)) + 16 * g) << 4); }
 
 __device__ __forceinline__ unsigned short bf_bits3(float x) {
   bf16 h = (bf16)x;
@@ -102,13 +114,48 @@ __device__ __forceinline__ unsigned short bf_bits3(float x) {
 }
 __device__ __forceinline__ float bf_val3(unsigned short u) { return (float)__builtin_bit_cast(bf16, u); }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_QUAD_1032 = 0xB1, DPP_QUAD_2301 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140,
+              DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;
+
 // Sum over the 16 lanes of a row (lanes 16 q .. 16 q + 15) with DPP adds.
 __device__ __forceinline__ float row_sum16(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  v += dpp_mov<DPP_QUAD_1032>(v);
+  v += dpp_mov<DPP_QUAD_2301>(v);
+  v += dpp_mov<DPP_HALF_MIRROR>(v);
+  v += dpp_mov<DPP_MIRROR>(v);
   return v;
+}
+
+// One reduce-scatter step over a DPP lane pairing: v[0, 2M) -> v[0, M), keeping the half
+// selected by `hi` and adding the partner lane's copy of it (the partner keeps the other).
+template <int M, int CTRL>
+__device__ __forceinline__ void halve(float* v, bool hi) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float keep = hi ? v[i + M] : v[i];
+    const float give = hi ? v[i] : v[i + M];
+    v[i] = keep + dpp_mov<CTRL>(give);
+  }
+}
+
+// Sums over the 16 rays of a row group (lanes of a row) of NV values per lane, scattered:
+// lane i returns the sum of value i % NV.  log2(NV) halving steps on pairings that flip
+// lane bits {3} (NV = 16 only), {0,1,2}, {1}, {0} -- each keeps the lanes that still share
+// a value set together -- then rotations complete the sum over the remaining lanes.
+template <int NV>
+__device__ __forceinline__ float ray_sum(float* v, int lane) {
+  static_assert(NV == 4 || NV == 8 || NV == 16, "values per lane");
+  if constexpr (NV == 16) halve<8, DPP_ROR8>(v, lane & 8);
+  if constexpr (NV >= 8) halve<4, DPP_HALF_MIRROR>(v, lane & 4);
+  halve<2, DPP_QUAD_2301>(v, lane & 2);
+  halve<1, DPP_QUAD_1032>(v, lane & 1);
+  if constexpr (NV == 4) v[0] += dpp_mov<DPP_ROR4>(v[0]);
+  if constexpr (NV <= 8) v[0] += dpp_mov<DPP_ROR8>(v[0]);
+  return v[0];
 }
 
 // Sum over lanes l, l ^ 16, l ^ 32, l ^ 48 (the four row groups of an accumulator column)
@@ -134,10 +181,12 @@ template <int H, int LOSS>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
   using C = L3<H>;
   constexpr int BM = C::BM, TN = C::TN, UPL = C::UPL;
+  constexpr int NV = TN * 4;  // accumulator values per lane
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = a.L;
   const int k_pad = a.k_pad;
   char* act = smem + C::OFF_ACT;
+  float* csb = reinterpret_cast<float*>(smem + C::OFF_CS);
   float* hws = reinterpret_cast<float*>(smem + C::OFF_HW);
   float* hbs = reinterpret_cast<float*>(smem + C::OFF_HB);
   double* lss = reinterpret_cast<double*>(smem + C::OFF_LS);
@@ -145,8 +194,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   float* dzs = reinterpret_cast<float*>(smem + C::OFF_DZ);
   float* tgs = reinterpret_cast<float*>(smem + C::OFF_TGT);
   float* zps = reinterpret_cast<float*>(smem + C::OFF_ZP);
-  int* rvid = reinterpret_cast<int*>(smem + C::OFF_RAY);                 // [BM][4]
-  float* rbary = reinterpret_cast<float*>(smem + C::OFF_RBARY);         // [BM][3]
+  int* rvid = reinterpret_cast<int*>(smem + C::OFF_RAY);          // [BM][4]
+  float* rbary = reinterpret_cast<float*>(smem + C::OFF_RBARY);  // [BM][3]
   float* w7s = reinterpret_cast<float*>(smem + C::OFF_W7);
   float* vecs = reinterpret_cast<float*>(smem + C::OFF_VEC);
   unsigned* maskw = reinterpret_cast<unsigned*>(smem + C::off_mask(L));
@@ -162,28 +211,30 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   const int nfwd = L - 1;  // forward phases 0..L-2
 
   unsigned long long* stl = nullptr;  // diagnostics only
-  if (a.stamps != nullptr && wave == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+  // wave 0 records everything; the last compute wave and the store wave their B1 arrivals
+  const bool stamp_wg = a.stamps != nullptr && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
+  if (stamp_wg && (wave == 0 || wave == C3_CW - 1 || wave == C3_CW))
     stl = reinterpret_cast<unsigned long long*>(smem + C::off_stamp(L, k_pad));
   const unsigned long long t_entry = stl != nullptr ? wall_clock64() : 0ull;
   auto stamp = [&](int i) {
     if (stl != nullptr) {
       __builtin_amdgcn_sched_barrier(0);
       const unsigned long long t = wall_clock64();
-      if (lane == 0) stl[i] = t;
+      if (lane == 0 && (wave == 0 || i >= 5 * nphase + 6)) stl[i] = t;
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  if (wave < 4) {
+  if (wave < C3_CW) {
     // =========================== compute waves ============================================
     const int wc = wave;
-    // fragment ring: D k-blocks (D * TN KiB per wave) in flight; 16 KiB per wave kept the
-    // L2 -> CU stream at its best rate in tools/microbench/l2ring (32 KiB: -35 %)
+    const int t0 = wc * TN;  // the wave's first 16-feature tile
+    // fragment ring: D k-blocks (D * TN KiB per wave) in flight
     constexpr int D = C3_DEPTH < UPL ? C3_DEPTH : UPL;
     bf16x8 fr[D][TN];
     // buffer loads: descriptor per image in SGPRs, k-block offset in soffset, tile offset
     // as the immediate, one VGPR of lane offset -- no 64-bit address registers
-    const unsigned lane_off = (unsigned)(wc * TN * 64 + lane) * 16u;
+    const unsigned lane_off = (unsigned)(t0 * 64 + lane) * 16u;
     auto rsrc_of = [&](const bf16* img) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(img), (short)0, 0x7FFFFFFF, 0x00020000);
     };
@@ -210,11 +261,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       }
       rvid[rl * 4 + i] = v;
       rbary[rl * 3 + i] = w;
-      // the ray's flag: all three corners in range (bit i per corner, summed by the gather)
       rvid[BM * 4 + tid] = ok;
     }
     // the first block's fragments, in k order (the loop's waits assume that order); issued
-    // after the dependent ray-record loads so those are not queued behind 64 KiB per CU
+    // after the dependent ray-record loads so those are not queued behind them
     {
       const __amdgpu_buffer_rsrc_t rs0 = rsrc_of(a.blk[0].img);
 #pragma unroll
@@ -233,17 +283,17 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     {
       const int cpr = k_pad >> 3;          // chunks per row
       const int nch = BM * cpr;            // chunks of the tile
-      constexpr int GR = 8;                // chunks per thread per round (k_pad 1024: one round)
+      constexpr int GR = 4;                // chunks per thread per round (k_pad 1024: one round)
       const __amdgpu_buffer_rsrc_t rt =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.table), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll 1
-      for (int q0 = tid; q0 < nch; q0 += 256 * GR) {
+      for (int q0 = tid; q0 < nch; q0 += C3_CT * GR) {
         u16x8 ev[GR][3];
         float wv[GR][3];
         int okv[GR];
 #pragma unroll
         for (int g = 0; g < GR; ++g) {
-          const int q = q0 + 256 * g;
+          const int q = q0 + C3_CT * g;
           const int r = (q < nch ? q : 0) / cpr, ch = (q < nch ? q : 0) % cpr;
           okv[g] = q < nch ? (rvid[BM * 4 + r * 3] & rvid[BM * 4 + r * 3 + 1] & rvid[BM * 4 + r * 3 + 2]) : 0;
 #pragma unroll
@@ -255,7 +305,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
 #pragma unroll
         for (int g = 0; g < GR; ++g) {
-          const int q = q0 + 256 * g;
+          const int q = q0 + C3_CT * g;
           if (q < nch) {
             const int r = q / cpr, ch = q % cpr;
             u16x8 o;
@@ -274,7 +324,53 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     lbar();  // barrier 0: feature tile in LDS
     stamp(3 * nphase + 5);
 
-    unsigned* my_mask = maskw + tid;  // + layer * 256
+    unsigned* my_mask = maskw + tid;  // + layer * C3_CT
+    // B-operand slot offsets of this lane inside a k block of the activation tile (the
+    // swizzle repeats every 4 k blocks)
+    int aoffs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) aoffs[q] = act_off(q, r16, g4) - q * 1024;
+    const char* xlane = xs + r16 * xrow;
+    // the lane's accumulator element (j, r) is ray r16, feature feat(j) + r
+    auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
+    // activations / dZ -> the LDS tile: one 16-byte write per k block (tile pair), 8 bytes
+    // for a lone tile (H = 128: a wave owns half a k block)
+    auto put_act = [&](const float (&v)[TN][4]) {
+      if constexpr (TN % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; j += 2) {
+          u16x8 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            o[r] = bf_bits3(v[j][r]);
+            o[4 + r] = bf_bits3(v[j + 1][r]);
+          }
+          *reinterpret_cast<u16x8*>(act + act_off((t0 + j) >> 1, r16, g4)) = o;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          u16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = bf_bits3(v[j][r]);
+          const int t = t0 + j;
+          *reinterpret_cast<u16x4*>(act + act_off(t >> 1, r16, g4) + 8 * (t & 1)) = o;
+        }
+      }
+    };
+    // sums over the 16 rays of per-lane values v[j][r] -> dst[feature] (lane r16 < NV
+    // holds value r16 after the reduce-scatter)
+    auto ray_sums_to = [&](const float (&v)[TN][4], float* dst) {
+      float t[NV];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[j * 4 + r] = v[j][r];
+      const float s = ray_sum<NV>(t, lane);
+      const int idx = r16 % NV;
+      if (r16 < NV) dst[feat(idx >> 2) + (idx & 3)] = s;
+    };
+
     f32x4 acc[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -288,91 +384,78 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       // of block i+1 (the last block reloads itself: harmless loads keep waits exact)
       const __amdgpu_buffer_rsrc_t crs = rsrc_of(B.img);
       const __amdgpu_buffer_rsrc_t nrs = rsrc_of(Bn.img);
-      const char* abase = B.a_x ? xs : act;
-      const int arow = B.a_x ? xrow : C::ACT_ROW;
+      const bool from_x = B.a_x != 0;
       const int ak0 = B.ak0, ckb = B.kb0, nkb = Bn.kb0;
 #pragma unroll
       for (int kb = 0; kb < UPL; ++kb) {
-        const bf16x8 av =
-            *reinterpret_cast<const bf16x8*>(abase + r16 * arow + ((((ak0 + kb) * 4 + g4) ^ r16) << 4));
+        // B operand: the feature tile (natural k order) or the activation tile
+        const char* bp = from_x ? xlane + ((((ak0 + kb) * 4 + g4) ^ r16) << 4) : act + kb * 1024 + aoffs[kb & 3];
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bp);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, fr[kb % D][j], acc[j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[j], 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
         __builtin_amdgcn_sched_barrier(0);
       }
+#ifdef C3_STREAM_ONLY  // diagnostics: the weight stream and MFMAs alone (wrong results);
+                      // with C3_STREAM_BARRIERS also the two barriers per phase
+      if (B.last) {
+        stamp(2 + 3 * B.phase);
+#ifdef C3_STREAM_BARRIERS
+        lbar();
+        lbar();
+#endif
+      }
+      continue;
+#endif
       if (!B.last) continue;
 
-      // ---- epilogue of phase p: LDS reads first, then arithmetic, then LDS writes -------
+      // ---- epilogue of phase p ---------------------------------------------------------
       const int p = B.phase;
-      stamp(2 + 3 * p);
-      lbar();  // B1: every wave is done reading the activation tile
+      stamp(wave == 0 ? 2 + 3 * p : 6 * nphase + 6 + p);
+      lbar();  // B1: every wave is done reading the activation tile; the store wave has copied it
       stamp(3 * nphase + 6 + p);
-      char* box = smem + C::OFF_BOX + (p & 1) * C::BOX_BYTES;
-      float* csb = reinterpret_cast<float*>(box + C::TILE_BYTES);
       if (p < nfwd) {
-        // forward of layer l: bias (+ Ly.bias at the skip layer) + ReLU -> tile, Y^T, bits
+        // forward of layer l: bias (+ Ly.bias at the skip layer) + ReLU -> tile, bits
         const int l = p;
         const bool skip = l == a.s;
         const bool last = l == L - 2;
-        float bv[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = wc * C::WN + j * 16 + r16;
-          bv[j] = vecs[l * H + col];
-        }
-        float by[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) by[j] = skip ? vecs[(L - 1) * H + wc * C::WN + j * 16 + r16] : 0.f;
         float hq[TN][4];  // bf16-rounded activations as f32
         unsigned bits = 0;
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+          f32x4 yv = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (skip) yv = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v = acc[j][r] + bv[j];
-            if (skip) v += by[j];
+            float v = acc[j][r] + bv[r];
+            if (skip) v += yv[r];
             v = fmaxf(v, 0.f);
             hq[j][r] = bf_val3(bf_bits3(v));
             bits |= (hq[j][r] > 0.f ? 1u : 0u) << (j * 4 + r);
           }
+        }
         if (!last) {
-          my_mask[l * 256] = bits;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int col = wc * C::WN + j * 16 + r16;
-            const int row0 = g4 * 4;
-            u16x4 q;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              q[r] = bf_bits3(hq[j][r]);
-              *reinterpret_cast<unsigned short*>(act + tile_off(C::ACT_ROW, row0 + r, col)) = q[r];
-            }
-            *reinterpret_cast<u16x4*>(box + box_off(col, row0)) = q;
-          }
+          my_mask[l * C3_CT] = bits;
+          put_act(hq);
         } else {
           // ---- head on the registers of the last hidden layer (model.py:89-94) ----------
-          // (W7 is read from LDS twice rather than held across the loss code: registers)
-          float w7r[3][TN];
-          auto load_w7 = [&]() {
+          // z partials over this lane's features, then over the 4 row groups (a wave's WN
+          // features), then over the waves through LDS
 #pragma unroll
-            for (int o = 0; o < 3; ++o)
+          for (int o = 0; o < 3; ++o) {
+            float z = 0.f;
 #pragma unroll
-              for (int j = 0; j < TN; ++j) w7r[o][j] = w7s[o * H + wc * C::WN + j * 16 + r16];
-          };
-          load_w7();
-          // z partials over this lane's columns, reduced over the 16 lanes of a row group
+            for (int j = 0; j < TN; ++j) {
+              const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int o = 0; o < 3; ++o) {
-              float z = 0.f;
-#pragma unroll
-              for (int j = 0; j < TN; ++j) z = fmaf(hq[j][r], w7r[o][j], z);
-              z = row_sum16(z);
-              if (r16 == 0) zps[(wc * BM + g4 * 4 + r) * 3 + o] = z;
+              for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
             }
+            z = col_sum4(z);
+            if (g4 == 0) zps[(wc * BM + r16) * 3 + o] = z;
+          }
           lbar();  // Bh1: per-wave head partial sums complete
           // sigmoid, loss and dL/dz (model.py:89-94, config.py:113-122, trainer.py:76):
           // every compute wave computes all BM x 3 of them (one lane each) into its own
@@ -384,7 +467,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               const int b = b0 + lane / 3, o = lane % 3;
               float z = w7s[3 * H + o];
 #pragma unroll
-              for (int w = 0; w < 4; ++w) z += zps[w * BM * 3 + lane];
+              for (int w = 0; w < C3_CW; ++w) z += zps[w * BM * 3 + lane];
               const float pv = 1.f / (1.f + expf(-z));
               float dz = 0.f;
               if (b < a.batch) {
@@ -419,85 +502,65 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's dz writes
           }
-          // head backward in registers: dZ_{L-2} = (dz W7) * (h > 0), its column sums, and
-          // the output layer's weight-gradient partials sum_rays dz_o * h
-          load_w7();
-          float dzr[4][3];
+          // head backward in registers: dZ_{L-2} = (dz W7) * (h > 0), its ray sums, and the
+          // output layer's weight-gradient partials sum_rays dz_o * h
+          float dzr[3];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int o = 0; o < 3; ++o) dzr[r][o] = dzs[wc * BM * 3 + (g4 * 4 + r) * 3 + o];
+          for (int o = 0; o < 3; ++o) dzr[o] = dzs[wc * BM * 3 + r16 * 3 + o];
           if (tid < 3) {
             float db = 0.f;
             for (int r = 0; r < BM; ++r) db += dzs[r * 3 + tid];
             hbs[tid] = db;
           }
+          float gv[TN][4];
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            const int col = wc * C::WN + j * 16 + r16;
-            const int row0 = g4 * 4;
-            float cs = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
-            u16x4 q;
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(w7s + 0 * H + feat(j));
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(w7s + 1 * H + feat(j));
+            const f32x4 w2 = *reinterpret_cast<const f32x4*>(w7s + 2 * H + feat(j));
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float h = hq[j][r];
-              const float d0 = dzr[r][0], d1 = dzr[r][1], d2 = dzr[r][2];
-              float g = fmaf(d2, w7r[2][j], fmaf(d1, w7r[1][j], d0 * w7r[0][j]));
-              g = h > 0.f ? g : 0.f;
-              q[r] = bf_bits3(g);
-              *reinterpret_cast<unsigned short*>(act + tile_off(C::ACT_ROW, row0 + r, col)) = q[r];
-              cs += g;
-              g0 = fmaf(d0, h, g0);
-              g1 = fmaf(d1, h, g1);
-              g2 = fmaf(d2, h, g2);
+              const float g = fmaf(dzr[2], w2[r], fmaf(dzr[1], w1[r], dzr[0] * w0[r]));
+              gv[j][r] = hq[j][r] > 0.f ? g : 0.f;
             }
-            *reinterpret_cast<u16x4*>(box + frag_box_off(col, row0)) = q;
-            cs = col_sum4(cs);
-            g0 = col_sum4(g0);
-            g1 = col_sum4(g1);
-            g2 = col_sum4(g2);
-            if (g4 == 0) {
-              csb[col] = cs;
-              hws[col] = g0;
-              hws[H + col] = g1;
-              hws[2 * H + col] = g2;
-            }
+          }
+          put_act(gv);
+          ray_sums_to(gv, csb);
+#pragma unroll
+          for (int o = 0; o < 3; ++o) {
+            float hv[TN][4];
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) hv[j][r] = dzr[o] * hq[j][r];
+            ray_sums_to(hv, hws + o * H);
           }
         }
       } else {
-        // dX of layer l masked by Y_{l-1} > 0 -> dZ_{l-1} (tile, dZ^T, bias partial)
+        // dX of layer l masked by Y_{l-1} > 0 -> dZ_{l-1} (tile, bias partial)
         const int l = (L - 2) - (p - nfwd);
-        const bool keep_act = l - 1 >= 1;
-        const unsigned bits = my_mask[(l - 1) * 256];
+        const unsigned bits = my_mask[(l - 1) * C3_CT];
+        float v[TN][4];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = wc * C::WN + j * 16 + r16;
-          const int row0 = g4 * 4;
-          float cs = 0.f;
-          u16x4 q;
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const bool on = (bits >> (j * 4 + r)) & 1u;
-            const float v = on ? acc[j][r] : 0.f;
-            cs += v;
-            q[r] = bf_bits3(v);
-            if (keep_act) *reinterpret_cast<unsigned short*>(act + tile_off(C::ACT_ROW, row0 + r, col)) = q[r];
-          }
-          *reinterpret_cast<u16x4*>(box + frag_box_off(col, row0)) = q;
-          cs = col_sum4(cs);
-          if (g4 == 0) csb[col] = cs;
-        }
+          for (int r = 0; r < 4; ++r) v[j][r] = ((bits >> (j * 4 + r)) & 1u) ? acc[j][r] : 0.f;
+        put_act(v);
+        ray_sums_to(v, csb);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       stamp(4 * nphase + 6 + p);
-      lbar();  // B2: tile of the next phase and this phase's box complete
+      lbar();  // B2: tile of the next phase and this phase's partials complete
       stamp(3 + 3 * p);
     }
+#ifdef C3_STREAM_ONLY
+    if (acc[0][0] == 1234.5f) act[lane] = 1;  // keep the MFMAs (and their loads) alive
+#endif
     stamp(2 + 3 * nphase);
-    if (stl != nullptr) {
+    if (stl != nullptr && wave == 0) {
       if (lane == 0) stl[0] = t_entry;
-      for (int i = lane; i < 5 * nphase + 6; i += 64) a.stamps[(blockIdx.x == 0 ? 0 : 5 * nphase + 6) + i] = stl[i];
+      for (int i = lane; i < 7 * nphase + 6; i += 64) a.stamps[(blockIdx.x == 0 ? 0 : 7 * nphase + 6) + i] = stl[i];
     }
   } else {
     // =========================== store wave ===============================================
@@ -537,57 +600,77 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         tt = a.rgb[ray_row(a.ray_idx, a.idx_dtype, offset, bt) * 3 + lane % 3];
       if (lane < BM * 3) tgs[lane] = tt;
     }
-    // X^T for the dW GEMM (layer 0 and Ly): 16-ray blocked tile [k_pad][16], one 8-column
-    // group per lane: 16 row reads, 8 x 32-byte column stores
-    {
-      bf16* xt = a.XT + (int64_t)(b0 / 16) * k_pad * 16;
-#pragma unroll 1
-      for (int cg = lane; cg < (k_pad >> 3); cg += 64) {
-        u16x8 rv[BM];
-#pragma unroll
-        for (int r = 0; r < BM; ++r) rv[r] = *reinterpret_cast<const u16x8*>(xs + r * xrow + ((cg ^ (r & 15)) << 4));
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          u16x8 lo, hi;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            lo[r] = rv[r][e];
-            hi[r] = rv[8 + r][e];
-          }
-          u16x8* dst = reinterpret_cast<u16x8*>(xt + (int64_t)(cg * 8 + e) * 16);
-          dst[0] = lo;
-          dst[1] = hi;
-        }
+    // ---- fragment images for the dW GEMM (lgemm.hpp: rows = features, k = rays) ----------
+    // The workgroup's 16 rays are half (b0 / 16) % 2 of k block b0 / 32: per 16-feature
+    // tile t one 512-byte piece, lane slot i + 16 rh = feature 16 t + i, rays 8 rh .. 8 rh + 7.
+    // One store instruction writes the pieces of tiles 2 s and 2 s + 1 (2 x 512 contiguous
+    // bytes, whole lines); the feature-major transpose comes from ds_read_b64_tr_b16: a
+    // 16-lane group reads 4 rays x 16 features, lane 4 q + p giving ray q's features
+    // 4 p .. 4 p + 3, and lane i receives feature i of the 4 rays.
+    const int tg = lane >> 4;                 // 16-lane group: (tile 2 s + tg / 2, rays 8 (tg % 2) ..)
+    const int ti = lane & 15;                 // slot in the piece = feature within the tile
+    const int tq = ti >> 2, tp = ti & 3;      // this lane's address: ray row tq, feature quad tp
+    const int trh = tg & 1;
+    const int64_t half_off = ((b0 >> 4) & 1) * 512 + (int64_t)(ti + 16 * trh) * 16;
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    auto tr_read = [&](const char* p8) -> s16x4 {
+      return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p8));
+    };
+    // tiles: R / 16 of an image with R rows; addr(t, ray, quad) -> the 8-byte LDS address of
+    // features 16 t + 4 quad .. + 3 of `ray`
+    auto copy_image = [&](auto addr, int R, bf16* img, int s_begin, int s_end) {
+      char* d = reinterpret_cast<char*>(img) + (int64_t)(b0 >> 5) * (R / 16) * 1024 + half_off;
+#pragma unroll 4
+      for (int s2 = s_begin; s2 < s_end; ++s2) {
+        const int t = 2 * s2 + (tg >> 1);
+        const s16x4 lo = tr_read(addr(t, 8 * trh + tq, tp));
+        const s16x4 hi = tr_read(addr(t, 8 * trh + 4 + tq, tp));
+        const s16x4x8 o = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<s16x4x8*>(d + (int64_t)t * 1024) = o;
       }
-    }
-    const int64_t tile_elems = (int64_t)(b0 / 16) * H * 16;
+    };
+    auto x_addr = [&](int t, int r, int q) -> const char* {
+      return xs + r * xrow + (((2 * t + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
+    };
+    auto act_addr = [&](int t, int r, int q) -> const char* { return act + act_off(t >> 1, r, q) + 8 * (t & 1); };
+    // X^T for the dW GEMMs of layer 0 and Ly: spread over the first forward phases (the
+    // feature tile stays in LDS), a slice after each of them
+    const int xs_total = k_pad / 32;
+    const int x_phases = nfwd - 1 < 4 ? nfwd - 1 : 4;
+    auto copy_x_slice = [&](int p) {
+      if (p < x_phases)
+        copy_image(x_addr, k_pad, a.XT, xs_total * p / x_phases, xs_total * (p + 1) / x_phases);
+    };
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
       for (int c = lane * 16; c < bytes; c += 64 * 16)
         *reinterpret_cast<u16x8*>(d + c) = *reinterpret_cast<const u16x8*>(src + c);
     };
-    // dZ^T box -> fragment image: piece t (512 B) to k-block b0 / 32, tile t, half
-    // (b0 / 16) % 2 of its 1 KiB
-    const int64_t frag_base = (int64_t)(b0 >> 5) * (H / 16) * 1024 + ((b0 >> 4) & 1) * 512;
-    auto copy_frag = [&](const char* src, bf16* dst) {
-      char* d = reinterpret_cast<char*>(dst) + frag_base;
-      for (int c = lane; c < C::TILE_BYTES / 16; c += 64)
-        *reinterpret_cast<u16x8*>(d + (c >> 5) * 1024 + (c & 31) * 16) = *reinterpret_cast<const u16x8*>(src + c * 16);
-    };
+#ifdef C3_STREAM_ONLY
+#ifdef C3_STREAM_BARRIERS
+    for (int p = 0; p < nphase; ++p) {
+      lbar();
+      lbar();
+    }
+#endif
+    return;
+#endif
 #pragma unroll 1
     for (int p = 0; p < nphase; ++p) {
+      stamp(5 * nphase + 6 + p);
       lbar();  // B1
       const bool head_phase = p == nfwd - 1;
       if (head_phase) lbar();  // Bh1
       lbar();  // B2
-      const char* box = smem + C::OFF_BOX + (p & 1) * C::BOX_BYTES;
-      const char* csb = box + C::TILE_BYTES;
+      const char* cs = reinterpret_cast<const char*>(csb);
       if (p < nfwd) {
         const int l = p;
-        if (!head_phase) copy_out(box, a.YT[l] + tile_elems, C::TILE_BYTES);
+        if (!head_phase) copy_image(act_addr, H, a.YT[l], 0, H / 32);
+        copy_x_slice(p);
         if (head_phase) {
-          copy_frag(box, a.dZT[L - 2]);
-          copy_out(csb, a.colsum[L - 2] + (int64_t)blockIdx.x * H, H * 4);
+          copy_image(act_addr, H, a.dZT[L - 2], 0, H / 32);
+          copy_out(cs, a.colsum[L - 2] + (int64_t)blockIdx.x * H, H * 4);
           copy_out(reinterpret_cast<const char*>(hws), a.hw_part + (int64_t)blockIdx.x * 3 * H, 3 * H * 4);
           if (lane < 3) a.hb_part[(int64_t)blockIdx.x * 3 + lane] = hbs[lane];
           if (lane < 2 && a.loss_part != nullptr) a.loss_part[2 * (int64_t)blockIdx.x + lane] = lss[lane];
@@ -597,8 +680,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       } else {
         const int l = (L - 2) - (p - nfwd);
-        copy_frag(box, a.dZT[l - 1]);
-        copy_out(csb, a.colsum[l - 1] + (int64_t)blockIdx.x * H, H * 4);
+        copy_image(act_addr, H, a.dZT[l - 1], 0, H / 32);
+        copy_out(cs, a.colsum[l - 1] + (int64_t)blockIdx.x * H, H * 4);
       }
     }
   }
@@ -621,7 +704,7 @@ int launch3_loss(const Chain3Args& a, hipStream_t stream) {
 }
 
 // the loss is a template parameter: one branch-free head per loss type keeps the compute
-// waves under the 256 VGPRs of a 5-wave workgroup (a spill would drain the weight queue)
+// waves inside their VGPR budget (a spill would drain the weight queue)
 template <int H>
 int launch3_typed(const Chain3Args& a, hipStream_t stream) {
   if (a.loss == INF_LOSS_L2) return launch3_loss<H, INF_LOSS_L2>(a, stream);

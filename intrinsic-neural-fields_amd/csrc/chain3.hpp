@@ -46,10 +46,10 @@ struct Chain3Args {
   const float* W7;                       // [3][H] fp32 output layer
   const float* b7;
   // outputs for the weight-gradient GEMM (lgemm.hip) and the update launch
-  bf16* XT;                        // 16-ray blocked X^T: (c, ray b) at (b/16) k_pad 16 + c 16 + b%16
-  bf16* YT[CHAIN_MAX_HIDDEN];      // 16-ray blocked Y_l^T, l = 0..L-3
-  bf16* dZT[CHAIN_MAX_HIDDEN];     // dZ_l^T fragment images (H/16 tiles x rows/32 k-blocks,
-                                   // lgemm.hpp operand B), l = 0..L-2
+  // fragment images (lgemm.hpp: rows = features, k = rays; 1 KiB per 16 features x 32 rays)
+  bf16* XT;                        // X^T, k_pad rows
+  bf16* YT[CHAIN_MAX_HIDDEN];      // Y_l^T, H rows, l = 0..L-3 (lgemm operand A)
+  bf16* dZT[CHAIN_MAX_HIDDEN];     // dZ_l^T, H rows, l = 0..L-2 (lgemm operand B)
   float* colsum[CHAIN_MAX_HIDDEN]; // [rows/16][H] bias-gradient partials
   float* hw_part;                  // [rows/16][3][H]
   float* hb_part;                  // [rows/16][3]

@@ -4,7 +4,10 @@
 // Block = BM rows x 128 columns, 4 waves; wave w owns columns [32 w, 32 w + 32) (two
 // 16-column MFMA tiles) for all BM rows.  Per 32-deep k block ("unit") a wave needs
 // one A fragment per 16-row tile (shared by the 4 waves: LDS) and two B fragments (its
-// own: two coalesced 1 KiB loads of the fragment image, no LDS).
+// own: two coalesced 1 KiB loads of the fragment image, no LDS).  Both operands are
+// fragment images, so the A tiles of a unit are BM/16 contiguous KiB: staged into LDS
+// in that order by 16-byte chunks and read back one lane-contiguous ds_read_b128 per
+// fragment (conflict-free, no swizzle).
 //
 // Why.  The LDS-DMA GEMM (gemm.hip) stages both operands through LDS: at 64x64 / 128x128
 // tiles every k-step costs each wave 4-8 direct-to-LDS issues (~100+ cycles each) for
@@ -44,10 +47,6 @@ struct LG {
   static_assert(ACH >= 1 && BM * 8 % 256 == 0, "A stage must split over 256 threads");
 };
 
-// 16-byte chunk c of 128-byte LDS row `row` (the gemm.hip swizzle: a ds_read_b128 lane
-// group of 16 rows at one chunk is conflict-free)
-__device__ __forceinline__ int lswz(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
-
 __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int BM>
@@ -82,18 +81,19 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   const int nst = kper / 64;        // A stages, multiple of 4
   const int nun = kper / 32;        // units
 
-  // ---- A: buffer descriptor at this split's first k; per-thread chunk offsets ---------
-  const bool akb = P.a_kblk != 0;
-  const char* a_base = reinterpret_cast<const char*>(P.A) + (akb ? (int64_t)(k_begin >> 4) * P.lda : k_begin) * 2;
+  // ---- A: buffer descriptor at this split's first k block; per-thread chunk offsets:
+  // chunk q of a 64-deep stage = k block q / (TM 64), byte (q % (TM 64)) 16 of its TM tiles
+  const int a_kstride = P.a_tiles * 1024;  // bytes per k block of the image
+  const char* a_base = reinterpret_cast<const char*>(P.Af) + (int64_t)(k_begin >> 5) * a_kstride;
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a_base), (short)0, 0x7FFFFFFF, 0x00020000);
-  const int a_step = akb ? (int)(4 * P.lda * 2) : 128;  // bytes per 64-deep stage
+  const int a_step = 2 * a_kstride;  // bytes per 64-deep stage
+  const int a_tile0 = (P.a_row0 + m0) >> 4;
   unsigned aoff[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
-    const int q = tid + 256 * i, row = q >> 3, c = q & 7;
-    aoff[i] = (unsigned)((akb ? (int64_t)(c >> 1) * P.lda + (int64_t)(m0 + row) * 16 + 8 * (c & 1)
-                              : (int64_t)(m0 + row) * P.lda + 8 * c) * 2);
+    const int q = tid + 256 * i, kl = q / (TM * 64), c = q % (TM * 64);
+    aoff[i] = (unsigned)(kl * a_kstride + a_tile0 * 1024 + c * 16);
   }
   // ---- B: fragment image; this wave's two 16-row tiles ---------------------------------
   const __amdgpu_buffer_rsrc_t rb =
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int q = tid + 256 * i;
-      *reinterpret_cast<u32x4*>(smem + buf * C::A_STAGE + lswz(q >> 3, q & 7)) = src[i];
+      *reinterpret_cast<u32x4*>(smem + buf * C::A_STAGE + q * 16) = src[i];
     }
   };
   auto loadB = [&](int u, bf16x8 (&dst)[TN]) {
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
         const int slot = (2 * ss + kk) % D;
         bf16x8 av[TM];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(As + lswz(i * 16 + r16, kk * 4 + g4));
+        for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(As + (kk * TM + i) * 1024 + lane * 16);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -250,10 +250,11 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   for (int i = 0; i < b.nprob; ++i) {
     LgemmProblem& p = b.p[i];
     if (p.splits < 1) p.splits = 1;
-    INF_CHECK_ARG(p.A != nullptr && p.Bf != nullptr, "lgemm: null operand");
+    INF_CHECK_ARG(p.Af != nullptr && p.Bf != nullptr, "lgemm: null operand");
     INF_CHECK_ARG(p.M > 0 && p.M % bm == 0 && p.N > 0 && p.N % LG_BN == 0, "lgemm: M/N not tile multiples");
     INF_CHECK_ARG(p.K > 0 && p.K % (256 * p.splits) == 0, "lgemm: K per split must be a multiple of 256");
-    INF_CHECK_ARG(p.lda % 8 == 0 && p.b_row0 % 16 == 0 && p.b_row0 + p.N <= 16 * p.b_tiles, "lgemm: operand layout");
+    INF_CHECK_ARG(p.a_row0 % 16 == 0 && p.a_row0 + p.M <= 16 * p.a_tiles && p.b_row0 % 16 == 0 &&
+                      p.b_row0 + p.N <= 16 * p.b_tiles, "lgemm: operand layout");
     INF_CHECK_ARG(p.splits == 1 || p.slab != nullptr, "lgemm: split-K needs a slab");
     INF_CHECK_ARG(p.slab != nullptr || p.C != nullptr, "lgemm: no output");
     p.tiles_m = p.M / bm;

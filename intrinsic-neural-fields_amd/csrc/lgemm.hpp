@@ -3,9 +3,12 @@
 //
 //   C[m][n] = epilogue( sum_k A[m][k] * B[n][k] )
 //
-//   input GEMM   A = X [rays][k_pad]          B = W_0 / W_y fragment images (adam.hip WF)
-//   dW GEMM      A = In^T [n_in][rays]        B = dZ_l^T fragment image (chain3.hip),
+//   dW GEMM      A = In^T [n_in][rays]        (X^T / Y_l^T fragment images, chain3.hip)
+//                B = dZ_l^T [n_out][rays]     (fragment image, chain3.hip)
 //                C = dW^T, stored transposed into the split-K slab [n_out][n_in]
+//
+// Fragment image of an R x K matrix: 1 KiB per (32-deep k block kb, 16-row tile t) at
+// (kb * R/16 + t) KiB, lane l's 16 bytes at 16 l = row 16 t + l % 16, k = 32 kb + 8 (l / 16) + e.
 #pragma once
 
 #include "common.hpp"
@@ -16,14 +19,11 @@ constexpr int LGEMM_MAX_PROBLEMS = 12;
 constexpr int LG_BN = 128;  // columns per block: 4 waves x 32
 
 struct LgemmProblem {
-  // A: M rows, K-contiguous: row-major (element (r, k) at r * lda + k) or 16-blocked
-  // (at (k / 16) * lda + r * 16 + k % 16, gemm.hpp a_kblk)
-  const bf16* A;
-  int64_t lda;
-  int32_t a_kblk;
-  // B: fragment image of an R x K matrix: 1 KiB per (32-deep k block kb, 16-row tile t)
-  // at (kb * b_tiles + t) KiB, lane l's 16 bytes at 16 l (row 16 t + l % 16, k = 32 kb +
-  // 8 (l / 16) + e); rows [b_row0, b_row0 + N) of the image are this problem's columns
+  // A: fragment image with a_tiles row tiles; rows [a_row0, a_row0 + M) are this problem's rows
+  const bf16* Af;
+  int32_t a_tiles;
+  int32_t a_row0;
+  // B: fragment image with b_tiles row tiles; rows [b_row0, b_row0 + N) are its columns
   const bf16* Bf;
   int32_t b_tiles;  // R / 16
   int32_t b_row0;

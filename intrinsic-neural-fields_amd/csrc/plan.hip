@@ -377,9 +377,8 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
   const int H = p->H, s = p->s;
   if (chain == 3) {
-    // register-streamed chain: dZ_l^T is a fragment image (chain3.hip); one lgemm launch
-    // computes every dW^T tile with the layer input (X^T, Y_0^T plain, Y_l^T 16-ray
-    // blocked) through LDS, into the split-K slabs the update launch reduces
+    // register-streamed chain: X^T, Y_l^T and dZ_l^T are fragment images (chain3.hip); one
+    // lgemm launch computes every dW^T tile into the split-K slabs the update launch reduces
     LgemmBatch lb;
     std::memset(&lb, 0, sizeof(lb));
     for (size_t i = 0; i < p->segs.size(); ++i) {
@@ -389,10 +388,10 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
       LgemmProblem& q = lb.p[lb.nprob++];
       const int l = g.layer;
       const bool from_input = (l == 0) || (l == s && g.sub == 1);
-      // layer inputs as the chain wrote them: 16-ray blocked X^T / Y_{l-1}^T
-      q.A = from_input ? p->W<bf16>(p->o_x0t) : p->W<bf16>(p->o_yt[l - 1]);
-      q.lda = (int64_t)(from_input ? p->k_pad : H) * 16;
-      q.a_kblk = 1;
+      // layer inputs as the chain wrote them: X^T / Y_{l-1}^T fragment images
+      q.Af = from_input ? p->W<bf16>(p->o_x0t) : p->W<bf16>(p->o_yt[l - 1]);
+      q.a_tiles = (from_input ? p->k_pad : H) / 16;
+      q.a_row0 = 0;
       q.Bf = p->W<bf16>(p->o_dZT[l]);
       q.b_tiles = H / 16;
       q.M = g.c_pad;
@@ -864,6 +863,7 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
       a.ldwt = g.R;
       a.WF = g.f_off >= 0 ? p->shadow + g.f_off : nullptr;
       a.WTF = g.ft_off >= 0 ? p->shadow + g.ft_off : nullptr;
+      a.wf_acc_order = g.ft_off >= 0 ? 1 : 0;  // hidden layers: fed by the activation tile
       const int flags = (g.C % 4 == 0 && g.off % 4 == 0) ? ITEM_VEC4 : 0;
       for (int r = 0; r < g.R; r += ADAM_TILE_R)
         for (int c = 0; c < g.C; c += ADAM_TILE_C) p->adam_items.push_back(AdamItem{(int32_t)i, r, c, flags});

@@ -42,7 +42,7 @@ ev1.record()
 torch.cuda.synchronize()
 print(f"chain3 stage: {ev0.elapsed_time(ev1) / 50 * 1e3:.1f} us  (B={B}, {nphase} phases)")
 
-n1 = 5 * nphase + 6
+n1 = 7 * nphase + 6
 stamps = torch.zeros(2 * n1, dtype=torch.int64, device="cuda")
 lib.inf_debug_timing(plan.handle, ctypes.c_void_p(stamps.data_ptr()), nphase)
 for _ in range(5):
@@ -63,6 +63,9 @@ for w, name in enumerate(("first", "last")):
         b1 = t[3 * nphase + 6 + p] - t[2 + 3 * p]
         body = t[4 * nphase + 6 + p] - t[3 * nphase + 6 + p]
         b2 = t[3 + 3 * p] - t[4 * nphase + 6 + p]
-        rows.append(f"{names[p]}: mfma {mm:.2f} epi {ep:.2f} (B1 wait {b1:.2f}, body {body:.2f}, B2 wait {b2:.2f})")
+        sw = t[5 * nphase + 6 + p] - t[2 + 3 * p]
+        lw = t[6 * nphase + 6 + p] - t[2 + 3 * p]
+        rows.append(f"{names[p]}: mfma {mm:.2f} epi {ep:.2f} (B1 wait {b1:.2f}, body {body:.2f}, B2 wait {b2:.2f}; "
+                    f"store wave at B1 {sw:+.2f}, last wave {lw:+.2f})")
     print("   " + "\n   ".join(rows))
 print("entry skew last-first:", (st[1][0] - st[0][0]), "us")

@@ -14,7 +14,7 @@ from collections import defaultdict
 
 
 def short(name):
-    for key in ("chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
+    for key in ("chain3_kernel", "lgemm_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
                 "head_bwd_kernel", "pack_kernel", "ctrl_advance_kernel"):
         if key in name:
             tail = ""
@@ -59,7 +59,11 @@ def counters(d, counter):
     return {k: sum(v) / len(v) * 1024.0 for k, v in acc.items()}  # KiB -> bytes per dispatch
 
 
-def main(root):
+# bench.py stage -> kernel, for the per-launch traffic table bench.py reads
+STAGE_KERNEL = {"chain3": "chain3_kernel", "dw_gemm": "lgemm_kernel", "update": "update_kernel"}
+
+
+def main(root, tag=None):
     tdir = os.path.join(root, "trace")
     res = {"kernels": stats(tdir if os.path.isdir(tdir) else root)}
     fetch = counters(os.path.join(root, "fetch"), "FETCH_SIZE")
@@ -72,8 +76,12 @@ def main(root):
             e["write_size_bytes"] = write[k]
         if k in fetch and k in write:
             e["traffic_bytes"] = 2.0 * fetch[k] + write[k]
+    if tag:  # e.g. bf16_B4096: {"chain3_bf16_B4096": bytes per launch, ...}
+        res["bench_traffic"] = {f"{st}_{tag}": res["kernels"][k]["traffic_bytes"]
+                                for st, k in STAGE_KERNEL.items()
+                                if "traffic_bytes" in res["kernels"].get(k, {})}
     print(json.dumps(res, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
