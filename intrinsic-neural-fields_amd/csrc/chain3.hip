@@ -55,9 +55,12 @@ constexpr int C3_CT = C3_CW * 64;             // compute threads
 constexpr int C3_THREADS = C3_CT + 64;        // + the store wave
 constexpr int C3_LDS_CAP = 160 * 1024;
 #ifndef C3_DEPTH
-#define C3_DEPTH 4
+#define C3_DEPTH 8
 #endif
 constexpr int C3BM = 16;  // rays per workgroup
+#ifndef C3_GATHER_CPOL
+#define C3_GATHER_CPOL 2  // table rows are read once per step: non-temporal, spare the weights' L2 lines
+#endif
 
 template <int H>
 struct L3 {
@@ -67,9 +70,11 @@ struct L3 {
   static constexpr int UPL = H / 32;            // 32-deep k blocks per hidden layer (= per stream block)
   static constexpr int NT = H / 16;             // 16-row tiles per k block of a weight image
   static constexpr int ACT_BYTES = BM * H * 2;
-  static constexpr int OFF_ACT = 0;                       // activation / dZ tile (act_off layout)
-  static constexpr int OFF_CS = OFF_ACT + ACT_BYTES;      // [H] bias-gradient partial of a phase
-  static constexpr int OFF_HW = OFF_CS + H * 4;           // [3][H] output-layer weight grad
+  // activation / dZ tiles (act_off layout), double-buffered: epilogue p writes tile
+  // (p + 1) & 1, phase p reads tile p & 1, so one barrier per phase suffices
+  static constexpr int OFF_ACT = 0;
+  static constexpr int OFF_CS = OFF_ACT + 2 * ACT_BYTES;  // [2][H] bias-gradient partials (epilogue p: p & 1)
+  static constexpr int OFF_HW = OFF_CS + 2 * H * 4;       // [3][H] output-layer weight grad
   static constexpr int OFF_HB = OFF_HW + 3 * H * 4;       // [4]
   static constexpr int OFF_LS = OFF_HB + 16;              // [2] f64 loss / SSE
   static constexpr int OFF_PRED = OFF_LS + 16;            // [BM][3]
@@ -80,14 +85,10 @@ struct L3 {
   static constexpr int OFF_RBARY = OFF_RAY + BM * 16 + BM * 12 + 16;  // [BM][3] barycentrics
   static constexpr int OFF_W7 = OFF_RBARY + BM * 12 + 16;  // [3][H] then b7[3]
   static constexpr int OFF_VEC = OFF_W7 + 3 * H * 4 + 16;  // biases [L-1][H], then Ly.bias [H]
-  // ReLU bits: per layer one 32-bit word per compute lane, bit j*4 + r for accumulator
-  // element (j, r) of that lane
-  static constexpr int MASK_BYTES = C3_CT * 4;
-  __host__ __device__ static int off_mask(int L) { return OFF_VEC + L * H * 4; }
-  __host__ __device__ static int off_x(int L) { return off_mask(L) + (L - 2) * MASK_BYTES; }
+  __host__ __device__ static int off_x(int L) { return OFF_VEC + L * H * 4; }
   __host__ __device__ static int off_stamp(int L, int k_pad) { return off_x(L) + BM * k_pad * 2; }
   static int lds_bytes(int L, int k_pad) { return off_stamp(L, k_pad) + (7 * C3_MAX_PHASES + 8) * 8; }
-  static_assert(TN >= 1 && TN * 4 <= 32, "ReLU bits of a lane must fit one word");
+  static_assert(TN >= 1 && TN * 4 <= 8, "ReLU bits of a lane: at most 8 per layer");
   static_assert(OFF_LS % 8 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
 
@@ -198,7 +199,6 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   float* rbary = reinterpret_cast<float*>(smem + C::OFF_RBARY);  // [BM][3]
   float* w7s = reinterpret_cast<float*>(smem + C::OFF_W7);
   float* vecs = reinterpret_cast<float*>(smem + C::OFF_VEC);
-  unsigned* maskw = reinterpret_cast<unsigned*>(smem + C::off_mask(L));
   char* xs = smem + C::off_x(L);  // gathered features [BM][k_pad] bf16 (tile_off layout)
   const int xrow = k_pad * 2;
 
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           for (int i = 0; i < 3; ++i) {
             wv[g][i] = rbary[r * 3 + i];
             const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + ch * 8) * 2u;
-            ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rt, off, 0, 0));
+            ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rt, off, 0, C3_GATHER_CPOL));
           }
         }
 #pragma unroll
@@ -324,7 +324,11 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     lbar();  // barrier 0: feature tile in LDS
     stamp(3 * nphase + 5);
 
-    unsigned* my_mask = maskw + tid;  // + layer * C3_CT
+    // ReLU bits of the lane's NV accumulator elements for layers 0..L-3 (bit j 4 + r), in
+    // registers: 64 / NV layers per word
+    constexpr int MPW = 64 / NV;
+    static_assert(2 * MPW >= CHAIN_MAX_HIDDEN - 1, "ReLU bit words");
+    unsigned long long mbits[2] = {0ull, 0ull};
     // B-operand slot offsets of this lane inside a k block of the activation tile (the
     // swizzle repeats every 4 k blocks)
     int aoffs[4];
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
     // activations / dZ -> the LDS tile: one 16-byte write per k block (tile pair), 8 bytes
     // for a lone tile (H = 128: a wave owns half a k block)
-    auto put_act = [&](const float (&v)[TN][4]) {
+    auto put_act = [&](const float (&v)[TN][4], char* act) {
       if constexpr (TN % 2 == 0) {
 #pragma unroll
         for (int j = 0; j < TN; j += 2) {
@@ -385,11 +389,12 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const __amdgpu_buffer_rsrc_t crs = rsrc_of(B.img);
       const __amdgpu_buffer_rsrc_t nrs = rsrc_of(Bn.img);
       const bool from_x = B.a_x != 0;
+      const char* act_in = act + (B.phase & 1) * C::ACT_BYTES;
       const int ak0 = B.ak0, ckb = B.kb0, nkb = Bn.kb0;
 #pragma unroll
       for (int kb = 0; kb < UPL; ++kb) {
         // B operand: the feature tile (natural k order) or the activation tile
-        const char* bp = from_x ? xlane + ((((ak0 + kb) * 4 + g4) ^ r16) << 4) : act + kb * 1024 + aoffs[kb & 3];
+        const char* bp = from_x ? xlane + ((((ak0 + kb) * 4 + g4) ^ r16) << 4) : act_in + kb * 1024 + aoffs[kb & 3];
         const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bp);
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[j], 0, 0, 0);
@@ -413,9 +418,11 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 
       // ---- epilogue of phase p ---------------------------------------------------------
       const int p = B.phase;
-      stamp(wave == 0 ? 2 + 3 * p : 6 * nphase + 6 + p);
-      lbar();  // B1: every wave is done reading the activation tile; the store wave has copied it
-      stamp(3 * nphase + 6 + p);
+      stamp(2 + 3 * p);
+      // no barrier before the writes: this epilogue's tiles (act (p + 1) & 1, colsum p & 1)
+      // were last read in phase p - 1 / copied by the store wave before B2(p - 1)
+      char* act_out = act + ((p + 1) & 1) * C::ACT_BYTES;
+      float* cs_out = csb + (p & 1) * H;
       if (p < nfwd) {
         // forward of layer l: bias (+ Ly.bias at the skip layer) + ReLU -> tile, bits
         const int l = p;
@@ -438,8 +445,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           }
         }
         if (!last) {
-          my_mask[l * C3_CT] = bits;
-          put_act(hq);
+          if (l < MPW) mbits[0] |= (unsigned long long)bits << (NV * l);
+          else mbits[1] |= (unsigned long long)bits << (NV * (l - MPW));
+          put_act(hq, act_out);
         } else {
           // ---- head on the registers of the last hidden layer (model.py:89-94) ----------
           // z partials over this lane's features, then over the 4 row groups (a wave's WN
@@ -524,8 +532,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               gv[j][r] = hq[j][r] > 0.f ? g : 0.f;
             }
           }
-          put_act(gv);
-          ray_sums_to(gv, csb);
+          put_act(gv, act_out);
+          ray_sums_to(gv, cs_out);
 #pragma unroll
           for (int o = 0; o < 3; ++o) {
             float hv[TN][4];
@@ -539,18 +547,19 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       } else {
         // dX of layer l masked by Y_{l-1} > 0 -> dZ_{l-1} (tile, bias partial)
         const int l = (L - 2) - (p - nfwd);
-        const unsigned bits = my_mask[(l - 1) * C3_CT];
+        const unsigned bits = (unsigned)((l - 1 < MPW ? mbits[0] >> (NV * (l - 1)) : mbits[1] >> (NV * (l - 1 - MPW))) &
+                                         ((1u << NV) - 1));
         float v[TN][4];
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[j][r] = ((bits >> (j * 4 + r)) & 1u) ? acc[j][r] : 0.f;
-        put_act(v);
-        ray_sums_to(v, csb);
+        put_act(v, act_out);
+        ray_sums_to(v, cs_out);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      stamp(4 * nphase + 6 + p);
+      stamp(wave == 0 ? 4 * nphase + 6 + p : 6 * nphase + 6 + p);
       lbar();  // B2: tile of the next phase and this phase's partials complete
       stamp(3 + 3 * p);
     }
@@ -564,6 +573,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     }
   } else {
     // =========================== store wave ===============================================
+#ifdef C3_STORE_PRIO
+    __builtin_amdgcn_s_setprio(C3_STORE_PRIO);
+#endif
     // per-launch vectors (biases, Ly.bias, W7, b7), loaded while the compute waves gather;
     // written into LDS between barriers R and 0 (the first reader is phase 0's epilogue)
     constexpr int CPL = H / 64;  // one 16-byte (H = 256) / 8-byte (H = 128) load per lane per row
@@ -621,27 +633,36 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // features 16 t + 4 quad .. + 3 of `ray`
     auto copy_image = [&](auto addr, int R, bf16* img, int s_begin, int s_end) {
       char* d = reinterpret_cast<char*>(img) + (int64_t)(b0 >> 5) * (R / 16) * 1024 + half_off;
-#pragma unroll 4
-      for (int s2 = s_begin; s2 < s_end; ++s2) {
-        const int t = 2 * s2 + (tg >> 1);
-        const s16x4 lo = tr_read(addr(t, 8 * trh + tq, tp));
-        const s16x4 hi = tr_read(addr(t, 8 * trh + 4 + tq, tp));
-        const s16x4x8 o = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        *reinterpret_cast<s16x4x8*>(d + (int64_t)t * 1024) = o;
+      // batches of 4 instructions: all 8 transposing reads issued before the first store
+      // waits on them (counted lgkmcnt), so LDS latency is paid once per batch
+      constexpr int NB = 4;
+#pragma unroll 1
+      for (int s0 = s_begin; s0 < s_end; s0 += NB) {
+        s16x4 lo[NB], hi[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int t = 2 * min(s0 + u, s_end - 1) + (tg >> 1);
+          lo[u] = tr_read(addr(t, 8 * trh + tq, tp));
+          hi[u] = tr_read(addr(t, 8 * trh + 4 + tq, tp));
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          if (s0 + u < s_end) {
+            const int t = 2 * (s0 + u) + (tg >> 1);
+            const s16x4x8 o = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
+            *reinterpret_cast<s16x4x8*>(d + (int64_t)t * 1024) = o;
+          }
+        }
       }
     };
     auto x_addr = [&](int t, int r, int q) -> const char* {
       return xs + r * xrow + (((2 * t + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
     };
-    auto act_addr = [&](int t, int r, int q) -> const char* { return act + act_off(t >> 1, r, q) + 8 * (t & 1); };
-    // X^T for the dW GEMMs of layer 0 and Ly: spread over the first forward phases (the
-    // feature tile stays in LDS), a slice after each of them
+    // X^T for the dW GEMMs of layer 0 and Ly, copied while the compute waves stream the
+    // long input-layer phases (W_0: phase 0, W_y: the skip phase s), half in each
     const int xs_total = k_pad / 32;
-    const int x_phases = nfwd - 1 < 4 ? nfwd - 1 : 4;
-    auto copy_x_slice = [&](int p) {
-      if (p < x_phases)
-        copy_image(x_addr, k_pad, a.XT, xs_total * p / x_phases, xs_total * (p + 1) / x_phases);
-    };
+    const int xs_mid = a.s >= 1 ? xs_total / 2 : xs_total;
+    copy_image(x_addr, k_pad, a.XT, 0, xs_mid);
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
       for (int c = lane * 16; c < bytes; c += 64 * 16)
@@ -659,15 +680,17 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 #pragma unroll 1
     for (int p = 0; p < nphase; ++p) {
       stamp(5 * nphase + 6 + p);
-      lbar();  // B1
       const bool head_phase = p == nfwd - 1;
       if (head_phase) lbar();  // Bh1
       lbar();  // B2
-      const char* cs = reinterpret_cast<const char*>(csb);
+      // phase p's outputs: act tile (p + 1) & 1, colsum p & 1 -- to be copied before B2(p + 1)
+      const char* act_p = act + ((p + 1) & 1) * C::ACT_BYTES;
+      auto act_addr = [&](int t, int r, int q) -> const char* { return act_p + act_off(t >> 1, r, q) + 8 * (t & 1); };
+      const char* cs = reinterpret_cast<const char*>(csb + (p & 1) * H);
       if (p < nfwd) {
         const int l = p;
         if (!head_phase) copy_image(act_addr, H, a.YT[l], 0, H / 32);
-        copy_x_slice(p);
+        if (p == a.s - 1) copy_image(x_addr, k_pad, a.XT, xs_mid, xs_total);
         if (head_phase) {
           copy_image(act_addr, H, a.dZT[L - 2], 0, H / 32);
           copy_out(cs, a.colsum[L - 2] + (int64_t)blockIdx.x * H, H * 4);

@@ -60,12 +60,11 @@ for w, name in enumerate(("first", "last")):
     for p in range(nphase):
         mm = t[2 + 3 * p] - t[1 + 3 * p]
         ep = t[3 + 3 * p] - t[2 + 3 * p]
-        b1 = t[3 * nphase + 6 + p] - t[2 + 3 * p]
-        body = t[4 * nphase + 6 + p] - t[3 * nphase + 6 + p]
+        body = t[4 * nphase + 6 + p] - t[2 + 3 * p]
         b2 = t[3 + 3 * p] - t[4 * nphase + 6 + p]
-        sw = t[5 * nphase + 6 + p] - t[2 + 3 * p]
-        lw = t[6 * nphase + 6 + p] - t[2 + 3 * p]
-        rows.append(f"{names[p]}: mfma {mm:.2f} epi {ep:.2f} (B1 wait {b1:.2f}, body {body:.2f}, B2 wait {b2:.2f}; "
-                    f"store wave at B1 {sw:+.2f}, last wave {lw:+.2f})")
+        sw = t[5 * nphase + 6 + p] - t[4 * nphase + 6 + p]
+        lw = t[6 * nphase + 6 + p] - t[4 * nphase + 6 + p]
+        rows.append(f"{names[p]}: mfma {mm:.2f} epi {ep:.2f} (body {body:.2f}, B2 wait {b2:.2f}; "
+                    f"at B2 vs wave 0: store wave {sw:+.2f}, last wave {lw:+.2f})")
     print("   " + "\n   ".join(rows))
 print("entry skew last-first:", (st[1][0] - st[0][0]), "us")
