@@ -304,7 +304,7 @@ def main():
     # per-kernel times (HIP events around repeated launches of one stage on its saved inputs)
     stages = {}
     stages["dw_gemm"] = time_stage(tr.plan, STAGE_DW_GEMM)
-    stages["update"] = time_stage(tr.plan, STAGE_UPDATE)
+    stages["update"] = time_stage(tr.plan, STAGE_UPDATE, layer=1)  # Adam + weight images, as in the step
     chain3 = (args.mode == "bf16" and args.batch <= 8192 and args.hidden in (128, 256)
               and not os.environ.get("INF_NO_CHAIN") and not os.environ.get("INF_NO_CHAIN3"))
     if chain3:

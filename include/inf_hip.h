@@ -178,8 +178,9 @@ int inf_render(inf_plan* plan, const inf_batch* batch, const int64_t* hit, const
  *   INF_STAGE_GATHER   - the gather kernel (X, X^T)
  *   INF_STAGE_FWD_GEMM - the forward GEMM of hidden layer `layer` (1..L-2)
  *   INF_STAGE_DW_GEMM  - the grouped split-K weight-gradient GEMM
- *   INF_STAGE_UPDATE   - the slab-reduction/Adam/packed-weight launch (reduce only:
- *                        parameters are not modified)
+ *   INF_STAGE_UPDATE   - the slab-reduction/Adam/packed-weight launch: layer 0 reduces
+ *                        only (parameters are not modified), layer 1 runs it as the
+ *                        training step does (Adam + weight images; parameters change)
  *   INF_STAGE_CHAIN    - the fused forward + loss + dX-chain kernel (bf16 mode; at
  *                        <= 8192 rays with the gather fused in)
  * *flops / *bytes receive the stage's algorithmic work per launch (unpadded). */
@@ -198,6 +199,12 @@ int inf_debug_ranges(inf_plan* plan, const uint64_t* ranges_dev, int n, unsigned
  * landed: stamps_dev[w * (max_steps + 1) + s], w = 0 (first) / 1 (last), entry max_steps
  * = the kernel's end.  Pass null to turn it off. */
 int inf_debug_timing(inf_plan* plan, unsigned long long* stamps_dev, int max_steps);
+
+/* Diagnostics: when `stamps_dev` is non-null, every workgroup of the weight-gradient GEMM
+ * (lgemm, register-streamed chain path) records the 100 MHz wall clock at entry, after its
+ * operand prologue, after its main loop and at exit: stamps_dev[block * 4 + i], block in
+ * launch order (before the XCD remap).  Pass null to turn it off. */
+int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

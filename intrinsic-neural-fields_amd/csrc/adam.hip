@@ -7,283 +7,24 @@
 //       slabs of the weight-gradient GEMM; the new weight is stored to the packed
 //       row-major shadow and, through a padded LDS tile, to the packed transposed shadow
 //       that the dX GEMMs read, both with coalesced stores;
-//   vector chunk (bias, output-layer weight, 8 elements): the gradient is a sum over many
-//       per-block partials, so 32 lanes share one element and reduce with shuffles.
+//   vector chunk (bias, output-layer weight, 64 elements): the gradient is a sum over many
+//       per-tile partials: four waves split them, one coalesced row per partial.
 // Both sums run in a fixed order: results are bitwise reproducible run to run.
 //
 // Adam, per element, exactly the single-tensor formula of torch 2.x:
 //   m = m + (1 - b1) * (g - m)            (lerp_, weight < 0.5 branch)
 //   v = v * b2 + (1 - b2) * g * g         (mul_ + addcmul_)
 //   p = p + (-lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
-#include "adam.hpp"
+#include "adam_dev.hpp"
 
 namespace inf {
 namespace {
 
-struct Scalars {
-  float step_neg;  // -lr / (1 - b1^t)
-  float bc2_sqrt;  // sqrt(1 - b2^t)
-};
-
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamArgs& a, const Scalars& s) {
-  m = m + a.one_minus_b1 * (g - m);
-  v = v * a.beta2 + (a.one_minus_b2 * g) * g;
-  const float denom = sqrtf(v) / s.bc2_sqrt + a.eps;
-  p = p + s.step_neg * (m / denom);
-}
-
-// Matrix tile: ADAM_TILE_R (64) rows x ADAM_TILE_C (32) columns, 256 threads; thread
-// (rb, c4) owns rows rb and rb + 32 at columns 4*c4 .. 4*c4+3.  Every load of a phase is
-// issued before its first use (parameters + Adam state, then the split-K slabs eight at a
-// time) so each thread keeps 16-24 16-byte loads in flight.  VEC4: the tensor's rows are
-// 16-byte aligned in the flat arena (C % 4 == 0, offset % 4 == 0); otherwise the arena
-// side is accessed element-wise (slabs are always padded and aligned).
-template <typename T, bool VEC4>
-__device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
-                                            const Scalars& sc, float (*tile)[ADAM_TILE_R + 1]) {
-  const int tid = threadIdx.x;
-  const int c4 = tid & 7, rb = tid >> 3;
-  const int cl = 4 * c4;
-  const int gc = item.c0 + cl;
-  constexpr int NR = ADAM_TILE_R / 32;
-  bool ok[NR];
-  int64_t e[NR];
-  float w[NR][4], g[NR][4], m[NR][4], v[NR][4];
-  auto ld4 = [&](const float* base, int i, float (&dst)[4]) {
-    if (VEC4) {
-      const float4 t = ok[i] ? *reinterpret_cast<const float4*>(base + e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-      dst[0] = t.x, dst[1] = t.y, dst[2] = t.z, dst[3] = t.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dst[j] = (ok[i] && gc + j < seg.C) ? base[e[i] + j] : 0.f;
-    }
-  };
-  auto st4 = [&](float* base, int i, const float (&src)[4]) {
-    if (!ok[i]) return;
-    if (VEC4) {
-      *reinterpret_cast<float4*>(base + e[i]) = make_float4(src[0], src[1], src[2], src[3]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (gc + j < seg.C) base[e[i] + j] = src[j];
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int gr = item.r0 + rb + 32 * i;
-    ok[i] = gr < seg.R && gc < seg.C;
-    e[i] = seg.off + (int64_t)(ok[i] ? gr : 0) * seg.C + (ok[i] ? gc : 0);
-    ld4(a.params, i, w[i]);
-  }
-  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
-  if (adam) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      ld4(a.exp_avg, i, m[i]);
-      ld4(a.exp_avg_sq, i, v[i]);
-    }
-  }
-  if (a.grad_src == GRAD_FLAT) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i) ld4(a.grads, i, g[i]);
-  } else if (a.grad_src == GRAD_SLABS) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g[i][j] = 0.f;
-    const float* base = seg.slab + gc;
-    const int ns = seg.nslab;
-#pragma unroll 1
-    for (int k0 = 0; k0 < ns; k0 += 8) {
-      float4 t[8][NR];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float* sk = base + (int64_t)min(k0 + q, ns - 1) * seg.slab_stride;
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-          t[q][i] = ok[i] ? *reinterpret_cast<const float4*>(sk + (int64_t)(item.r0 + rb + 32 * i) * seg.slab_ld)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      // fixed order: partial 0, 1, ..., ns-1
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (k0 + q < ns) {
-#pragma unroll
-          for (int i = 0; i < NR; ++i) {
-            g[i][0] += t[q][i].x;
-            g[i][1] += t[q][i].y;
-            g[i][2] += t[q][i].z;
-            g[i][3] += t[q][i].w;
-          }
-        }
-      }
-    }
-  }
-  if (a.grad_src != GRAD_NONE) {
-    if (a.write_grads) {
-#pragma unroll
-      for (int i = 0; i < NR; ++i) st4(a.grads, i, g[i]);
-    }
-    if (adam) {
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) adam_elem(w[i][j], m[i][j], v[i][j], g[i][j], a, sc);
-        st4(a.params, i, w[i]);
-        st4(a.exp_avg, i, m[i]);
-        st4(a.exp_avg_sq, i, v[i]);
-      }
-    }
-  }
-  if (!a.write_shadow) return;
-  // packed row-major shadow: 4 consecutive columns per store (padded columns stay zero)
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int r = rb + 32 * i;
-    if (ok[i]) {
-      T* dst = reinterpret_cast<T*>(seg.W) + (int64_t)(item.r0 + r) * seg.ldw + gc;
-      if (VEC4) {
-        if constexpr (sizeof(T) == 2) {
-          const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
-          *reinterpret_cast<bf16x4*>(dst) = pk;
-        } else {
-          *reinterpret_cast<float4*>(dst) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (gc + j < seg.C) dst[j] = (T)w[i][j];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tile[cl + j][r] = w[i][j];
-    if constexpr (sizeof(T) == 2) {
-      if (seg.WF != nullptr && ok[i]) {
-        // forward fragment image: 4 consecutive k of one lane's 8 (gc % 4 == 0), in natural
-        // or accumulator k order (adam.hpp wf_acc_order)
-        const int gr = item.r0 + r;
-        const int kk = gc & 31;
-        const int slot = seg.wf_acc_order ? (kk & 15) >> 2 : kk >> 3;
-        const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
-        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
-        const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
-      }
-    }
-  }
-  __syncthreads();
-  if constexpr (sizeof(T) == 2) {
-    if (seg.WTF != nullptr) {
-      // backward fragment image, accumulator k order: thread (column c, 32-row block kbl,
-      // row group g) stores one lane's 16 bytes = rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3
-      const int cc = tid >> 3, kbl = (tid >> 2) & 1, g = tid & 3;
-      const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
-      if (gcc < seg.C && gr + 31 < seg.R) {
-        bf16x8 v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
-        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
-      }
-    }
-  }
-  // packed transposed shadow: 64 consecutive rows of one column per wave
-#pragma unroll
-  for (int i = 0; i < ADAM_TILE_R * ADAM_TILE_C / 256; ++i) {
-    const int idx = tid + 256 * i;
-    const int cc = idx / ADAM_TILE_R, r = idx % ADAM_TILE_R;
-    const int gr = item.r0 + r, gcc = item.c0 + cc;
-    if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
-  }
-}
-
-// End-of-step item: loss / SSE partials (one per chain tile) summed in a fixed order, so
-// the epoch loss is bitwise reproducible (unlike per-tile atomics), then the step's sums
-// are stored and added to the epoch sums; optionally the replayed batch index advances.
-__device__ void finish_step(const AdamArgs& a) {
-  __shared__ double rl[256], rs[256];
-  const int tid = threadIdx.x;
-  double l = 0.0, s = 0.0;
-  for (int i = tid; i < a.nloss; i += 256) {
-    l += a.loss_part[2 * i];
-    s += a.loss_part[2 * i + 1];
-  }
-  rl[tid] = l;
-  rs[tid] = s;
-  __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
-    if (tid < w) {
-      rl[tid] += rl[tid + w];
-      rs[tid] += rs[tid + w];
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    if (a.nloss > 0) {
-      a.ctrl->loss_sum = rl[0];
-      a.ctrl->sse_sum = rs[0];
-      a.ctrl->epoch_loss += rl[0];
-      a.ctrl->epoch_sse += rs[0];
-    }
-    if (a.advance) a.ctrl->batch_index += 1;
-  }
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   __shared__ float tile[ADAM_TILE_C][ADAM_TILE_R + 1];
-  __shared__ Scalars sc;
-  const AdamItem item = a.items[blockIdx.x];
-  if (item.seg < 0) {
-    if ((a.nloss > 0 || a.advance) && a.ctrl != nullptr) finish_step(a);
-    return;
-  }
-  const AdamSeg seg = a.segs[item.seg];
-  const int tid = threadIdx.x;
-
-  if (a.do_adam && tid == 0) {
-    int t = a.step_host;
-    float lr = a.lr_host;
-    if (t <= 0) t = a.ctrl->step;
-    if (!(lr > 0.f)) lr = a.ctrl->lr;
-    const double bc1 = 1.0 - pow((double)a.beta1_d, (double)t);
-    const double bc2 = 1.0 - pow((double)a.beta2_d, (double)t);
-    sc.step_neg = (float)(-((double)lr / bc1));
-    sc.bc2_sqrt = (float)sqrt(bc2);
-  }
-  if (a.do_adam) __syncthreads();
-
-  if (seg.matrix) {
-    if (item.pad & ITEM_VEC4)
-      matrix_tile<T, true>(a, seg, item, sc, tile);
-    else
-      matrix_tile<T, false>(a, seg, item, sc, tile);
-  } else {
-    // vector chunk: 8 elements x 32 lanes
-    const int el = tid >> 5, j = tid & 31;
-    const int gi = item.c0 + el;
-    const bool ok = gi < seg.C;
-    float g = 0.f;
-    if (a.grad_src == GRAD_SLABS && ok) {
-      for (int s = j; s < seg.nslab; s += 32) g += seg.slab[(int64_t)s * seg.slab_stride + gi];
-    }
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) g += __shfl_xor(g, o, 32);
-    if (j == 0 && ok) {
-      const int64_t e = seg.off + gi;
-      if (a.grad_src == GRAD_FLAT) g = a.grads[e];
-      if (a.grad_src != GRAD_NONE) {
-        if (a.write_grads) a.grads[e] = g;
-        if (a.do_adam) {
-          float w = a.params[e], m = a.exp_avg[e], v = a.exp_avg_sq[e];
-          adam_elem(w, m, v, g, a, sc);
-          a.params[e] = w;
-          a.exp_avg[e] = m;
-          a.exp_avg_sq[e] = v;
-        }
-      }
-    }
-  }
+  __shared__ adam_dev::Scalars sc;
+  adam_dev::update_item<T>(a, a.items[blockIdx.x], tile, sc);
 }
 
 }  // namespace

@@ -32,9 +32,10 @@ struct AdamSeg {
   int32_t pad_;
 };
 
-// Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = 8 elements.
+// Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = ADAM_VEC elements.
 constexpr int ADAM_TILE_R = 64;
 constexpr int ADAM_TILE_C = 32;
+constexpr int ADAM_VEC = 64;
 constexpr int ITEM_VEC4 = 1;  // AdamItem.pad flag: 16-byte aligned rows in the arena
 
 struct AdamItem {

@@ -1,0 +1,311 @@
+// Device side of the parameter update (adam.hip), shared with the weight-gradient GEMM
+// (lgemm.hip), which runs the same work items for a tile once its last split-K partial
+// has landed: one definition, bitwise-identical results either way.
+#pragma once
+
+#include <cmath>
+
+#include "adam.hpp"
+
+namespace inf {
+namespace adam_dev {
+
+struct Scalars {
+  float step_neg;  // -lr / (1 - b1^t)
+  float bc2_sqrt;  // sqrt(1 - b2^t)
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamArgs& a, const Scalars& s) {
+  m = m + a.one_minus_b1 * (g - m);
+  v = v * a.beta2 + (a.one_minus_b2 * g) * g;
+  const float denom = sqrtf(v) / s.bc2_sqrt + a.eps;
+  p = p + s.step_neg * (m / denom);
+}
+
+// Matrix tile: ADAM_TILE_R (64) rows x ADAM_TILE_C (32) columns, 256 threads; thread
+// (rb, c4) owns rows rb and rb + 32 at columns 4*c4 .. 4*c4+3.  Every load of a phase is
+// issued before its first use (parameters + Adam state, then the split-K slabs eight at a
+// time) so each thread keeps 16-24 16-byte loads in flight.  VEC4: the tensor's rows are
+// 16-byte aligned in the flat arena (C % 4 == 0, offset % 4 == 0); otherwise the arena
+// side is accessed element-wise (slabs are always padded and aligned).
+// PB: split-K partials loaded per batch; SC1: read the partials write-through (`sc1`, the
+// in-launch hand-off of lgemm.hip: they were stored sc1 by other workgroups of the launch)
+template <typename T, bool VEC4, int PB, bool SC1>
+__device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
+                                            const Scalars& sc, float (*tile)[ADAM_TILE_R + 1]) {
+  const int tid = threadIdx.x;
+  const int c4 = tid & 7, rb = tid >> 3;
+  const int cl = 4 * c4;
+  const int gc = item.c0 + cl;
+  constexpr int NR = ADAM_TILE_R / 32;
+  bool ok[NR];
+  int64_t e[NR];
+  float w[NR][4], g[NR][4], m[NR][4], v[NR][4];
+  auto ld4 = [&](const float* base, int i, float (&dst)[4]) {
+    if (VEC4) {
+      const float4 t = ok[i] ? *reinterpret_cast<const float4*>(base + e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      dst[0] = t.x, dst[1] = t.y, dst[2] = t.z, dst[3] = t.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = (ok[i] && gc + j < seg.C) ? base[e[i] + j] : 0.f;
+    }
+  };
+  auto st4 = [&](float* base, int i, const float (&src)[4]) {
+    if (!ok[i]) return;
+    if (VEC4) {
+      *reinterpret_cast<float4*>(base + e[i]) = make_float4(src[0], src[1], src[2], src[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (gc + j < seg.C) base[e[i] + j] = src[j];
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int gr = item.r0 + rb + 32 * i;
+    ok[i] = gr < seg.R && gc < seg.C;
+    e[i] = seg.off + (int64_t)(ok[i] ? gr : 0) * seg.C + (ok[i] ? gc : 0);
+    ld4(a.params, i, w[i]);
+  }
+  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
+  if (adam) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      ld4(a.exp_avg, i, m[i]);
+      ld4(a.exp_avg_sq, i, v[i]);
+    }
+  }
+  if (a.grad_src == GRAD_FLAT) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) ld4(a.grads, i, g[i]);
+  } else if (a.grad_src == GRAD_SLABS) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[i][j] = 0.f;
+    const float* base = seg.slab + gc;
+    const int ns = seg.nslab;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg.slab), (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll 1
+    for (int k0 = 0; k0 < ns; k0 += PB) {
+      float4 t[PB][NR];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const float* sk = base + (int64_t)(k0 + q) * seg.slab_stride;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int64_t eo = (int64_t)(item.r0 + rb + 32 * i) * seg.slab_ld;
+          if constexpr (SC1) {
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v x = (ok[i] && k0 + q < ns)
+                              ? __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                            rs, (unsigned)((sk + eo - seg.slab) * 4), 0, 16))
+                              : f4v{0.f, 0.f, 0.f, 0.f};
+            t[q][i] = make_float4(x[0], x[1], x[2], x[3]);
+          } else {
+            t[q][i] = (ok[i] && k0 + q < ns) ? *reinterpret_cast<const float4*>(sk + eo) : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+      }
+      // fixed order: partial 0, 1, ..., ns-1
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        if (k0 + q < ns) {
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            g[i][0] += t[q][i].x;
+            g[i][1] += t[q][i].y;
+            g[i][2] += t[q][i].z;
+            g[i][3] += t[q][i].w;
+          }
+        }
+      }
+    }
+  }
+  if (a.grad_src != GRAD_NONE) {
+    if (a.write_grads) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) st4(a.grads, i, g[i]);
+    }
+    if (adam) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) adam_elem(w[i][j], m[i][j], v[i][j], g[i][j], a, sc);
+        st4(a.params, i, w[i]);
+        st4(a.exp_avg, i, m[i]);
+        st4(a.exp_avg_sq, i, v[i]);
+      }
+    }
+  }
+  if (!a.write_shadow) return;
+  // packed row-major shadow: 4 consecutive columns per store (padded columns stay zero)
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = rb + 32 * i;
+    if (ok[i]) {
+      T* dst = reinterpret_cast<T*>(seg.W) + (int64_t)(item.r0 + r) * seg.ldw + gc;
+      if (VEC4) {
+        if constexpr (sizeof(T) == 2) {
+          const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
+          *reinterpret_cast<bf16x4*>(dst) = pk;
+        } else {
+          *reinterpret_cast<float4*>(dst) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (gc + j < seg.C) dst[j] = (T)w[i][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[cl + j][r] = w[i][j];
+    if constexpr (sizeof(T) == 2) {
+      if (seg.WF != nullptr && ok[i]) {
+        // forward fragment image: 4 consecutive k of one lane's 8 (gc % 4 == 0), in natural
+        // or accumulator k order (adam.hpp wf_acc_order)
+        const int gr = item.r0 + r;
+        const int kk = gc & 31;
+        const int slot = seg.wf_acc_order ? (kk & 15) >> 2 : kk >> 3;
+        const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
+        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
+        const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (sizeof(T) == 2) {
+    if (seg.WTF != nullptr) {
+      // backward fragment image, accumulator k order: thread (column c, 32-row block kbl,
+      // row group g) stores one lane's 16 bytes = rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3
+      const int cc = tid >> 3, kbl = (tid >> 2) & 1, g = tid & 3;
+      const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
+      if (gcc < seg.C && gr + 31 < seg.R) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
+        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
+      }
+    }
+  }
+  // packed transposed shadow: 64 consecutive rows of one column per wave
+#pragma unroll
+  for (int i = 0; i < ADAM_TILE_R * ADAM_TILE_C / 256; ++i) {
+    const int idx = tid + 256 * i;
+    const int cc = idx / ADAM_TILE_R, r = idx % ADAM_TILE_R;
+    const int gr = item.r0 + r, gcc = item.c0 + cc;
+    if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
+  }
+}
+
+// End-of-step item: loss / SSE partials (one per chain tile) summed in a fixed order, so
+// the epoch loss is bitwise reproducible (unlike per-tile atomics), then the step's sums
+// are stored and added to the epoch sums; optionally the replayed batch index advances.
+__device__ inline void finish_step(const AdamArgs& a) {
+  __shared__ double rl[256], rs[256];
+  const int tid = threadIdx.x;
+  double l = 0.0, s = 0.0;
+  for (int i = tid; i < a.nloss; i += 256) {
+    l += a.loss_part[2 * i];
+    s += a.loss_part[2 * i + 1];
+  }
+  rl[tid] = l;
+  rs[tid] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) {
+      rl[tid] += rl[tid + w];
+      rs[tid] += rs[tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (a.nloss > 0) {
+      a.ctrl->loss_sum = rl[0];
+      a.ctrl->sse_sum = rs[0];
+      a.ctrl->epoch_loss += rl[0];
+      a.ctrl->epoch_sse += rs[0];
+    }
+    if (a.advance) a.ctrl->batch_index += 1;
+  }
+}
+
+// One work item (adam.hpp AdamItem) on 256 threads: a matrix tile, a vector chunk or the
+// end-of-step item.  `tile` and `sc` are the caller's LDS.
+// VT: vector-partial loads in flight per thread; PB, SC1: matrix_tile
+template <typename T, int VT = 64, int PB = 8, bool SC1 = false>
+__device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& item, float (*tile)[ADAM_TILE_R + 1],
+                                            Scalars& sc) {
+  if (item.seg < 0) {
+    if ((a.nloss > 0 || a.advance) && a.ctrl != nullptr) finish_step(a);
+    return;
+  }
+  const AdamSeg seg = a.segs[item.seg];
+  const int tid = threadIdx.x;
+
+  if (a.do_adam && tid == 0) {
+    int t = a.step_host;
+    float lr = a.lr_host;
+    if (t <= 0) t = a.ctrl->step;
+    if (!(lr > 0.f)) lr = a.ctrl->lr;
+    const double bc1 = 1.0 - pow((double)a.beta1_d, (double)t);
+    const double bc2 = 1.0 - pow((double)a.beta2_d, (double)t);
+    sc.step_neg = (float)(-((double)lr / bc1));
+    sc.bc2_sqrt = (float)sqrt(bc2);
+  }
+  if (a.do_adam) __syncthreads();
+
+  if (seg.matrix) {
+    if (item.pad & ITEM_VEC4)
+      matrix_tile<T, true, PB, SC1>(a, seg, item, sc, tile);
+    else
+      matrix_tile<T, false, PB, SC1>(a, seg, item, sc, tile);
+  } else {
+    // vector chunk: ADAM_VEC (64) consecutive elements; wave w sums the partials w, w + 4,
+    // ... (one coalesced 256-byte load per partial, up to 64 in flight: one round trip for
+    // the 256 partials of a 4096-ray step), then the four wave sums are added in a fixed order
+    const int el = tid & 63, w = tid >> 6;
+    const int gi = item.c0 + el;
+    const bool ok = gi < seg.C;
+    float g = 0.f;
+    if (a.grad_src == GRAD_SLABS) {
+      const float* base = seg.slab + (ok ? gi : 0);
+      const int ns = seg.nslab;
+#pragma unroll 1
+      for (int s0 = w; s0 < ns; s0 += 4 * VT) {
+        float t[VT];
+#pragma unroll
+        for (int q = 0; q < VT; ++q) {
+          const int sl = s0 + 4 * q;
+          t[q] = (ok && sl < ns) ? base[(int64_t)sl * seg.slab_stride] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < VT; ++q) g += t[q];
+      }
+    }
+    float* vs = &tile[0][0];  // [4][64]
+    vs[w * 64 + el] = g;
+    __syncthreads();
+    if (w == 0 && ok) {
+      g = ((vs[el] + vs[64 + el]) + vs[128 + el]) + vs[192 + el];
+      const int64_t e = seg.off + gi;
+      if (a.grad_src == GRAD_FLAT) g = a.grads[e];
+      if (a.grad_src != GRAD_NONE) {
+        if (a.write_grads) a.grads[e] = g;
+        if (a.do_adam) {
+          float pw = a.params[e], m = a.exp_avg[e], v = a.exp_avg_sq[e];
+          adam_elem(pw, m, v, g, a, sc);
+          a.params[e] = pw;
+          a.exp_avg[e] = m;
+          a.exp_avg_sq[e] = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace adam_dev
+}  // namespace inf

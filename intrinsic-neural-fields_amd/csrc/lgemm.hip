@@ -24,6 +24,7 @@
 // block computes dW^T, the slab holds dW as the update kernel reads it).
 #include <algorithm>
 
+#include "adam_dev.hpp"
 #include "lgemm.hpp"
 
 namespace inf {
@@ -43,20 +44,33 @@ struct LG {
   static constexpr int ACH = BM * 8 / 256;  // 16-byte A chunks per thread per stage
   static constexpr int A_STAGE = BM * 128;  // bytes: BM rows x 64 bf16
   static constexpr int CLD = LG_BN + 4;     // f32 staging row stride
-  static constexpr int LDS = std::max(2 * A_STAGE, BM * CLD * 4);
+  // + the fused update's LDS (adam_dev tile + scalars) and a flag word at the end
+  static constexpr int LDS = std::max(std::max(2 * A_STAGE, BM * CLD * 4), ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
   static_assert(ACH >= 1 && BM * 8 % 256 == 0, "A stage must split over 256 threads");
 };
 
 __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM>
+template <int BM, bool FUSED>
 __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   using C = LG<BM>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
+  // ---- fused update: vector / end-of-step items first ----------------------------------
+  float(*const atile)[ADAM_TILE_R + 1] = reinterpret_cast<float(*)[ADAM_TILE_R + 1]>(smem);
+  adam_dev::Scalars& asc = *reinterpret_cast<adam_dev::Scalars*>(smem + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4);
+  if (FUSED && (int)blockIdx.x < batch.n_aux) {
+    if ((int)blockIdx.x < batch.n_aux_items)
+      adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
+    return;
+  }
+  const int gblk = (int)blockIdx.x - (FUSED ? batch.n_aux : 0);  // n_aux % 8 == 0: same XCD order
+  unsigned long long* const stl =
+      (batch.stamps != nullptr && threadIdx.x == 0) ? batch.stamps + 4 * (size_t)gblk : nullptr;
+  if (stl != nullptr) stl[0] = wall_clock64();
   // ---- block -> problem / split / tile (XCD-aware order, gemm.hip) --------------------
-  int bid = (int)blockIdx.x;
+  int bid = gblk;
   if (batch.total_blocks % 8 == 0) bid = (bid & 7) * (batch.total_blocks >> 3) + (bid >> 3);
   int pi = 0;
 #pragma unroll 1
@@ -142,6 +156,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   storeA(0, ar[0]);
   loadA(RA, ar[0]);
   lg_bar();
+  if (stl != nullptr) stl[1] = wall_clock64();
 
 #pragma unroll 1
   for (int s0 = 0; s0 < nst; s0 += 4) {
@@ -170,6 +185,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
     }
   }
   __syncthreads();
+  if (stl != nullptr) stl[2] = wall_clock64();
 
   // ---- epilogue: accumulators -> f32 LDS tile ------------------------------------------
   float* Cs = reinterpret_cast<float*>(smem);
@@ -183,16 +199,51 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   __syncthreads();
 
   if (P.slab != nullptr) {
-    // dW^T tile -> slab [n][m]: four consecutive m per 16-byte store
+    // dW^T tile -> slab [n][m]: four consecutive m per 16-byte store; write-through (sc1)
+    // when another workgroup of this launch reduces it (fused update)
     float* dst = P.slab + (int64_t)split * P.slab_stride;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
     constexpr int MQ = BM / 4;
 #pragma unroll 4
     for (int q = tid; q < LG_BN * MQ; q += 256) {
       const int col = q / MQ, mq = q - col * MQ;
       const f32x4 v = {Cs[(mq * 4 + 0) * CLD + col], Cs[(mq * 4 + 1) * CLD + col], Cs[(mq * 4 + 2) * CLD + col],
                        Cs[(mq * 4 + 3) * CLD + col]};
-      *reinterpret_cast<f32x4*>(dst + (int64_t)(n0 + col) * P.slab_ld + m0 + mq * 4) = v;
+      const int64_t eo = (int64_t)(n0 + col) * P.slab_ld + m0 + mq * 4;
+      if (FUSED)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (unsigned)(eo * 4), 0, 16);
+      else
+        *reinterpret_cast<f32x4*>(dst + eo) = v;
     }
+    if (FUSED) {
+      // publish this partial (sc1 stores drained by every wave, then a relaxed agent-scope
+      // ticket: cdna_hip_programming.md split-K recipe); the last of the tile's split blocks
+      // sums them with sc1 loads (fixed order, the update kernel's own code) and applies Adam
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* last_flag = reinterpret_cast<int*>(smem + C::LDS - 16);
+      if (tid == 0) {
+        int* ctr = batch.counters + P.ctr0 + tm * P.tiles_n + tn;
+        const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == P.splits - 1;
+        // every split has arrived: ready for the next launch
+        if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last_flag = last;
+      }
+      __syncthreads();
+      if (*last_flag) {
+        // the tile is dW^T rows m0.. (inputs) x cols n0.. (outputs): weight rows n0..n0+127,
+        // columns m0..m0+BM-1 = (128 / ADAM_TILE_R) x (BM / ADAM_TILE_C) work items
+#pragma unroll 1
+        for (int it = 0; it < (LG_BN / ADAM_TILE_R) * (BM / ADAM_TILE_C); ++it) {
+          const AdamItem item{P.adam_seg, n0 + (it / (BM / ADAM_TILE_C)) * ADAM_TILE_R,
+                              m0 + (it % (BM / ADAM_TILE_C)) * ADAM_TILE_C, P.adam_vec4};
+          __syncthreads();
+          adam_dev::update_item<bf16, 16, 4, true>(batch.adam, item, atile, asc);
+        }
+      }
+    }
+    if (stl != nullptr) stl[3] = wall_clock64();
     return;
   }
   constexpr int NQ = LG_BN / 4;
@@ -228,15 +279,16 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   }
 }
 
-template <int BM>
+template <int BM, bool FUSED>
 int launch_typed(const LgemmBatch& b, hipStream_t stream) {
   constexpr int lds = LG<BM>::LDS;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    lds));
     attr = true;
   }
-  lgemm_kernel<BM><<<dim3((unsigned)b.total_blocks), dim3(256), lds, stream>>>(b);
+  lgemm_kernel<BM, FUSED><<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -263,8 +315,13 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     blocks += p.tiles_m * p.tiles_n * p.splits;
   }
   b.total_blocks = blocks;
-  if (bm == 64) return launch_typed<64>(b, stream);
-  return launch_typed<32>(b, stream);
+  if (b.fused) {
+    INF_CHECK_ARG(b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.counters != nullptr, "lgemm: fused update layout");
+    for (int i = 0; i < b.nprob; ++i)
+      INF_CHECK_ARG(b.p[i].slab != nullptr && b.p[i].adam_seg >= 0, "lgemm: fused update needs split-K slabs");
+  }
+  if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
+  return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }
 
 }  // namespace inf

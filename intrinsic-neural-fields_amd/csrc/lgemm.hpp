@@ -11,6 +11,7 @@
 // (kb * R/16 + t) KiB, lane l's 16 bytes at 16 l = row 16 t + l % 16, k = 32 kb + 8 (l / 16) + e.
 #pragma once
 
+#include "adam.hpp"
 #include "common.hpp"
 
 namespace inf {
@@ -41,12 +42,25 @@ struct LgemmProblem {
   float* slab;
   int64_t slab_ld, slab_stride;
   int32_t tiles_m, tiles_n, block_begin;
+  // fused update (LgemmBatch::fused): the weight's AdamSeg index, its ITEM_VEC4 flag, and
+  // the first of its per-tile arrival counters
+  int32_t adam_seg, adam_vec4, ctr0;
 };
 
 struct LgemmBatch {
   LgemmProblem p[LGEMM_MAX_PROBLEMS];
   int32_t nprob;
   int32_t total_blocks;
+  unsigned long long* stamps;  // diagnostics (inf_debug_block_times) or null
+  // Fused parameter update (adam.hip work items, same code): the last split-K block to
+  // finish a tile runs the matrix items of that tile on the summed partials; the first
+  // n_aux blocks of the grid (a multiple of 8; n_aux_items of them busy) run the vector
+  // and end-of-step items.  counters: one int per tile, zero between launches.
+  int32_t fused;
+  int32_t n_aux, n_aux_items;
+  const AdamItem* aux_items;
+  int32_t* counters;
+  AdamArgs adam;
 };
 
 // Rows per block for an M: 64 (the shapes of config B) or 32.

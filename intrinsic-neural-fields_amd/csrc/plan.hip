@@ -65,6 +65,8 @@ struct inf_plan {
 
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_ws_end = 0;
+  int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
+  int n_aux_items = 0;
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
   std::vector<int64_t> o_slab;                            // per param segment (weights)
   int64_t o_hw = 0, o_hb = 0;                             // head partials
@@ -94,6 +96,7 @@ struct inf_plan {
   unsigned long long* dbg_out = nullptr;
   unsigned long long* stamps = nullptr;
   int stamp_steps = 0;
+  unsigned long long* lg_stamps = nullptr;  // inf_debug_block_times
 
   template <typename T = char>
   T* W(int64_t off) const { return reinterpret_cast<T*>(ws + off); }
@@ -234,9 +237,14 @@ int build_layout(inf_plan* p) {
 
   // update work list
   int64_t nitems = 1;  // + the end-of-step item
-  for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, ADAM_TILE_R) * ceil_div(g.C, ADAM_TILE_C) : ceil_div((int64_t)g.R * g.C, 8);
+  for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, ADAM_TILE_R) * ceil_div(g.C, ADAM_TILE_C) : ceil_div((int64_t)g.R * g.C, ADAM_VEC);
   p->table_bytes = align_up((int64_t)p->segs.size() * sizeof(AdamSeg)) + align_up(nitems * sizeof(AdamItem));
   p->o_tables = take(p->table_bytes);
+  p->o_aux_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
+  int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
+  for (const auto& g : p->segs)
+    if (g.gemm) max_tiles += ceil_div(g.c_pad, 32) * ceil_div(g.R, 128);
+  p->o_counters = take(align_up(max_tiles * 4));
   p->o_ws_end = w;
   return INF_OK;
 }
@@ -337,7 +345,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
   return INF_OK;
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0);
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr);
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
@@ -374,18 +382,23 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
 
 // chain (2, 3): Y^T / dZ^T were written by the fused chain in its 16-ray blocked layout;
 // with the register-streamed chain (3) Y_0^T comes plain from the input GEMM
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse) {
   const int H = p->H, s = p->s;
   if (chain == 3) {
     // register-streamed chain: X^T, Y_l^T and dZ_l^T are fragment images (chain3.hip); one
     // lgemm launch computes every dW^T tile into the split-K slabs the update launch reduces
     LgemmBatch lb;
     std::memset(&lb, 0, sizeof(lb));
+    int ctr = 0;
     for (size_t i = 0; i < p->segs.size(); ++i) {
       const ParamSeg& g = p->segs[i];
       if (!g.gemm) continue;
       INF_CHECK_ARG(lb.nprob < LGEMM_MAX_PROBLEMS, "lgemm: too many weight matrices");
       LgemmProblem& q = lb.p[lb.nprob++];
+      q.adam_seg = (int32_t)i;
+      q.adam_vec4 = (g.C % 4 == 0 && g.off % 4 == 0) ? ITEM_VEC4 : 0;
+      q.ctr0 = ctr;
+      ctr += (g.c_pad / 64) * (g.R / LG_BN);
       const int l = g.layer;
       const bool from_input = (l == 0) || (l == s && g.sub == 1);
       // layer inputs as the chain wrote them: X^T / Y_{l-1}^T fragment images
@@ -401,6 +414,15 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain) {
       q.slab = p->W<float>(p->o_slab[i]);
       q.slab_ld = g.c_pad;
       q.slab_stride = (int64_t)g.R * g.c_pad;
+    }
+    lb.stamps = p->lg_stamps;
+    if (fuse != nullptr) {
+      lb.fused = 1;
+      lb.adam = *fuse;
+      lb.n_aux_items = p->n_aux_items;
+      lb.n_aux = (int)round_up(p->n_aux_items, 8);
+      lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
+      lb.counters = p->W<int32_t>(p->o_counters);
     }
     return launch_lgemm(lb, 64, st);
   }
@@ -880,7 +902,7 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
         a.slab = p->W<float>(p->o_colsum[g.layer]);
         a.slab_stride = p->H;
       }
-      for (int e = 0; e < a.C; e += 8) p->adam_items.push_back(AdamItem{(int32_t)i, 0, e, 0});
+      for (int e = 0; e < a.C; e += ADAM_VEC) p->adam_items.push_back(AdamItem{(int32_t)i, 0, e, 0});
     }
     p->adam_segs.push_back(a);
   }
@@ -891,6 +913,13 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
                         hipMemcpyHostToDevice));
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables + seg_bytes, p->adam_items.data(),
                         p->adam_items.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  // the vector and end-of-step items, run by the dW GEMM's first blocks when it fuses the update
+  std::vector<AdamItem> aux;
+  for (const auto& it : p->adam_items)
+    if (it.seg < 0 || !p->adam_segs[it.seg].matrix) aux.push_back(it);
+  p->n_aux_items = (int)aux.size();
+  INF_HIP_TRY(hipMemcpy(p->ws + p->o_aux_items, aux.data(), aux.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  INF_HIP_TRY(hipMemset(p->ws + p->o_counters, 0, (size_t)(p->o_ws_end - p->o_counters)));
   // padded shadow columns/rows must read as zero
   INF_HIP_TRY(hipMemset(p->shadow, 0, p->shadow_bytes));
   p->bound = true;
@@ -960,16 +989,40 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   int ck = 0;
   int Bp3 = 0;
   if ((rc = pad_batch(p, batch->batch, true, &Bp3))) return rc;
+  // the update launch's arguments for a step whose gradient partials are complete
+  auto step_update = [&](int Bp_, int nloss_) {
+    AdamArgs a = update_args(p, Bp_);
+    a.grad_src = GRAD_SLABS;
+    if (apply_adam) {
+      a.do_adam = 1;
+      a.write_shadow = 1;
+    } else {
+      a.write_grads = 1;
+    }
+    a.loss_part = p->W<double>(p->o_loss);
+    a.nloss = nloss_;
+    a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
+    return a;
+  };
   if (use_chain3(p, batch, Bp3)) {
-    // fused gather + chain -> dW GEMM (-> update below)
+    // fused gather + chain -> dW GEMM (-> update below).  INF_FUSED_UPDATE=1: the update
+    // runs inside the dW launch instead (each tile's last split-K block applies Adam to
+    // it, the first blocks do the biases and the end-of-step sums; bitwise the same) --
+    // slower today: the last arriver's four items run back to back
     const int Bp = Bp3;
     if ((rc = run_chain3(p, batch, Bp, pred, st))) return rc;
-    if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
     p->saved = false;
     p->saved_batch = batch->batch;
     p->saved_bp = Bp;
     ck = 3;
     nloss = Bp / chain3_bm(Bp);
+    if (std::getenv("INF_FUSED_UPDATE") != nullptr) {
+      p->last_chain = 3;
+      if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
+      const AdamArgs a = step_update(Bp, nloss);
+      return run_weight_grads(p, Bp, st, 3, &a);
+    }
+    if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
   } else if (chain) {
     // the chain leaves per-tile loss partials; the update launch stores their sum
     int Bp = 0;
@@ -993,18 +1046,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   p->last_chain = ck;
   const int Bp = p->saved_bp;
   if ((rc = refresh_tables(p, Bp, st, ck))) return rc;
-  AdamArgs a = update_args(p, Bp);
-  a.grad_src = GRAD_SLABS;
-  if (apply_adam) {
-    a.do_adam = 1;
-    a.write_shadow = 1;
-  } else {
-    a.write_grads = 1;
-  }
-  a.loss_part = p->W<double>(p->o_loss);
-  a.nloss = nloss;
-  a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
-  return launch_update(a, p->mode, st);
+  return launch_update(step_update(Bp, nloss), p->mode, st);
 }
 
 int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) {
@@ -1089,11 +1131,22 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
     case INF_STAGE_UPDATE: {
       if ((rc = refresh_tables(p, Bp, st, p->last_chain))) return rc;
       AdamArgs a = update_args(p, Bp);
-      INF_CHECK_ARG(p->grads != nullptr, "update stage needs a bound grads arena");
-      a.grad_src = GRAD_SLABS;  // reduce only into the grads arena: parameters unchanged
-      a.write_grads = 1;
+      a.grad_src = GRAD_SLABS;
+      if (layer == 1) {
+        // the step's update as launched by inf_train_step: Adam and the weight images
+        // (parameters change; lr from ctrl)
+        a.do_adam = 1;
+        a.write_shadow = 1;
+      } else {
+        INF_CHECK_ARG(p->grads != nullptr, "update stage needs a bound grads arena");
+        a.write_grads = 1;  // reduce only into the grads arena: parameters unchanged
+      }
       rc = launch_update(a, p->mode, st);
-      for (const auto& g : p->segs) by += 4.0 * g.R * g.C;
+      for (const auto& g : p->segs) {
+        const double n = (double)g.R * g.C;
+        by += 4.0 * n * (g.gemm ? p->dw_splits : 1) + 4.0 * n;  // partials in, gradient out
+        if (layer == 1) by += 20.0 * n + (g.gemm ? 2.0 * n * (g.ft_off >= 0 ? 4 : 3) : 0.0);
+      }
       break;
     }
     default:
@@ -1109,6 +1162,12 @@ int inf_debug_ranges(inf_plan* p, const uint64_t* ranges, int n, unsigned long l
   p->dbg_ranges = ranges;
   p->dbg_n = n;
   p->dbg_out = out;
+  return INF_OK;
+}
+
+int inf_debug_block_times(inf_plan* p, unsigned long long* stamps) {
+  INF_CHECK_ARG(p != nullptr, "debug block times");
+  p->lg_stamps = stamps;
   return INF_OK;
 }
 

@@ -75,6 +75,7 @@ _SIGNATURES = {
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "inf_debug_timing": (c_int, [c_void_p, c_void_p, c_int]),
+    "inf_debug_block_times": (c_int, [c_void_p, c_void_p]),
     "inf_run_stage": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_int, ctypes.POINTER(c_double),
                               ctypes.POINTER(c_double), c_void_p]),
 }
