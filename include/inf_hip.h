@@ -202,8 +202,10 @@ int inf_debug_timing(inf_plan* plan, unsigned long long* stamps_dev, int max_ste
 
 /* Diagnostics: when `stamps_dev` is non-null, every workgroup of the weight-gradient GEMM
  * (lgemm, register-streamed chain path) records the 100 MHz wall clock at entry, after its
- * operand prologue, after its main loop and at exit: stamps_dev[block * 4 + i], block in
- * launch order (before the XCD remap).  Pass null to turn it off. */
+ * operand prologue, after its main loop and at exit: stamps_dev[block * 8 + i], block in
+ * launch order (before the XCD remap); with the update fused in, also [4] ticket taken,
+ * [5] items decided, [6] / [7] around its update item (8 words per block).  Pass null to
+ * turn it off. */
 int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */

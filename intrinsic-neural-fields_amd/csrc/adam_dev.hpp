@@ -10,6 +10,23 @@
 namespace inf {
 namespace adam_dev {
 
+// beta^t for the step count t >= 1 by binary exponentiation in double (libm's double pow
+// is a long software sequence on one lane that every other thread of the block waits for;
+// this differs from it by a few double ulps, far below the fp32 rounding of the result)
+__device__ __forceinline__ double pow_int(double b, int t) {
+  double r = 1.0;
+  while (t > 0) {
+    if (t & 1) r *= b;
+    b *= b;
+    t >>= 1;
+  }
+  return r;
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also drains vmcnt: every
+// store and every prefetched load of the thread would be waited for at each item.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 struct Scalars {
   float step_neg;  // -lr / (1 - b1^t)
   float bc2_sqrt;  // sqrt(1 - b2^t)
@@ -20,6 +37,108 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   v = v * a.beta2 + (a.one_minus_b2 * g) * g;
   const float denom = sqrtf(v) / s.bc2_sqrt + a.eps;
   p = p + s.step_neg * (m / denom);
+}
+
+// The part of a matrix item after its gradient is summed: Adam (or the gradient store),
+// the fp32 master write-back and the packed shadows / fragment images.  `tile`: LDS.
+template <typename T, bool VEC4>
+__device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
+                                         const Scalars& sc, float (*tile)[ADAM_TILE_R + 1],
+                                         const bool (&ok)[ADAM_TILE_R / 32], const int64_t (&e)[ADAM_TILE_R / 32],
+                                         float (&w)[ADAM_TILE_R / 32][4], float (&m)[ADAM_TILE_R / 32][4],
+                                         float (&v)[ADAM_TILE_R / 32][4], const float (&g)[ADAM_TILE_R / 32][4]) {
+  const int tid = threadIdx.x;
+  const int c4 = tid & 7, rb = tid >> 3;
+  const int cl = 4 * c4;
+  const int gc = item.c0 + cl;
+  constexpr int NR = ADAM_TILE_R / 32;
+  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
+  auto st4 = [&](float* base, int i, const float (&src)[4]) {
+    if (!ok[i]) return;
+    if (VEC4) {
+      *reinterpret_cast<float4*>(base + e[i]) = make_float4(src[0], src[1], src[2], src[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (gc + j < seg.C) base[e[i] + j] = src[j];
+    }
+  };
+  if (a.grad_src != GRAD_NONE) {
+    if (a.write_grads) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) st4(a.grads, i, g[i]);
+    }
+    if (adam) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) adam_elem(w[i][j], m[i][j], v[i][j], g[i][j], a, sc);
+        st4(a.params, i, w[i]);
+        st4(a.exp_avg, i, m[i]);
+        st4(a.exp_avg_sq, i, v[i]);
+      }
+    }
+  }
+  if (!a.write_shadow) return;
+  // packed row-major shadow: 4 consecutive columns per store (padded columns stay zero)
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = rb + 32 * i;
+    if (ok[i]) {
+      T* dst = reinterpret_cast<T*>(seg.W) + (int64_t)(item.r0 + r) * seg.ldw + gc;
+      if (VEC4) {
+        if constexpr (sizeof(T) == 2) {
+          const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
+          *reinterpret_cast<bf16x4*>(dst) = pk;
+        } else {
+          *reinterpret_cast<float4*>(dst) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (gc + j < seg.C) dst[j] = (T)w[i][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[cl + j][r] = w[i][j];
+    if constexpr (sizeof(T) == 2) {
+      if (seg.WF != nullptr && ok[i]) {
+        // forward fragment image: 4 consecutive k of one lane's 8 (gc % 4 == 0), in natural
+        // or accumulator k order (adam.hpp wf_acc_order)
+        const int gr = item.r0 + r;
+        const int kk = gc & 31;
+        const int slot = seg.wf_acc_order ? (kk & 15) >> 2 : kk >> 3;
+        const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
+        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
+        const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
+      }
+    }
+  }
+  lds_barrier();
+  if constexpr (sizeof(T) == 2) {
+    if (seg.WTF != nullptr) {
+      // backward fragment image, accumulator k order: thread (column c, 32-row block kbl,
+      // row group g) stores one lane's 16 bytes = rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3
+      const int cc = tid >> 3, kbl = (tid >> 2) & 1, g = tid & 3;
+      const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
+      if (gcc < seg.C && gr + 31 < seg.R) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
+        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
+      }
+    }
+  }
+  // packed transposed shadow: 64 consecutive rows of one column per wave
+#pragma unroll
+  for (int i = 0; i < ADAM_TILE_R * ADAM_TILE_C / 256; ++i) {
+    const int idx = tid + 256 * i;
+    const int cc = idx / ADAM_TILE_R, r = idx % ADAM_TILE_R;
+    const int gr = item.r0 + r, gcc = item.c0 + cc;
+    if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
+  }
 }
 
 // Matrix tile: ADAM_TILE_R (64) rows x ADAM_TILE_C (32) columns, 256 threads; thread
@@ -48,16 +167,6 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) dst[j] = (ok[i] && gc + j < seg.C) ? base[e[i] + j] : 0.f;
-    }
-  };
-  auto st4 = [&](float* base, int i, const float (&src)[4]) {
-    if (!ok[i]) return;
-    if (VEC4) {
-      *reinterpret_cast<float4*>(base + e[i]) = make_float4(src[0], src[1], src[2], src[3]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (gc + j < seg.C) base[e[i] + j] = src[j];
     }
   };
 #pragma unroll
@@ -123,81 +232,85 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
       }
     }
   }
-  if (a.grad_src != GRAD_NONE) {
-    if (a.write_grads) {
-#pragma unroll
-      for (int i = 0; i < NR; ++i) st4(a.grads, i, g[i]);
-    }
-    if (adam) {
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) adam_elem(w[i][j], m[i][j], v[i][j], g[i][j], a, sc);
-        st4(a.params, i, w[i]);
-        st4(a.exp_avg, i, m[i]);
-        st4(a.exp_avg_sq, i, v[i]);
-      }
-    }
+  mt_apply<T, VEC4>(a, seg, item, sc, tile, ok, e, w, m, v, g);
+}
+
+// NI matrix items of one segment, software-pipelined: the next item's parameters, Adam
+// state and split-K partials (sc1: published in-launch by other workgroups, lgemm.hip)
+// are in flight while the current one is applied.  Same arithmetic in the same order as
+// matrix_tile: bitwise the same results.  Requires VEC4 rows, GRAD_SLABS and nslab <= PB.
+template <typename T, int NI, int PB>
+__device__ __forceinline__ void matrix_items_pipelined(const AdamArgs& a, const AdamSeg& seg, const AdamItem (&items)[NI],
+                                                       Scalars& sc, float (*tile)[ADAM_TILE_R + 1]) {
+  constexpr int NR = ADAM_TILE_R / 32;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int c4 = tid & 7, rb = tid >> 3;
+  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
+  if (a.do_adam && tid == 0) {
+    int t = a.step_host;
+    float lr = a.lr_host;
+    if (t <= 0) t = a.ctrl->step;
+    if (!(lr > 0.f)) lr = a.ctrl->lr;
+    const double bc1 = 1.0 - pow_int(a.beta1_d, t);
+    const double bc2 = 1.0 - pow_int(a.beta2_d, t);
+    sc.step_neg = (float)(-((double)lr / bc1));
+    sc.bc2_sqrt = (float)sqrt(bc2);
   }
-  if (!a.write_shadow) return;
-  // packed row-major shadow: 4 consecutive columns per store (padded columns stay zero)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg.slab), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int ns = seg.nslab;
+  struct Regs {
+    bool ok[NR];
+    int64_t e[NR];
+    float w[NR][4], m[NR][4], v[NR][4];
+    f4v t[PB][NR];
+  } R[2];
+  auto load = [&](const AdamItem& item, Regs& r) {
+    const int gc = item.c0 + 4 * c4;
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int r = rb + 32 * i;
-    if (ok[i]) {
-      T* dst = reinterpret_cast<T*>(seg.W) + (int64_t)(item.r0 + r) * seg.ldw + gc;
-      if (VEC4) {
-        if constexpr (sizeof(T) == 2) {
-          const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
-          *reinterpret_cast<bf16x4*>(dst) = pk;
-        } else {
-          *reinterpret_cast<float4*>(dst) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
-        }
-      } else {
+    for (int i = 0; i < NR; ++i) {
+      const int gr = item.r0 + rb + 32 * i;
+      r.ok[i] = gr < seg.R && gc < seg.C;
+      r.e[i] = seg.off + (int64_t)(r.ok[i] ? gr : 0) * seg.C + (r.ok[i] ? gc : 0);
+      auto ld = [&](const float* base, float (&dst)[4]) {
+        const float4 x = r.ok[i] ? *reinterpret_cast<const float4*>(base + r.e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[0] = x.x, dst[1] = x.y, dst[2] = x.z, dst[3] = x.w;
+      };
+      ld(a.params, r.w[i]);
+      if (adam) {
+        ld(a.exp_avg, r.m[i]);
+        ld(a.exp_avg_sq, r.v[i]);
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (gc + j < seg.C) dst[j] = (T)w[i][j];
+      for (int q = 0; q < PB; ++q) {
+        const int64_t eo = (int64_t)q * seg.slab_stride + (int64_t)gr * seg.slab_ld + gc;
+        r.t[q][i] = (r.ok[i] && q < ns)
+                        ? __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(eo * 4), 0, 16))
+                        : f4v{0.f, 0.f, 0.f, 0.f};
       }
     }
+  };
+  load(items[0], R[0]);
+  if (a.do_adam) lds_barrier();  // sc
 #pragma unroll
-    for (int j = 0; j < 4; ++j) tile[cl + j][r] = w[i][j];
-    if constexpr (sizeof(T) == 2) {
-      if (seg.WF != nullptr && ok[i]) {
-        // forward fragment image: 4 consecutive k of one lane's 8 (gc % 4 == 0), in natural
-        // or accumulator k order (adam.hpp wf_acc_order)
-        const int gr = item.r0 + r;
-        const int kk = gc & 31;
-        const int slot = seg.wf_acc_order ? (kk & 15) >> 2 : kk >> 3;
-        const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
-        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
-        const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
-      }
-    }
-  }
-  __syncthreads();
-  if constexpr (sizeof(T) == 2) {
-    if (seg.WTF != nullptr) {
-      // backward fragment image, accumulator k order: thread (column c, 32-row block kbl,
-      // row group g) stores one lane's 16 bytes = rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3
-      const int cc = tid >> 3, kbl = (tid >> 2) & 1, g = tid & 3;
-      const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
-      if (gcc < seg.C && gr + 31 < seg.R) {
-        bf16x8 v;
+  for (int it = 0; it < NI; ++it) {
+    Regs& r = R[it & 1];
+    if (it + 1 < NI) load(items[it + 1], R[(it + 1) & 1]);
+    float g[NR][4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
-        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
-      }
-    }
-  }
-  // packed transposed shadow: 64 consecutive rows of one column per wave
+    for (int i = 0; i < NR; ++i)
 #pragma unroll
-  for (int i = 0; i < ADAM_TILE_R * ADAM_TILE_C / 256; ++i) {
-    const int idx = tid + 256 * i;
-    const int cc = idx / ADAM_TILE_R, r = idx % ADAM_TILE_R;
-    const int gr = item.r0 + r, gcc = item.c0 + cc;
-    if (gr < seg.R && gcc < seg.C) reinterpret_cast<T*>(seg.WT)[(int64_t)gcc * seg.ldwt + gr] = (T)tile[cc][r];
+      for (int j = 0; j < 4; ++j) g[i][j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < PB; ++q)  // fixed order: partial 0, 1, ..., ns-1
+      if (q < ns)
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[i][j] += r.t[q][i][j];
+    lds_barrier();  // the previous item's LDS tile reads are done
+    mt_apply<T, true>(a, seg, items[it], sc, tile, r.ok, r.e, r.w, r.m, r.v, g);
   }
 }
 
@@ -251,12 +364,12 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
     float lr = a.lr_host;
     if (t <= 0) t = a.ctrl->step;
     if (!(lr > 0.f)) lr = a.ctrl->lr;
-    const double bc1 = 1.0 - pow((double)a.beta1_d, (double)t);
-    const double bc2 = 1.0 - pow((double)a.beta2_d, (double)t);
+    const double bc1 = 1.0 - pow_int(a.beta1_d, t);
+    const double bc2 = 1.0 - pow_int(a.beta2_d, t);
     sc.step_neg = (float)(-((double)lr / bc1));
     sc.bc2_sqrt = (float)sqrt(bc2);
   }
-  if (a.do_adam) __syncthreads();
+  if (a.do_adam) lds_barrier();
 
   if (seg.matrix) {
     if (item.pad & ITEM_VEC4)
@@ -288,7 +401,7 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
     }
     float* vs = &tile[0][0];  // [4][64]
     vs[w * 64 + el] = g;
-    __syncthreads();
+    lds_barrier();
     if (w == 0 && ok) {
       g = ((vs[el] + vs[64 + el]) + vs[128 + el]) + vs[192 + el];
       const int64_t e = seg.off + gi;

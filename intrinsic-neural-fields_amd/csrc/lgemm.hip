@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   }
   const int gblk = (int)blockIdx.x - (FUSED ? batch.n_aux : 0);  // n_aux % 8 == 0: same XCD order
   unsigned long long* const stl =
-      (batch.stamps != nullptr && threadIdx.x == 0) ? batch.stamps + 4 * (size_t)gblk : nullptr;
+      (batch.stamps != nullptr && threadIdx.x == 0) ? batch.stamps + 8 * (size_t)gblk : nullptr;
   if (stl != nullptr) stl[0] = wall_clock64();
   // ---- block -> problem / split / tile (XCD-aware order, gemm.hip) --------------------
   int bid = gblk;
@@ -217,31 +217,59 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
     }
     if (FUSED) {
       // publish this partial (sc1 stores drained by every wave, then a relaxed agent-scope
-      // ticket: cdna_hip_programming.md split-K recipe); the last of the tile's split blocks
-      // sums them with sc1 loads (fixed order, the update kernel's own code) and applies Adam
+      // ticket: cdna_hip_programming.md split-K recipe).  Every split block then takes one
+      // of the tile's NI update items: it waits (bounded) for the tile's last partial and
+      // claims item `split`; the last arriver claims and runs whatever is left (all of
+      // them if the waiters gave up), so no block ever waits for an item -- nothing can
+      // deadlock however the blocks are placed.  Items read the partials with sc1 loads
+      // and run the update kernel's own arithmetic (bitwise the same results).
+      // Counters never reset: per tile [0] arrivals (S per launch, so ticket / S is this
+      // launch's epoch e), [1 + i] the last epoch + 1 that claimed item i (atomic max).
+      constexpr int NI = (LG_BN / ADAM_TILE_R) * (BM / ADAM_TILE_C);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      int* last_flag = reinterpret_cast<int*>(smem + C::LDS - 16);
+      int* flag = reinterpret_cast<int*>(smem + C::LDS - 16);
+      int* ctr = batch.counters + (size_t)(P.ctr0 + tm * P.tiles_n + tn) * 8;
+      auto ld_rlx = [](int* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+      if (tid == 0) flag[0] = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stl != nullptr) stl[4] = wall_clock64();
+      __syncthreads();
+      const int ticket = flag[0];
+      const int epoch = ticket / P.splits, target = (epoch + 1) * P.splits;
+      const bool last = ticket == target - 1;
+      auto claim = [&](int it) {
+        return __hip_atomic_fetch_max(ctr + 1 + it, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch + 1;
+      };
+      const AdamSeg seg = batch.adam.segs[P.adam_seg];  // into registers once
+      auto run_item = [&](int it) {
+        const AdamItem item[1] = {AdamItem{P.adam_seg, n0 + (it / (BM / ADAM_TILE_C)) * ADAM_TILE_R,
+                                           m0 + (it % (BM / ADAM_TILE_C)) * ADAM_TILE_C, P.adam_vec4}};
+        __syncthreads();
+        if (stl != nullptr) stl[6] = wall_clock64();
+        adam_dev::matrix_items_pipelined<bf16, 1, 4>(batch.adam, seg, item, asc, atile);
+        if (stl != nullptr) stl[7] = wall_clock64();
+      };
+      __syncthreads();
       if (tid == 0) {
-        int* ctr = batch.counters + P.ctr0 + tm * P.tiles_n + tn;
-        const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == P.splits - 1;
-        // every split has arrived: ready for the next launch
-        if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *last_flag = last;
+        int won = 0;  // bit i: item i is this block's
+        if (last) {
+          // claim every item still open (those of waiters that gave up, or came late)
+          for (int it = 0; it < NI; ++it)
+            if (claim(it)) won |= 1 << it;
+        } else if (split < NI) {
+          const unsigned long long t0 = wall_clock64();
+          while (ld_rlx(ctr) < target && wall_clock64() - t0 < 20000ull)  // bounded: <= 200 us
+            __builtin_amdgcn_s_sleep(2);
+          if (ld_rlx(ctr) >= target && claim(split)) won = 1 << split;
+        }
+        flag[1] = won;
       }
       __syncthreads();
-      if (*last_flag) {
-        // the tile is dW^T rows m0.. (inputs) x cols n0.. (outputs): weight rows n0..n0+127,
-        // columns m0..m0+BM-1 = (128 / ADAM_TILE_R) x (BM / ADAM_TILE_C) work items
+      if (stl != nullptr) stl[5] = wall_clock64();
+      const int won = flag[1];
 #pragma unroll 1
-        for (int it = 0; it < (LG_BN / ADAM_TILE_R) * (BM / ADAM_TILE_C); ++it) {
-          const AdamItem item{P.adam_seg, n0 + (it / (BM / ADAM_TILE_C)) * ADAM_TILE_R,
-                              m0 + (it % (BM / ADAM_TILE_C)) * ADAM_TILE_C, P.adam_vec4};
-          __syncthreads();
-          adam_dev::update_item<bf16, 16, 4, true>(batch.adam, item, atile, asc);
-        }
-      }
+      for (int it = 0; it < NI; ++it)
+        if (won & (1 << it)) run_item(it);
     }
     if (stl != nullptr) stl[3] = wall_clock64();
     return;
@@ -318,7 +346,9 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   if (b.fused) {
     INF_CHECK_ARG(b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.counters != nullptr, "lgemm: fused update layout");
     for (int i = 0; i < b.nprob; ++i)
-      INF_CHECK_ARG(b.p[i].slab != nullptr && b.p[i].adam_seg >= 0, "lgemm: fused update needs split-K slabs");
+      INF_CHECK_ARG(b.p[i].slab != nullptr && b.p[i].adam_seg >= 0 && b.p[i].adam_vec4 && b.p[i].splits <= 4,
+                    "lgemm: fused update needs split-K slabs (at most 4), 16-byte rows");
+    INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: fused update reduces the slabs");
   }
   if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);

@@ -244,7 +244,7 @@ int build_layout(inf_plan* p) {
   int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
   for (const auto& g : p->segs)
     if (g.gemm) max_tiles += ceil_div(g.c_pad, 32) * ceil_div(g.R, 128);
-  p->o_counters = take(align_up(max_tiles * 4));
+  p->o_counters = take(align_up(max_tiles * 8 * 4));  // 8 ints per tile (lgemm.hip fused update)
   p->o_ws_end = w;
   return INF_OK;
 }

@@ -34,7 +34,7 @@ for _ in range(3):
     plan.train_step(b, None, apply_adam=True)
 torch.cuda.synchronize()
 NB = 8192
-st = torch.zeros(NB * 4, dtype=torch.int64, device="cuda")
+st = torch.zeros(NB * 8, dtype=torch.int64, device="cuda")
 for _ in range(3):
     plan.run_stage(STAGE_DW_GEMM, 0, b)
 torch.cuda.synchronize()
@@ -45,10 +45,11 @@ else:
     plan.run_stage(STAGE_DW_GEMM, 0, b)
 torch.cuda.synchronize()
 lib.inf_debug_block_times(plan.handle, None)
-t = st.cpu().numpy().reshape(NB, 4).astype(np.float64)
+t = st.cpu().numpy().reshape(NB, 8).astype(np.float64)
 n = int((t[:, 0] > 0).sum())
 t = t[:n] * 10.0 / 1e3  # 100 MHz -> us
-t -= t[:, 0].min()
+raw = t.copy()
+t = t - t[:, 0].min()
 pro, main, epi, tot = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[:, 3] - t[:, 0]
 print(f"{n} blocks, kernel span {t[:, 3].max():.2f} us")
 q = lambda v: f"median {np.median(v):.2f}  p10 {np.percentile(v, 10):.2f}  p90 {np.percentile(v, 90):.2f}  max {v.max():.2f}"
@@ -57,5 +58,10 @@ print("  prologue ", q(pro))
 print("  main     ", q(main))
 print("  epilogue ", q(epi))
 print("  total    ", q(tot))
+if (raw[:, 4] > 0).any():
+    ep = raw[:, 4] > 0
+    print("  fused: ticket after main", q(raw[ep, 4] - raw[ep, 2]), "\n         wait/claim   ", q(raw[ep, 5] - raw[ep, 4]))
+    it = raw[:, 6] > 0
+    print(f"         items run by {int(it.sum())} blocks: ", q(raw[it, 7] - raw[it, 6]))
 late = t[:, 0] > 1.0
 print(f"  blocks starting after 1 us: {int(late.sum())} (start median {np.median(t[late, 0]) if late.any() else 0:.2f})")
