@@ -249,6 +249,64 @@ def render_bench(args, device):
             "hits": nhit, "verts": V, "chunk": chunk}
 
 
+def torus_mesh(nu=640, nv=320, R=1.0, r=0.4):
+    """Synthetic render mesh: a torus grid of nu * nv vertices, 2 nu nv faces."""
+    u = np.linspace(0, 2 * np.pi, nu, endpoint=False)
+    v = np.linspace(0, 2 * np.pi, nv, endpoint=False)
+    uu, vv = np.meshgrid(u, v, indexing="ij")
+    V = np.stack([(R + r * np.cos(vv)) * np.cos(uu), (R + r * np.cos(vv)) * np.sin(uu), r * np.sin(vv)], -1)
+    i, j = np.meshgrid(np.arange(nu), np.arange(nv), indexing="ij")
+    a = i * nv + j
+    b = ((i + 1) % nu) * nv + j
+    c = ((i + 1) % nu) * nv + (j + 1) % nv
+    d = i * nv + (j + 1) % nv
+    F = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+    return V.reshape(-1, 3), F
+
+
+def render_e2e_bench(args, device):
+    """End-to-end render of a 2048x2048 view (renderer.py:64-146 incl. ray casting,
+    mesh.py:171-251): camera rays cast against a device BVH of a
+    409,600-face mesh, hit compaction, then gather + MLP + placement -- Renderer.render."""
+    import mesh as MS
+    from renderer import Renderer
+    H = W = 2048
+    Vn, Fn = torus_mesh()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    E = torch.randn((Vn.shape[0], args.k), generator=g)
+    E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
+    m = build_model(args, device)
+    t0 = time.perf_counter()
+    r = Renderer(m, MS.TriMesh(Vn, Fn), eigenfunctions=E, H=H, W=W, device=device)
+    build_s = time.perf_counter() - t0
+    th = 0.5
+    Rm = np.array([[1, 0, 0], [0, np.cos(th), -np.sin(th)], [0, np.sin(th), np.cos(th)]])
+    cam = torch.from_numpy(np.concatenate([Rm, (Rm @ np.array([0.0, 0, -3.2]))[:, None]], 1)).float()
+    K = torch.tensor([[1400.0, 0, 1024], [0, 1400, 1024], [0, 0, 1]])
+    bvh = r.ray_mesh_intersector
+    r.render(cam, K)  # warm (plan, tables)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        img = r.render(cam, K)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    # the cast alone (HIP events; one ray per pixel)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        face, bary, dirs = bvh.cast(cam, K, H, W)
+    e1.record()
+    torch.cuda.synchronize()
+    cast_ms = e0.elapsed_time(e1) / reps
+    hits = int((face >= 0).sum().item())
+    return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
+            "faces": int(Fn.shape[0]), "hits": hits, "raycast_ms": cast_ms,
+            "raycast_rays_per_s": H * W / (cast_ms * 1e-3), "bvh_nodes": bvh.num_nodes, "bvh_depth": bvh.depth,
+            "bvh_build_s": build_s, "timing": "host wall clock per Renderer.render call (incl. the hit-count readback)"}
+
+
 def cpu_baseline(args):
     """The CPU oracle (numpy fp32 restatement of the reference step, oracle/inf_oracle.py)
     on this host's cores, config B at batch 4096: bounded sample of ~cpu_seconds."""
@@ -348,6 +406,7 @@ def main():
         del tr
         torch.cuda.empty_cache()
         render = render_bench(args, device)
+        render["end_to_end"] = render_e2e_bench(args, device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -211,6 +211,41 @@ int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);
 
+/* ---- Ray casting (render path) ---------------------------------
+ * Replaces trimesh/embree in mesh.get_ray_mesh_intersector (mesh.py:111-117),
+ * mesh.create_ray_origins_and_directions (mesh.py:171-207) and mesh.ray_mesh_intersect
+ * (mesh.py:210-251): closest hit along each ray (multiple_hits=False, two-sided, t > 0)
+ * and the hit point's Cramer barycentrics w.r.t. the face's vertices in mesh order. */
+typedef struct inf_bvh inf_bvh;
+
+/* Build a BVH over a triangle mesh.  vertices: host [V][3] f32; faces: host [F][3] int64
+ * (mesh.faces).  Device memory is allocated here (not on the hot path). */
+int inf_bvh_create(const float* vertices, int64_t num_vertices, const int64_t* faces, int64_t num_faces,
+                   inf_bvh** bvh);
+void inf_bvh_destroy(inf_bvh* bvh);
+int inf_bvh_info(const inf_bvh* bvh, int64_t* num_faces, int32_t* num_nodes, int32_t* depth);
+
+/* Cast one ray per masked pixel.  cam_cv2world: host [3][4] f32 (row-major), K: host [3][3]
+ * f32; pixel_idx: device [num_rays] int64 pixel indices y * W + x in increasing order (the
+ * obj_mask_1d-selected pixels), or null for all H * W pixels.  Outputs (device, per ray):
+ * hit_face [num_rays] int32 (-1 = miss), bary [num_rays][3] f32, unit_dirs [num_rays][3] f32
+ * (or null). */
+int inf_raycast(const inf_bvh* bvh, const float* cam_cv2world, const float* K, int H, int W, const int64_t* pixel_idx,
+                int64_t num_rays, int32_t* hit_face, float* bary, float* unit_dirs, inf_stream_t stream);
+
+/* Cast given rays (mesh.ray_mesh_intersect's ray_origins / ray_directions): origins, dirs
+ * device [num_rays][3] f32; outputs as inf_raycast. */
+int inf_raycast_rays(const inf_bvh* bvh, const float* origins, const float* dirs, int64_t num_rays, int32_t* hit_face,
+                     float* bary, inf_stream_t stream);
+
+/* The hit lists of mesh.ray_mesh_intersect, in ray order: out_vids [M][3] int64 (the hit
+ * faces' vertex ids), out_bary [M][3] f32, out_ray [M] int64 (hit_ray_idxs), out_face [M]
+ * int64 (face_idxs, or null); *num_hits (device int64) = M.  Outputs are sized for
+ * num_rays; scratch: device int32 [ceil(num_rays / 256)]. */
+int inf_compact_hits(const inf_bvh* bvh, const int32_t* hit_face, const float* bary, int64_t num_rays,
+                     int32_t* scratch, int64_t* num_hits, int64_t* out_vids, float* out_bary, int64_t* out_ray,
+                     int64_t* out_face, inf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

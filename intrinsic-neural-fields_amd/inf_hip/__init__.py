@@ -76,6 +76,15 @@ _SIGNATURES = {
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "inf_debug_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "inf_debug_block_times": (c_int, [c_void_p, c_void_p]),
+    "inf_bvh_create": (c_int, [c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, ctypes.POINTER(c_void_p)]),
+    "inf_bvh_destroy": (None, [c_void_p]),
+    "inf_bvh_info": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
+                             ctypes.POINTER(ctypes.c_int32)]),
+    "inf_raycast": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, ctypes.c_int64, c_void_p,
+                            c_void_p, c_void_p, c_void_p]),
+    "inf_raycast_rays": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p]),
+    "inf_compact_hits": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_run_stage": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_int, ctypes.POINTER(c_double),
                               ctypes.POINTER(c_double), c_void_p]),
 }

@@ -275,3 +275,80 @@ class RaySource:
             T = pack_table(self.E, plan.in_pad, plan.gemm_dtype)
             self._tables[key] = T
         return T
+
+
+class Bvh:
+    """A triangle mesh's BVH on the device (inf_bvh_create): the GPU replacement of the
+    reference's trimesh/embree RayMeshIntersector (mesh.py:111-117)."""
+
+    def __init__(self, vertices, faces):
+        import numpy as np
+        v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float32).reshape(-1, 3))
+        f = np.ascontiguousarray(np.asarray(faces, dtype=np.int64).reshape(-1, 3))
+        h = c_void_p()
+        check(lib.inf_bvh_create(v.ctypes.data, v.shape[0], f.ctypes.data, f.shape[0], ctypes.byref(h)),
+              "bvh_create")
+        self.handle = h
+        self.num_vertices, self.num_faces = v.shape[0], f.shape[0]
+        nf, nn, dp = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib.inf_bvh_info(h, ctypes.byref(nf), ctypes.byref(nn), ctypes.byref(dp)), "bvh_info")
+        self.num_nodes, self.depth = nn.value, dp.value
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            lib.inf_bvh_destroy(h)
+            self.handle = None
+
+    @staticmethod
+    def _cam(camCv2world, K):
+        import numpy as np
+        cam = np.ascontiguousarray(np.asarray(torch.as_tensor(camCv2world).detach().cpu(), dtype=np.float32)[:3, :4])
+        k = np.ascontiguousarray(np.asarray(torch.as_tensor(K).detach().cpu(), dtype=np.float32)[:3, :3])
+        return cam, k
+
+    def cast(self, camCv2world, K, H: int, W: int, pixel_idx: torch.Tensor | None = None, device="cuda"):
+        """One ray per pixel (or per pixel_idx entry): per-ray hit face (-1 = miss), Cramer
+        barycentrics and unit directions, on the device."""
+        cam, k = self._cam(camCv2world, K)
+        if pixel_idx is not None:
+            require_hip(pixel_idx)
+            pixel_idx = pixel_idx.to(torch.int64).contiguous()
+            n = pixel_idx.shape[0]
+        else:
+            n = H * W
+        face = torch.empty(n, dtype=torch.int32, device=device)
+        bary = torch.empty((n, 3), dtype=torch.float32, device=device)
+        dirs = torch.empty((n, 3), dtype=torch.float32, device=device)
+        check(lib.inf_raycast(self.handle, cam.ctypes.data, k.ctypes.data, H, W, ptr(pixel_idx), n, ptr(face), ptr(bary),
+                              ptr(dirs), stream_handle()), "raycast")
+        return face, bary, dirs
+
+    def cast_rays(self, origins: torch.Tensor, dirs: torch.Tensor):
+        """Given rays (device [L][3] f32): per-ray hit face and barycentrics."""
+        require_hip(origins, dirs)
+        o = origins.to(torch.float32).contiguous()
+        d = dirs.to(torch.float32).contiguous()
+        n = o.shape[0]
+        face = torch.empty(n, dtype=torch.int32, device=o.device)
+        bary = torch.empty((n, 3), dtype=torch.float32, device=o.device)
+        check(lib.inf_raycast_rays(self.handle, ptr(o), ptr(d), n, ptr(face), ptr(bary), stream_handle()),
+              "raycast_rays")
+        return face, bary
+
+    def compact(self, face: torch.Tensor, bary: torch.Tensor):
+        """The hit lists of mesh.ray_mesh_intersect, in ray order: (vids [M][3] int64,
+        bary [M][3] f32, hit_ray_idxs [M] int64, face_idxs [M] int64)."""
+        require_hip(face, bary)
+        n = face.shape[0]
+        dev = face.device
+        scratch = torch.empty(max((n + 255) // 256, 1), dtype=torch.int32, device=dev)
+        count = torch.zeros(1, dtype=torch.int64, device=dev)
+        vids = torch.empty((n, 3), dtype=torch.int64, device=dev)
+        ob = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        ray = torch.empty(n, dtype=torch.int64, device=dev)
+        fc = torch.empty(n, dtype=torch.int64, device=dev)
+        check(lib.inf_compact_hits(self.handle, ptr(face), ptr(bary), n, ptr(scratch), ptr(count), ptr(vids), ptr(ob),
+                                   ptr(ray), ptr(fc), stream_handle()), "compact_hits")
+        m = int(count.item())
+        return vids[:m], ob[:m], ray[:m], fc[:m]

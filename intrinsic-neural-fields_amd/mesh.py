@@ -7,9 +7,15 @@
   batched variant, which fills a host buffer, the batched form keeps the result on the
   table's device.
 
-Mesh IO, the Laplace-Beltrami eigensolve and ray casting (mesh.py:19-50, 111-310,
-342-605) need igl / trimesh / embree and are outside this build's scope
-(SURVEY.md §2, §8(f) rank 1).
+* Ray casting runs on the GPU (csrc/raycast.hip):
+  `get_ray_mesh_intersector` builds a device BVH in place of trimesh/embree (mesh.py:111-117);
+  `ray_mesh_intersect` / `ray_mesh_intersect_batched` (mesh.py:210-310) and `ray_tracing`
+  (mesh.py:342-390) return the reference's hit lists (closest hit, two-sided, t > 0, Cramer
+  barycentrics), in ray order, on the device.  `load_mesh` reads OBJ / PLY triangle meshes
+  with numpy in place of igl (mesh.py:39-50).
+
+The Laplace-Beltrami eigensolve, point clouds and lens undistortion (mesh.py:111-165,
+392-605) need igl / scipy-sparse LBO tooling and stay out of scope.
 """
 from __future__ import annotations
 
@@ -90,15 +96,165 @@ def get_k_eigenfunc_vec_vals_batched(E, vertex_idxs_of_hit_faces, barycentric_co
 
 def _out_of_scope(name):
     def f(*args, **kwargs):
-        raise NotImplementedError(f"mesh.{name} needs igl/trimesh/embree and is outside this build's hot path "
-                                  "(SURVEY.md §8(f)); provide precomputed hits instead")
+        raise NotImplementedError(f"mesh.{name} needs igl / the LBO eigensolve and is outside this build's hot path "
+                                  "(SURVEY.md §2)")
     f.__name__ = name
     return f
 
 
-load_mesh = _out_of_scope("load_mesh")
 load_pointcloud = _out_of_scope("load_pointcloud")
 compute_first_k_eigenfunctions = _out_of_scope("compute_first_k_eigenfunctions")
-get_ray_mesh_intersector = _out_of_scope("get_ray_mesh_intersector")
-ray_tracing = _out_of_scope("ray_tracing")
-ray_tracing_xyz = _out_of_scope("ray_tracing_xyz")
+
+
+class TriMesh:
+    """The subset of trimesh.Trimesh the hot path uses: vertices [V][3] float64, faces
+    [F][3] int64 (mesh order kept, as the reference's igl-based loader does)."""
+
+    def __init__(self, vertices, faces):
+        self.vertices = np.asarray(vertices, dtype=np.float64).reshape(-1, 3)
+        self.faces = np.asarray(faces, dtype=np.int64).reshape(-1, 3)
+
+
+def _read_obj(path):
+    verts, faces = [], []
+    with open(path) as fh:
+        for line in fh:
+            parts = line.split()
+            if not parts:
+                continue
+            if parts[0] == "v":
+                verts.append([float(x) for x in parts[1:4]])
+            elif parts[0] == "f":
+                idx = [int(p.split("/")[0]) for p in parts[1:]]
+                idx = [i - 1 if i > 0 else len(verts) + i for i in idx]
+                for j in range(1, len(idx) - 1):  # fan-triangulate polygons
+                    faces.append([idx[0], idx[j], idx[j + 1]])
+    return np.asarray(verts, dtype=np.float64), np.asarray(faces, dtype=np.int64)
+
+
+def _read_ply(path):
+    with open(path, "rb") as fh:
+        header = []
+        while True:
+            line = fh.readline().decode("ascii", errors="replace").strip()
+            header.append(line)
+            if line == "end_header":
+                break
+        fmt = next(h.split()[1] for h in header if h.startswith("format"))
+        elems, cur = [], None
+        for h in header:
+            p = h.split()
+            if p and p[0] == "element":
+                cur = [p[1], int(p[2]), []]
+                elems.append(cur)
+            elif p and p[0] == "property" and cur is not None:
+                cur[2].append(p[1:])
+        tmap = {"char": "i1", "uchar": "u1", "int8": "i1", "uint8": "u1", "short": "i2", "ushort": "u2",
+                "int16": "i2", "uint16": "u2", "int": "i4", "uint": "u4", "int32": "i4", "uint32": "u4",
+                "float": "f4", "float32": "f4", "double": "f8", "float64": "f8"}
+        end = "<" if fmt == "binary_little_endian" else ">"
+        V = F = None
+        for name, n, props in elems:
+            if fmt == "ascii":
+                rows = [fh.readline().split() for _ in range(n)]
+                if name == "vertex":
+                    names = [q[-1] for q in props]
+                    cols = [names.index(c) for c in ("x", "y", "z")]
+                    V = np.asarray([[float(r[c]) for c in cols] for r in rows])
+                elif name == "face":
+                    F = np.asarray([[int(x) for x in r[1:4]] for r in rows], dtype=np.int64)
+                continue
+            if name == "vertex":
+                dt = np.dtype([(q[-1], end + tmap[q[0]]) for q in props])
+                arr = np.frombuffer(fh.read(dt.itemsize * n), dtype=dt, count=n)
+                V = np.stack([arr["x"], arr["y"], arr["z"]], -1).astype(np.float64)
+            elif name == "face":
+                lp = props[0]  # "list <count type> <index type> vertex_indices"
+                ct, it = np.dtype(end + tmap[lp[1]]), np.dtype(end + tmap[lp[2]])
+                F = np.empty((n, 3), dtype=np.int64)
+                for i in range(n):
+                    c = int(np.frombuffer(fh.read(ct.itemsize), dtype=ct)[0])
+                    F[i] = np.frombuffer(fh.read(it.itemsize * c), dtype=it)[:3]
+            else:
+                dt = np.dtype([(q[-1], end + tmap[q[0]]) for q in props])
+                fh.read(dt.itemsize * n)
+    return V, F
+
+
+def load_mesh(path):
+    """Reference mesh.py:39-50 (igl.read_triangle_mesh -> trimesh, order kept): OBJ / PLY."""
+    ext = path.lower().rsplit(".", 1)[-1]
+    if ext == "obj":
+        v, f = _read_obj(path)
+    elif ext == "ply":
+        v, f = _read_ply(path)
+    else:
+        raise NotImplementedError(f"mesh format .{ext}: OBJ and PLY are supported")
+    return TriMesh(v, f)
+
+
+def get_ray_mesh_intersector(mesh):
+    """Reference mesh.py:111-117 (trimesh + pyembree): a device BVH (csrc/raycast.hip)."""
+    from inf_hip import runtime
+    return runtime.Bvh(mesh.vertices, mesh.faces)
+
+
+def create_ray_origins_and_directions(camCv2world, K, mask_1d, *, H, W, distortion_coeffs=None, distortion_type=None):
+    """Reference mesh.py:171-207 on the device: (ray_origins [L][3], unit_ray_dirs [L][3])
+    for the mask-selected pixels, generated by the ray-casting kernel."""
+    if distortion_type is not None:
+        raise NotImplementedError("lens undistortion (mesh.py:186-193) is outside this build's scope")
+    from inf_hip import runtime
+    pixel_idx = None if mask_1d is None else torch.nonzero(torch.as_tensor(mask_1d).reshape(-1).cuda()).reshape(-1)
+    cam = torch.as_tensor(camCv2world, dtype=torch.float32)
+    # a one-face dummy scene is enough to generate the rays
+    bvh = runtime.Bvh(np.zeros((3, 3), np.float32), np.asarray([[0, 1, 2]]))
+    _, _, dirs = bvh.cast(camCv2world, K, H, W, pixel_idx)
+    origins = cam[:3, 3].to(dirs.device).expand(dirs.shape[0], -1)
+    return origins, dirs
+
+
+def ray_mesh_intersect(ray_mesh_intersector, mesh, ray_origins, ray_directions, return_depth=False, camCv2world=None):
+    """Reference mesh.py:210-251: (vertex_idxs_of_hit_faces [M][3], barycentric_coords
+    [M][3], hit_ray_idxs [M], face_idxs [M]) of the closest hits, in ray order, on the
+    device.  return_depth is not supported."""
+    if return_depth:
+        raise NotImplementedError("return_depth (mesh.py:226-243) is outside this build's scope")
+    o = torch.as_tensor(ray_origins, dtype=torch.float32).cuda()
+    d = torch.as_tensor(ray_directions, dtype=torch.float32).cuda()
+    face, bary = ray_mesh_intersector.cast_rays(o, d)
+    return ray_mesh_intersector.compact(face, bary)
+
+
+def ray_mesh_intersect_batched(ray_mesh_intersector, mesh, ray_origins, ray_directions):
+    """Reference mesh.py:254-310: the GPU casts all rays in one launch (no 2^18 batching)."""
+    return ray_mesh_intersect(ray_mesh_intersector, mesh, ray_origins, ray_directions)
+
+
+def cast_camera_rays(ray_mesh_intersector, camCv2world, K, obj_mask_1d=None, *, H, W):
+    """Camera rays of the mask-selected pixels cast in one launch: (vids, bary, hit_ray_idxs,
+    face_idxs, unit_ray_dirs) -- the hit lists of ray_mesh_intersect plus all L directions."""
+    pixel_idx = None
+    if obj_mask_1d is not None:
+        pixel_idx = torch.nonzero(torch.as_tensor(obj_mask_1d).reshape(-1).cuda()).reshape(-1)
+    face, bary, dirs = ray_mesh_intersector.cast(camCv2world, K, H, W, pixel_idx)
+    vids, b, hit, fidx = ray_mesh_intersector.compact(face, bary)
+    return vids, b, hit, fidx, dirs
+
+
+def ray_tracing(ray_mesh_intersector, mesh, eigenfunctions, camCv2world, K, obj_mask_1d=None, *, H, W, batched=True,
+                distortion_coeffs=None, distortion_type=None):
+    """Reference mesh.py:342-390: (first_k_eigenfunctions [M][k], hit_ray_idxs,
+    unit_ray_dirs[hit_ray_idxs], face_idxs), ray casting and gather on the device."""
+    if distortion_type is not None:
+        raise NotImplementedError("lens undistortion (mesh.py:186-193) is outside this build's scope")
+    vids, bary, hit, fidx, dirs = cast_camera_rays(ray_mesh_intersector, camCv2world, K, obj_mask_1d, H=H, W=W)
+    E = torch.as_tensor(eigenfunctions)
+    if not E.is_cuda:
+        E = E.to(vids.device)
+    feats = get_k_eigenfunc_vec_vals_batched(E, vids, bary)
+    return feats, hit, dirs[hit], fidx
+
+
+def ray_tracing_xyz(*args, **kwargs):
+    raise NotImplementedError("the xyz / ff / rff front-ends (mesh.py:395-430) are SURVEY.md §8(f) rank 3")

@@ -6,11 +6,11 @@ un-masking to H x W) runs on the HIP device in `render_hits`: gather + forward +
 in one launch sequence per 2^18-ray chunk (csrc/plan.hip inf_render), with the table
 resident on the device instead of the reference's host-side M x k feature buffer.
 
-Ray casting (reference renderer.py:71-81 -> mesh.ray_tracing) needs trimesh/embree and
-is outside this build's scope: `render()` takes its hits from a
-`ray_tracer` callable with the signature and return value of mesh.ray_tracing
-(features-or-None, hit_ray_idxs, unit_ray_dirs, face_idxs) extended by the hit
-vertex ids and barycentric coordinates, or raises.
+Ray casting (reference renderer.py:71-81 -> mesh.ray_tracing, trimesh/embree) runs on
+the GPU too (csrc/raycast.hip): given a mesh, `render()` casts
+the view's camera rays against a device BVH and hands the hit lists to `render_hits`
+without leaving the device.  A `ray_tracer` callable returning (vids, bary,
+hit_ray_idxs) overrides it.
 """
 from __future__ import annotations
 
@@ -25,14 +25,16 @@ RENDER_CHUNK = 1 << 18
 
 
 def make_renderer_with_trained_model(config, device="cuda"):
-    """Reference renderer.py:9-32 (without the mesh: ray casting is out of scope)."""
+    """Reference renderer.py:9-32."""
+    from mesh import load_mesh
+    mesh = load_mesh(config["data"]["mesh_path"])
     efuncs = load_first_k_eigenfunctions(config["data"]["eigenfunctions_path"], config["model"].get("k"),
                                          rescale_strategy=config["data"].get("rescale_strategy", "standard"),
                                          embed_strategy=config["data"].get("embed_strategy"),
                                          eigenvalues_path=config["data"].get("eigenvalues_path"))
     weights_path = os.path.join(config["training"]["out_dir"], "model.pt")
     model = load_trained_model(config["model"], weights_path, device, mesh=None)
-    return Renderer(model, None, eigenfunctions=efuncs, device=device, H=config["data"]["img_height"],
+    return Renderer(model, mesh, eigenfunctions=efuncs, device=device, H=config["data"]["img_height"],
                     W=config["data"]["img_width"])
 
 
@@ -52,7 +54,20 @@ class Renderer:
         self.background = background
         self.device = device
         self.ray_tracer = ray_tracer
+        self.ray_mesh_intersector = None
+        if ray_tracer is None and mesh is not None:
+            from mesh import get_ray_mesh_intersector
+            self.ray_mesh_intersector = get_ray_mesh_intersector(mesh)
         self._dev_features = None
+
+    def apply_mesh_transform(self, transform):
+        """Reference renderer.py:62-64: transform the vertices, rebuild the intersector."""
+        import numpy as np
+        from mesh import get_ray_mesh_intersector
+        T = np.asarray(transform, dtype=np.float64)
+        v = np.concatenate([self.mesh.vertices, np.ones((self.mesh.vertices.shape[0], 1))], 1) @ T.T
+        self.mesh.vertices = v[:, :3] / v[:, 3:4]
+        self.ray_mesh_intersector = get_ray_mesh_intersector(self.mesh)
 
     def set_height(self, height):
         self.H = height
@@ -105,13 +120,19 @@ class Renderer:
     @torch.no_grad()
     def render(self, camCv2world, K, obj_mask_1d=None, eval_render=False, distortion_coeffs=None,
                distortion_type=None):
-        """Reference renderer.py:64-146 with hits from `self.ray_tracer`."""
-        if self.ray_tracer is None:
-            raise NotImplementedError("ray casting (mesh.ray_tracing, trimesh/embree) is outside this build's hot "
-                                      "path; pass ray_tracer=... or call render_hits with precomputed hits")
-        vids, bary, hit_ray_idxs = self.ray_tracer(camCv2world, K, obj_mask_1d=obj_mask_1d, H=self.H, W=self.W,
-                                                   distortion_coeffs=distortion_coeffs,
-                                                   distortion_type=distortion_type)
+        """Reference renderer.py:64-146: camera rays cast on the device (or `self.ray_tracer`)."""
+        if self.ray_tracer is not None:
+            vids, bary, hit_ray_idxs = self.ray_tracer(camCv2world, K, obj_mask_1d=obj_mask_1d, H=self.H, W=self.W,
+                                                       distortion_coeffs=distortion_coeffs,
+                                                       distortion_type=distortion_type)
+        elif self.ray_mesh_intersector is not None:
+            if distortion_type is not None:
+                raise NotImplementedError("lens undistortion (mesh.py:186-193) is outside this build's scope")
+            from mesh import cast_camera_rays
+            vids, bary, hit_ray_idxs, _, _ = cast_camera_rays(self.ray_mesh_intersector, camCv2world, K, obj_mask_1d,
+                                                              H=self.H, W=self.W)
+        else:
+            raise ValueError("Renderer.render needs a mesh (or a ray_tracer); render_hits takes precomputed hits")
         img = self.render_hits(vids, bary, hit_ray_idxs, obj_mask_1d, return_tensor=True)
         if eval_render:
             return img.cpu(), hit_ray_idxs
