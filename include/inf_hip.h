@@ -38,6 +38,13 @@ enum {
 enum { INF_DTYPE_F32 = 0, INF_DTYPE_BF16 = 1, INF_DTYPE_I32 = 2, INF_DTYPE_I64 = 3 };
 enum { INF_MODE_FP32 = 0, INF_MODE_BF16 = 1 };             /* GEMM arithmetic          */
 enum { INF_LOSS_L2 = 0, INF_LOSS_L1 = 1, INF_LOSS_CAUCHY = 2 }; /* config.py:113-122   */
+/* Input front-end of a batch (TextureField.input_feature_embed, model.py:33-40,98-104).
+ * NONE: the table rows are the features (efuncs).  XYZ/RFF/FF: the table is the fp32
+ * V x 3 vertex table (ray_dataloader.py:28-30) and the feature of a ray is its
+ * barycentric hit position x (ray_dataloader.py:134-136), as is (XYZ) or encoded:
+ *   RFF  [cos e | sin e | x?], e_j = sum_c (2 pi x_c) B[c][j]   (layers.py:28-39)
+ *   FF   [cos e | sin e | x?], e_{c k + f} = x_c band_f        (layers.py:6-25)     */
+enum { INF_ENC_NONE = 0, INF_ENC_XYZ = 1, INF_ENC_RFF = 2, INF_ENC_FF = 3 };
 
 /* TextureField architecture (model.py:12-96, make_model model.py:199-258). */
 typedef struct inf_mlp_desc {
@@ -87,6 +94,11 @@ typedef struct inf_batch {
   int64_t num_rays;      /* entries of ray_idx (rows of vids/bary/rgb when ray_idx is  */
                          /* null); rays past it read as zero features / targets.       */
                          /* 0 = unchecked.  Vertex ids >= num_vertices read as zero.   */
+  int32_t encoding;      /* INF_ENC_* (form (a) only).  With vids == NULL the table    */
+                         /* rows are the rays' positions x themselves (batch["xyz"]). */
+  int32_t enc_k;         /* embedding size k (RFF/FF)                                  */
+  const float* enc_proj; /* RFF: B [3][enc_k]; FF: freq_bands [enc_k]                  */
+  int32_t enc_include_input; /* append x (embed_include_input)                        */
 } inf_batch;
 
 /* Device-resident step state (lets a captured HIP graph replay a whole epoch). */
@@ -116,6 +128,18 @@ int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, 
                const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
                void* out, int out_dtype, int64_t ld_out, int rows_out,
                void* out_t, int64_t ld_out_t, inf_stream_t stream);
+
+/* ---- encoders: RandomFourierFeatEnc / FourierFeatEnc forward (layers.py:6-39) applied
+ *      to the loader's interpolated hit positions (ray_dataloader.py:134-136).  With
+ *      vids == NULL, `table` holds the positions x of the rays themselves ([rows][3]).
+ *      out[b][j], j < in_dim (3, 2k(+3) or 6k(+3)); columns in_dim..ld_out-1 and rows
+ *      batch..rows_out-1 are written as zero.                                        */
+int inf_encode(const float* table, int64_t num_rows, const void* vids, int vid_dtype, const float* bary,
+               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
+               int encoding, int enc_k, const float* enc_proj, int include_input,
+               void* out, int out_dtype, int64_t ld_out, int rows_out, inf_stream_t stream);
+/* in_dim of an encoding (3, 2k + 3*inc, 6k + 3*inc); -1 for a bad encoding */
+int inf_encoded_dim(int encoding, int enc_k, int include_input);
 
 /* ---- plan: one TextureField (model.py:12-112) + its training step ---------------- */
 typedef struct inf_plan inf_plan;

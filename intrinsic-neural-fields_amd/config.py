@@ -61,10 +61,13 @@ def get_log_dir(config):
 
 
 def get_data(config, device, num_workers_per_data_loader=6):
-    """Reference config.py:56-99.  The mesh is only needed by the extrinsic (xyz/ff/rff)
-    strategies, which are out of scope, so it is not loaded.  Like the reference
+    """Reference config.py:56-99.  The mesh (config.py:58) supplies the vertex positions of
+    the extrinsic (xyz/ff/rff) strategies; efuncs runs do not need it.  Like the reference
     (config.py:85, hasattr on a dict), no test loader is built."""
     mesh = None
+    if config["model"].get("feature_strategy", "efuncs") in ("ff", "rff", "xyz"):
+        from mesh import load_mesh
+        mesh = load_mesh(config["data"]["mesh_path"])
     common = dict(eigenfunctions_path=config["data"]["eigenfunctions_path"], k=config["model"].get("k"),
                   feature_strategy=config["model"].get("feature_strategy", "efuncs"), mesh=mesh,
                   rescale_strategy=config["data"].get("rescale_strategy", "standard"),
@@ -111,6 +114,9 @@ def get_loss_fn(config):
 def get_renderer(config, model, mesh, device):
     """Reference config.py:125-139."""
     feature_strategy = config["model"].get("feature_strategy", "efuncs")
+    if feature_strategy in ("ff", "rff", "xyz"):
+        return Renderer(model, mesh, feature_strategy=feature_strategy, H=config["data"]["img_height"],
+                        W=config["data"]["img_width"], device=device)
     if feature_strategy != "efuncs":
         raise ValueError(f"Unknown feature strategy: {feature_strategy}")
     E = load_first_k_eigenfunctions(config["data"]["eigenfunctions_path"], config["model"]["k"],

@@ -73,6 +73,11 @@ __device__ __forceinline__ int64_t vid_at(const void* vids, int vid_dtype, int64
 }
 
 // ---- kernel launch wrappers (defined in the .hip files) --------------------------
+int encoded_dim(int enc, int k, int inc);
+int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype, const float* bary,
+                  const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_batch_index,
+                  int64_t num_rays, int batch, int enc, int enc_k, const float* proj, int inc, void* out,
+                  int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream);
 int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
                   int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
                   const int32_t* ctrl_batch_index, int64_t num_rays, int batch, void* out, int out_dtype,

@@ -69,6 +69,52 @@ __device__ __forceinline__ void store16<bf16>(bf16* __restrict__ p, const float 
   }
 }
 
+// Stores a 64-ray x 64-column tile held as 16 columns per lane (lane t: ray t/4, columns
+// 16(t%4)..+15): the row-major copy straight from registers, the transposed copy (used by
+// the weight-gradient GEMMs) through a padded LDS tile so both stores are coalesced.
+template <typename OutT, bool VEC>
+__device__ __forceinline__ void store_tile(const float (&acc)[16], float (&tile)[GT_COLS][GT_ROWS + 1],
+                                           OutT* __restrict__ out, int64_t ld_out, int rows_out,
+                                           OutT* __restrict__ out_t, int64_t ld_out_t) {
+  const int t = threadIdx.x;
+  const int r = t >> 2;
+  const int cq = (t & 3) * 16;
+  const int b = blockIdx.x * GT_ROWS + r;
+  const int64_t c0 = (int64_t)blockIdx.y * GT_COLS + cq;
+  if (out != nullptr && b < rows_out) {
+    OutT* dst = out + (int64_t)b * ld_out + c0;
+    if (VEC) {
+      if (c0 < ld_out) store16<OutT>(dst, acc);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (c0 + i < ld_out) dst[i] = (OutT)acc[i];
+    }
+  }
+  if (out_t != nullptr) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tile[cq + i][r] = acc[i];
+    __syncthreads();
+    const int c = t >> 2;
+    const int rq = (t & 3) * 16;
+    const int64_t gc = (int64_t)blockIdx.y * GT_COLS + c;
+    const int gb = blockIdx.x * GT_ROWS + rq;
+    if (gc < ld_out) {
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = tile[c][rq + i];
+      OutT* dst = out_t + gc * ld_out_t + gb;
+      if (VEC && gb + 16 <= rows_out) {
+        store16<OutT>(dst, v);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (gb + i < rows_out) dst[i] = (OutT)v[i];
+      }
+    }
+  }
+}
+
 // VEC: table rows / output rows are 16-byte aligned and ld multiple of 16 elements, so a
 // lane moves its 16 columns with vector loads/stores.  Otherwise a masked scalar path.
 template <typename TabT, typename OutT, bool VEC>
@@ -127,40 +173,7 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
     }
   }
 
-  // row-major tile
-  if (out != nullptr && b < rows_out) {
-    OutT* dst = out + (int64_t)b * ld_out + c0;
-    if (VEC) {
-      if (c0 < ld_out) store16<OutT>(dst, acc);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (c0 + i < ld_out) dst[i] = (OutT)acc[i];
-    }
-  }
-
-  if (out_t != nullptr) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) tile[cq + i][r] = acc[i];
-    __syncthreads();
-    const int c = t >> 2;
-    const int rq = (t & 3) * 16;
-    const int64_t gc = (int64_t)blockIdx.y * GT_COLS + c;
-    const int gb = blockIdx.x * GT_ROWS + rq;
-    if (gc < ld_out) {
-      float v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = tile[c][rq + i];
-      OutT* dst = out_t + gc * ld_out_t + gb;
-      if (VEC && gb + 16 <= rows_out) {
-        store16<OutT>(dst, v);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (gb + i < rows_out) dst[i] = (OutT)v[i];
-      }
-    }
-  }
+  store_tile<OutT, VEC>(acc, tile, out, ld_out, rows_out, out_t, ld_out_t);
 }
 
 template <typename TabT, typename OutT>
@@ -218,6 +231,121 @@ int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t 
   return launch_typed<bf16, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
                                   ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
                                       stream);
+}
+
+// Extrinsic front-ends (model.py:33-40,98-104): the barycentric hit position
+// x = sum_i bary_i * P[vid_i] over the V x 3 vertex table (ray_dataloader.py:134-136),
+// then RandomFourierFeatEnc / FourierFeatEnc (layers.py:6-39), written straight into the
+// plan's X / X^T tiles (or an fp32 feature matrix): the B x in_dim encoding never exists
+// as a separate tensor.  Lanes as in gather_kernel (4 lanes per ray, 16 columns each);
+// each lane recomputes its ray's x (3 x 12 B of L2-resident vertex rows) and evaluates
+// cos/sin with the precise ocml routines (the arguments reach ~1e3 rad).
+namespace {
+__device__ __forceinline__ float pick3(const float (&x)[3], int i) { return i == 0 ? x[0] : (i == 1 ? x[1] : x[2]); }
+
+__global__ __launch_bounds__(GT_THREADS) void encode_kernel(
+    const float* __restrict__ table, int64_t V, const void* __restrict__ vids, int vid_dtype,
+    const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype, int64_t idx_offset,
+    const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int batch, int enc, int ek,
+    const float* __restrict__ proj, int inc, int in_dim, float* __restrict__ outf, bf16* __restrict__ outb,
+    int64_t ld_out, int rows_out, float* __restrict__ outf_t, bf16* __restrict__ outb_t, int64_t ld_out_t) {
+  __shared__ float tile[GT_COLS][GT_ROWS + 1];
+  const int t = threadIdx.x;
+  const int r = t >> 2;
+  const int cq = (t & 3) * 16;
+  const int b = blockIdx.x * GT_ROWS + r;
+  const int64_t c0 = (int64_t)blockIdx.y * GT_COLS + cq;
+  int64_t offset = idx_offset;
+  if (ctrl_batch_index != nullptr) offset += (int64_t)(*ctrl_batch_index) * batch;
+
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  if (b < batch && c0 < in_dim && ray_in_range(offset, b, num_rays)) {
+    const int64_t row = ray_row(ray_idx, idx_dtype, offset, b);
+    float x[3] = {0.f, 0.f, 0.f};
+    if (vids == nullptr) {
+      if ((uint64_t)row < (uint64_t)V) {
+        x[0] = table[3 * row + 0];
+        x[1] = table[3 * row + 1];
+        x[2] = table[3 * row + 2];
+      }
+    } else {
+      const float w0 = bary[3 * row + 0], w1 = bary[3 * row + 1], w2 = bary[3 * row + 2];
+      const int64_t v0 = vid_at(vids, vid_dtype, 3 * row + 0);
+      const int64_t v1 = vid_at(vids, vid_dtype, 3 * row + 1);
+      const int64_t v2 = vid_at(vids, vid_dtype, 3 * row + 2);
+      if ((uint64_t)v0 < (uint64_t)V && (uint64_t)v1 < (uint64_t)V && (uint64_t)v2 < (uint64_t)V) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          x[c] = fmaf(w2, table[3 * v2 + c], fmaf(w1, table[3 * v1 + c], w0 * table[3 * v0 + c]));
+      }
+    }
+    // RFF: (2 * torch.pi * x) is an fp32 product with the fp32-rounded 2 pi
+    const float tp = 6.283185307179586f;
+    const float px[3] = {tp * x[0], tp * x[1], tp * x[2]};
+    const int ne = enc == INF_ENC_RFF ? ek : 3 * ek;  // embedding width before cos/sin
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int c = (int)c0 + i;
+      if (c >= in_dim) break;
+      float v;
+      if (enc == INF_ENC_XYZ) {
+        v = pick3(x, c);
+      } else if (c >= 2 * ne) {
+        v = pick3(x, c - 2 * ne);  // include_input tail
+      } else {
+        const int j = c < ne ? c : c - ne;
+        float e;
+        if (enc == INF_ENC_RFF)
+          e = fmaf(px[2], proj[2 * ek + j], fmaf(px[1], proj[ek + j], px[0] * proj[j]));
+        else
+          e = pick3(x, j / ek) * proj[j % ek];
+        v = c < ne ? cosf(e) : sinf(e);
+      }
+      acc[i] = v;
+    }
+  }
+  if (outf != nullptr || outf_t != nullptr)
+    store_tile<float, false>(acc, tile, outf, ld_out, rows_out, outf_t, ld_out_t);
+  else
+    store_tile<bf16, false>(acc, tile, outb, ld_out, rows_out, outb_t, ld_out_t);
+}
+}  // namespace
+
+int encoded_dim(int enc, int k, int inc) {
+  if (enc == INF_ENC_XYZ) return 3;
+  if (k < 1 || (inc != 0 && inc != 1)) return -1;
+  if (enc == INF_ENC_RFF) return 2 * k + 3 * inc;
+  if (enc == INF_ENC_FF) return 6 * k + 3 * inc;
+  return -1;
+}
+
+int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype, const float* bary,
+                  const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_batch_index,
+                  int64_t num_rays, int batch, int enc, int enc_k, const float* proj, int inc, void* out,
+                  int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
+  const int in_dim = encoded_dim(enc, enc_k, inc);
+  INF_CHECK_ARG(in_dim > 0, "encode: bad encoding / k / include_input");
+  INF_CHECK_ARG(table != nullptr && V > 0, "encode: null or empty vertex table");
+  INF_CHECK_ARG(vids == nullptr || (bary != nullptr && (vid_dtype == INF_DTYPE_I32 || vid_dtype == INF_DTYPE_I64)),
+                "encode: vids must be int32/int64 with barycentrics");
+  INF_CHECK_ARG(enc == INF_ENC_XYZ || proj != nullptr, "encode: missing projection / frequency bands");
+  INF_CHECK_ARG(batch >= 0 && rows_out >= batch && ld_out >= in_dim, "encode: bad output shape");
+  INF_CHECK_ARG(out != nullptr || out_t != nullptr, "encode: no output");
+  INF_CHECK_ARG(out_t == nullptr || ld_out_t >= rows_out, "encode: bad transposed output stride");
+  INF_CHECK_ARG(ray_idx == nullptr || idx_dtype == INF_DTYPE_I32 || idx_dtype == INF_DTYPE_I64,
+                "encode: ray_idx must be int32/int64");
+  INF_CHECK_ARG(out_dtype == INF_DTYPE_F32 || out_dtype == INF_DTYPE_BF16, "encode: out dtype must be f32/bf16");
+  if (rows_out == 0) return INF_OK;
+  dim3 grid((unsigned)ceil_div(rows_out, GT_ROWS), (unsigned)ceil_div(ld_out, GT_COLS));
+  const bool of = out_dtype == INF_DTYPE_F32;
+  encode_kernel<<<grid, GT_THREADS, 0, stream>>>(
+      table, V, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_batch_index, num_rays, batch, enc, enc_k,
+      proj, inc, in_dim, of ? (float*)out : nullptr, of ? nullptr : (bf16*)out, ld_out, rows_out,
+      of ? (float*)out_t : nullptr, of ? nullptr : (bf16*)out_t, ld_out_t);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
 }
 
 // Features given by the caller (model(batch) with batch["eigenfunctions"], model.py:104):

@@ -281,6 +281,15 @@ int dtype_of(const inf_plan* p) { return p->mode == INF_MODE_BF16 ? INF_DTYPE_BF
 int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStream_t st) {
   void* x0 = p->W(p->o_x0);
   void* x0t = transposed ? (void*)p->W(p->o_x0t) : nullptr;
+  if (b->table != nullptr && b->encoding != INF_ENC_NONE) {
+    INF_CHECK_ARG(b->table_dtype == INF_DTYPE_F32, "encoded batches read an fp32 vertex table");
+    INF_CHECK_ARG(encoded_dim(b->encoding, b->enc_k, b->enc_include_input) == p->d.in_dim,
+                  "encoding width does not match the model's in_dim");
+    return launch_encode((const float*)b->table, b->num_vertices, b->vids, b->vid_dtype, b->bary, b->ray_idx,
+                         b->idx_dtype, b->idx_offset, b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr,
+                         b->num_rays, b->batch, b->encoding, b->enc_k, b->enc_proj, b->enc_include_input, x0,
+                         dtype_of(p), p->k_pad, Bp, x0t, Bp, st);
+  }
   if (b->table != nullptr) {
     const int64_t k_table = p->k_pad;  // device tables are packed with k_pad zero-filled columns
     return launch_gather(b->table, b->table_dtype, b->num_vertices, (int)k_table, k_table, b->vids, b->vid_dtype,
@@ -675,7 +684,7 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   // the fused gather reads a device-resident bf16 table; the dW lgemm streams
   // K = Bp / dw_splits rays per block in 256-ray steps
   return use_chain(p) && chain3_supported(p->H, p->L, p->k_pad, Bp) && w1 != nullptr && w1->f_off >= 0 &&
-         w0->f_off >= 0 && b->table != nullptr && b->table_dtype == INF_DTYPE_BF16 &&
+         w0->f_off >= 0 && b->table != nullptr && b->encoding == INF_ENC_NONE && b->table_dtype == INF_DTYPE_BF16 &&
          (Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0 && std::getenv("INF_NO_CHAIN3") == nullptr;
 }
 
@@ -797,6 +806,19 @@ int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, 
   return launch_gather(table, table_dtype, num_vertices, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype,
                        idx_offset, nullptr, 0, batch, out, out_dtype, ld_out, rows_out, out_t, ld_out_t,
                        (hipStream_t)stream);
+}
+
+int inf_encode(const float* table, int64_t num_rows, const void* vids, int vid_dtype, const float* bary,
+               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch, int encoding, int enc_k,
+               const float* enc_proj, int include_input, void* out, int out_dtype, int64_t ld_out, int rows_out,
+               inf_stream_t stream) {
+  return launch_encode(table, num_rows, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, nullptr, 0, batch,
+                       encoding, enc_k, enc_proj, include_input, out, out_dtype, ld_out, rows_out, nullptr, 0,
+                       (hipStream_t)stream);
+}
+
+int inf_encoded_dim(int encoding, int enc_k, int include_input) {
+  return encoded_dim(encoding, enc_k, include_input);
 }
 
 int inf_plan_create(const inf_mlp_desc* desc, int max_batch, inf_plan** plan) {

@@ -22,6 +22,8 @@ LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
 STEP_ADAM, STEP_ADVANCE = 1, 2  # inf_train_step flags
+ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF = 0, 1, 2, 3
+ENC_CODES = {"xyz": ENC_XYZ, "rff": ENC_RFF, "ff": ENC_FF}
 
 c_void_p, c_int, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int32,
                                                         ctypes.c_int64, ctypes.c_float, ctypes.c_double)
@@ -43,7 +45,8 @@ class Batch(ctypes.Structure):
                 ("vids", c_void_p), ("vid_dtype", c_int32), ("bary", c_void_p), ("rgb", c_void_p),
                 ("ray_idx", c_void_p), ("idx_dtype", c_int32), ("idx_offset", c_int64),
                 ("offset_from_ctrl", c_int32), ("features", c_void_p), ("ld_features", c_int64),
-                ("batch", c_int32), ("loss_count", c_int64), ("loss", c_int32), ("num_rays", c_int64)]
+                ("batch", c_int32), ("loss_count", c_int64), ("loss", c_int32), ("num_rays", c_int64),
+                ("encoding", c_int32), ("enc_k", c_int32), ("enc_proj", c_void_p), ("enc_include_input", c_int32)]
 
 
 class Ctrl(ctypes.Structure):
@@ -60,6 +63,9 @@ _SIGNATURES = {
     "inf_abi_version": (c_int, []),
     "inf_gather": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int,
                            c_int64, c_int, c_void_p, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p]),
+    "inf_encode": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int64, c_int, c_int, c_int,
+                           c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_void_p]),
+    "inf_encoded_dim": (c_int, [c_int, c_int, c_int]),
     "inf_plan_create": (c_int, [ctypes.POINTER(MlpDesc), c_int, ctypes.POINTER(c_void_p)]),
     "inf_plan_destroy": (None, [c_void_p]),
     "inf_plan_get_info": (c_int, [c_void_p, ctypes.POINTER(PlanInfo)]),

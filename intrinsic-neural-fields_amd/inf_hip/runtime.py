@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import (CTRL_BYTES, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, LOSS_CODES, MODE_BF16, MODE_CODES, Batch,
+from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, LOSS_CODES, MODE_BF16, MODE_CODES, Batch,
                STEP_ADAM, STEP_ADVANCE, MlpDesc, PlanInfo, c_int64, c_void_p, check, lib)
 
 _TORCH_DTYPE = {DTYPE_F32: torch.float32, DTYPE_BF16: torch.bfloat16}
@@ -70,6 +70,56 @@ def gather(E: torch.Tensor, vids: torch.Tensor, bary: torch.Tensor, ray_idx: tor
     return out
 
 
+class Encoding:
+    """An input front-end (model.py:33-40): 'xyz', 'rff' (proj = the RFF matrix B [3, k],
+    layers.py:28-31) or 'ff' (proj = the frequency bands [k], layers.py:11-18)."""
+
+    def __init__(self, kind: str, k: int = 0, proj: torch.Tensor | None = None, include_input: bool = True):
+        if kind not in ENC_CODES:
+            raise ValueError(f"unknown encoding {kind!r}")
+        self.kind, self.code = kind, ENC_CODES[kind]
+        self.k = int(k) if kind != "xyz" else 0
+        self.include_input = bool(include_input) if kind != "xyz" else False
+        if kind != "xyz":
+            require_hip(proj)
+            want = (3, self.k) if kind == "rff" else (self.k,)
+            if proj is None or tuple(proj.shape) != want or proj.dtype != torch.float32 or not proj.is_contiguous():
+                raise ValueError(f"{kind} encoding needs a contiguous fp32 {list(want)} tensor")
+        self.proj = proj
+        self.dim = int(lib.inf_encoded_dim(self.code, self.k, int(self.include_input)))
+        if self.dim <= 0:
+            raise ValueError("bad encoding parameters")
+
+
+def encode(enc: Encoding, points: torch.Tensor, vids: torch.Tensor | None = None, bary: torch.Tensor | None = None,
+           ray_idx: torch.Tensor | None = None, offset: int = 0, batch: int | None = None) -> torch.Tensor:
+    """Encoded features [B, enc.dim] fp32.  With vids/bary: points is the V x 3 vertex
+    table and rays are interpolated first (ray_dataloader.py:134-136); without: points
+    are the rays' positions (layers.py:21-39 applied to batch["xyz"])."""
+    require_hip(points, vids, bary, ray_idx)
+    if points.dim() != 2 or points.shape[1] != 3 or points.dtype != torch.float32 or not points.is_contiguous():
+        raise ValueError("positions must be a contiguous fp32 [N, 3] tensor")
+    if vids is not None:
+        if vids.dim() != 2 or vids.shape[1] != 3 or not vids.is_contiguous():
+            raise ValueError("vertex ids must be a contiguous [N, 3] tensor")
+        if bary is None or bary.shape != vids.shape or bary.dtype != torch.float32 or not bary.is_contiguous():
+            raise ValueError("barycentric coordinates must be a contiguous fp32 [N, 3] tensor")
+        n_rows = ray_idx.shape[0] if ray_idx is not None else vids.shape[0]
+    else:
+        n_rows = ray_idx.shape[0] if ray_idx is not None else points.shape[0]
+    batch = n_rows - offset if batch is None else batch
+    if batch < 0 or offset + batch > n_rows:
+        raise ValueError("batch out of range")
+    out = torch.empty((batch, enc.dim), dtype=torch.float32, device=points.device)
+    if batch == 0:
+        return out
+    check(lib.inf_encode(ptr(points), points.shape[0], ptr(vids), dtype_code(vids) if vids is not None else DTYPE_I32,
+                         ptr(bary), ptr(ray_idx), dtype_code(ray_idx) if ray_idx is not None else DTYPE_I64, offset,
+                         batch, enc.code, enc.k, ptr(enc.proj), int(enc.include_input), ptr(out), DTYPE_F32,
+                         out.stride(0), out.shape[0], stream_handle()), "encode")
+    return out
+
+
 def pack_table(E: torch.Tensor, k_pad: int, dtype: torch.dtype) -> torch.Tensor:
     """Device copy of the V x k table with zero columns up to k_pad (the GEMM tile),
     in the GEMM dtype (mesh.py:53-108 produces E; this is the upload of it)."""
@@ -117,6 +167,7 @@ class Plan:
         for t in (self.shadow, self.workspace):
             assert t.data_ptr() % 256 == 0
         self.params = params
+        self.encoding: Encoding | None = None  # the model's front-end (set by TextureField)
         self.bind(grads, exp_avg, exp_avg_sq)
 
     def bind(self, grads=None, exp_avg=None, exp_avg_sq=None):
@@ -177,9 +228,30 @@ class Plan:
         check(lib.inf_plan_set_adam(self.handle, beta1, beta2, eps), "set_adam")
 
     def make_batch(self, *, features=None, rgb=None, source=None, ray_idx=None, offset=0, batch=None, loss_count=0,
-                   offset_from_ctrl=False, loss=None) -> Batch:
+                   offset_from_ctrl=False, loss=None, xyz=None) -> Batch:
+        """Rays of a RaySource (gathered, or interpolated + encoded under self.encoding),
+        given positions `xyz` [B, 3] (encoded), or given features [B, in_dim]."""
         b = Batch()
-        if features is not None:
+        b.encoding = ENC_NONE
+        enc = self.encoding
+        if enc is not None and features is None:
+            if enc.dim != self.desc.in_dim:
+                raise ValueError(f"encoding width {enc.dim} does not match the model's in_dim {self.desc.in_dim}")
+            b.encoding, b.enc_k, b.enc_include_input = enc.code, enc.k, int(enc.include_input)
+            b.enc_proj = enc.proj.data_ptr() if enc.proj is not None else None
+        if xyz is not None:
+            if enc is None:
+                raise ValueError("positions given to a model without an xyz/ff/rff front-end")
+            require_hip(xyz)
+            if xyz.dim() != 2 or xyz.shape[1] != 3 or xyz.dtype != torch.float32 or not xyz.is_contiguous():
+                raise ValueError("positions must be a contiguous fp32 [B, 3] tensor")
+            b.table = xyz.data_ptr()
+            b.table_dtype = DTYPE_F32
+            b.num_vertices = xyz.shape[0]
+            b.vids = None
+            b.batch = xyz.shape[0] if batch is None else int(batch)
+            b.num_rays = xyz.shape[0]
+        elif features is not None:
             require_hip(features)
             if features.dtype != torch.float32 or features.dim() != 2 or features.stride(1) != 1:
                 raise ValueError("features must be a row-major fp32 [B, k] tensor")
@@ -267,6 +339,14 @@ class RaySource:
         self._tables = {}
 
     def table_for(self, plan: Plan) -> torch.Tensor:
+        if plan.encoding is not None:  # the fp32 V x 3 vertex table of the xyz front-ends
+            if self.E.dim() != 2 or self.E.shape[1] != 3:
+                raise ValueError("an xyz/ff/rff model reads the V x 3 vertex table (ray_dataloader.py:28-30)")
+            T = self._tables.get("xyz")
+            if T is None:
+                T = self.E.to(torch.float32).contiguous()
+                self._tables["xyz"] = T
+            return T
         key = (plan.in_pad, plan.gemm_dtype)
         T = self._tables.get(key)
         if T is None:

@@ -256,8 +256,16 @@ def ray_tracing(ray_mesh_intersector, mesh, eigenfunctions, camCv2world, K, obj_
     return feats, hit, dirs[hit], fidx
 
 
-def ray_tracing_xyz(*args, **kwargs):
-    raise NotImplementedError("the xyz / ff / rff front-ends (mesh.py:395-430) are SURVEY.md §8(f) rank 3")
+def ray_tracing_xyz(ray_mesh_intersector, mesh, vertices, camCv2world, K, obj_mask_1d=None, *, H, W, batched=True,
+                    distortion_coeffs=None, distortion_type=None):
+    """Reference mesh.py:388-428: (hit_points_xyz [M][3], hit_ray_idxs, unit_ray_dirs[hit],
+    face_idxs), the hit points being the barycentric sums over the hit faces' vertices."""
+    if distortion_type is not None:
+        raise NotImplementedError("lens undistortion (mesh.py:186-193) is outside this build's scope")
+    vids, bary, hit, fidx, dirs = cast_camera_rays(ray_mesh_intersector, camCv2world, K, obj_mask_1d, H=H, W=W)
+    P = torch.as_tensor(vertices if vertices is not None else mesh.vertices).to(vids.device, torch.float32)
+    xyz = get_k_eigenfunc_vec_vals_batched(P.contiguous(), vids, bary)
+    return xyz, hit, dirs[hit], fidx
 
 
 class MeshViewPreProcessor:

@@ -20,7 +20,7 @@ import weakref
 import torch
 import torch.nn as nn
 
-from layers import LinearWithConcatAndActivation
+from layers import FourierFeatEnc, LinearWithConcatAndActivation, RandomFourierFeatEnc
 
 RGB_COLOR_DIM = 3
 
@@ -61,17 +61,15 @@ class _Runtime:
 
 
 class TextureField(nn.Module):
-    """Reference model.py:12-112.  Supported: feature strategy "efuncs", ReLU,
-    batchnorm=False, sigmoid RGB head (every intrinsic config in configs/)."""
+    """Reference model.py:12-112.  Supported: feature strategies "efuncs" and the
+    extrinsic "xyz" / "rff" (and "ff", which the reference's own constructor rejects),
+    ReLU, batchnorm=False, sigmoid RGB head (every TextureField config in configs/)."""
 
     def __init__(self, num_layers, in_dim, hidden_dim, skip_layer_idx, input_feature_embed=None, embed_dim=None,
                  embed_include_input=True, embed_std=1., return_rgb=True, out_dim=RGB_COLOR_DIM, batchnorm=False,
                  activation=nn.ReLU):
         super().__init__()
         assert num_layers > 2 and 0 < skip_layer_idx and skip_layer_idx < num_layers - 1
-        if input_feature_embed in ("ff", "rff", "xyz"):
-            raise NotImplementedError(f"feature strategy '{input_feature_embed}' (extrinsic baselines) is outside "
-                                      "this build's hot path; use 'efuncs'")
         if batchnorm:
             raise NotImplementedError("batchnorm=True is not used by any intrinsic config and is not implemented")
         if activation is not nn.ReLU:
@@ -80,7 +78,15 @@ class TextureField(nn.Module):
             raise NotImplementedError("only the sigmoid RGB head is implemented")
         self.skip_layer_idx = skip_layer_idx
         self.input_feature_embed = input_feature_embed
-        self.embedding = None
+        # model.py:33-40: the encoder (and its RNG draw) precedes the layers
+        if input_feature_embed == "ff":
+            self.embedding = FourierFeatEnc(embed_dim, include_input=embed_include_input)
+            in_dim = 3 * embed_dim * 2 + (3 if embed_include_input else 0)
+        elif input_feature_embed == "rff":
+            self.embedding = RandomFourierFeatEnc(embed_dim, std=embed_std, include_input=embed_include_input)
+            in_dim = embed_dim * 2 + (3 if embed_include_input else 0)
+        else:
+            self.embedding = None
         self.num_layers = num_layers
         self.in_dim = in_dim
         self.hidden_dim = hidden_dim
@@ -136,6 +142,23 @@ class TextureField(nn.Module):
     def _versions(self):
         return tuple(p._version for p in self.parameters())
 
+    @property
+    def extrinsic(self) -> bool:
+        """Position-fed front-end (ray_dataloader.py:134-136) instead of eigenfunctions."""
+        return self.input_feature_embed in ("ff", "rff", "xyz")
+
+    def _encoding(self):
+        if not self.extrinsic:
+            return None
+        rt = _hip()
+        if self.input_feature_embed == "xyz":
+            return rt.Encoding("xyz")
+        e = self.embedding
+        proj = e.B if self.input_feature_embed == "rff" else e.freq_bands
+        if proj.dtype != torch.float32 or not proj.is_contiguous():
+            raise ValueError("the encoder's projection must be a contiguous fp32 buffer")
+        return rt.Encoding(self.input_feature_embed, proj.shape[-1], proj, e.include_input)
+
     def hip_plan(self, batch: int, loss: str = "L2"):
         rt = self.hip_runtime()
         plan = rt.plan
@@ -154,6 +177,7 @@ class TextureField(nn.Module):
         if rt.synced != versions:
             plan.sync_shadow()
             rt.synced = versions
+        plan.encoding = self._encoding()
         return plan
 
     # ---- forward (model.py:98-112) -----------------------------------------------
@@ -174,7 +198,17 @@ class TextureField(nn.Module):
         lazy = getattr(batch, "is_lazy_rays", None)
         if lazy is not None and lazy():
             feats, rays = None, batch.ray_args()
+            if rays["extrinsic"] != self.extrinsic:
+                raise ValueError("the loader's feature strategy does not match the model's input_feature_embed")
             B = rays["batch"]
+        elif self.extrinsic:
+            xyz = batch["xyz"]  # model.py:99-101
+            if not xyz.is_cuda:
+                raise RuntimeError("TextureField runs on MI355X (HIP) devices only; positions are on "
+                                   f"{xyz.device}. There is no CPU fallback.")
+            xyz = xyz.to(torch.float32).contiguous()
+            rays = {"xyz": xyz}
+            return _TextureFieldFn.apply(self, None, rays, xyz.shape[0], needs, *params)
         else:
             feats = batch["eigenfunctions"]
             if not feats.is_cuda:
@@ -207,15 +241,20 @@ class TextureField(nn.Module):
         return pred
 
 
+def _make_batch(plan, feats, rays, B):
+    if rays is None:
+        return plan.make_batch(features=feats)
+    if "xyz" in rays:
+        return plan.make_batch(xyz=rays["xyz"])
+    return plan.make_batch(source=rays["source"], ray_idx=rays["ray_idx"], offset=rays["offset"], batch=B)
+
+
 class _TextureFieldFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, module, feats, rays, B, needs, *params):
         plan = module.hip_plan(B)
         rt = module._rt
-        if rays is not None:
-            b = plan.make_batch(source=rays["source"], ray_idx=rays["ray_idx"], offset=rays["offset"], batch=B)
-        else:
-            b = plan.make_batch(features=feats)
+        b = _make_batch(plan, feats, rays, B)
         pred = torch.empty((B, 3), device=rt.device)
         plan.forward(b, pred, save=needs)
         if needs:
@@ -240,11 +279,7 @@ class _TextureFieldFn(torch.autograd.Function):
         if rt.plan is not plan or rt.saved_gen != ctx.gen:
             # activations were overwritten by another forward: recompute them
             plan = module.hip_plan(ctx.B)
-            if ctx.rays is not None:
-                r = ctx.rays
-                b = plan.make_batch(source=r["source"], ray_idx=r["ray_idx"], offset=r["offset"], batch=ctx.B)
-            else:
-                b = plan.make_batch(features=ctx.saved_tensors[0])
+            b = _make_batch(plan, ctx.saved_tensors[0] if ctx.rays is None else None, ctx.rays, ctx.B)
             plan.forward(b, torch.empty((ctx.B, 3), device=rt.device), save=True)
             rt.gen += 1
             rt.saved_gen = rt.gen
@@ -264,7 +299,7 @@ def init_weights(m):
 
 
 def make_model(model_config, mesh=None):
-    """Reference model.py:199-258 for the intrinsic (efuncs) configurations."""
+    """Reference model.py:199-258 for the TextureField configurations (efuncs, xyz, rff)."""
     view_dependence_config = model_config.get("view_dependence")
     feature_strategy = model_config.get("feature_strategy", "efuncs")
     if model_config.get("type") == "neutex":

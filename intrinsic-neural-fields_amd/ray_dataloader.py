@@ -5,7 +5,9 @@
 :103-107), batch slicing (:109-113) and drop_last semantics (:88-95).  The arrays live
 on the HIP device (:73-83).  Each batch is a `RayBatch`: a dict whose values are
 computed on first access -- "eigenfunctions" by the HIP gather (mesh.py:313-324 fused
-with the loader's index-select :122-129), "expected_rgbs" etc. by index-select -- so a
+with the loader's index-select :122-129), or for the xyz/ff/rff strategies "xyz" by the
+same gather over the V x 3 vertex positions (:134-136), "expected_rgbs" etc. by
+index-select -- so a
 consumer that reads `batch["eigenfunctions"]` sees exactly the reference's tensor, while
 TextureField / Trainer hand the ray indices straight to the fused kernels and never
 materialise the B x k feature matrix.
@@ -25,7 +27,8 @@ def create_ray_dataloader(preproc_data_path, eigenfunctions_path, k, feature_str
         features = load_first_k_eigenfunctions(eigenfunctions_path, k, rescale_strategy=rescale_strategy,
                                                embed_strategy=embed_strategy, eigenvalues_path=eigenvalues_path)
     elif feature_strategy in ("ff", "rff", "xyz"):
-        raise NotImplementedError("extrinsic feature strategies (xyz/ff/rff) are outside this build's hot path")
+        # ray_dataloader.py:28-30: the vertex positions; the loader interpolates hit points
+        features = torch.as_tensor(mesh.vertices).to(dtype=torch.float32)
     else:
         raise ValueError(f"Unknown input feature strategy: {feature_strategy}")
     data = load_preprocessed_data(preproc_data_path)
@@ -43,7 +46,8 @@ class RayBatch(dict):
         self._perm = idxs          # the loader's index vector (identity or permutation)
         self._offset = offset
         self._count = count
-        self._keys = ["expected_rgbs", "eigenfunctions"]
+        self._feat_key = "eigenfunctions" if loader.feature_strategy == "efuncs" else "xyz"
+        self._keys = ["expected_rgbs", self._feat_key]
         if loader.unit_ray_dirs is not None:
             self._keys += ["unit_ray_dirs", "hit_face_idxs"]
 
@@ -53,6 +57,10 @@ class RayBatch(dict):
 
     def _compute(self, key):
         ld = self._loader
+        if key == "xyz":  # ray_dataloader.py:134-136, the same barycentric sum over the V x 3 positions
+            from inf_hip import runtime
+            return runtime.gather(ld.features, ld.source.vids32, ld.source.bary, ray_idx=self._perm,
+                                  offset=self._offset, batch=self._count)
         if key == "eigenfunctions":
             from inf_hip import runtime
             v = runtime.gather(ld.features, ld.source.vids32, ld.source.bary, ray_idx=self._perm, offset=self._offset,
@@ -98,10 +106,11 @@ class RayBatch(dict):
 
     # ---- fused-path hooks ----
     def is_lazy_rays(self):
-        return not dict.__contains__(self, "eigenfunctions")
+        return not dict.__contains__(self, self._feat_key)
 
     def ray_args(self):
-        return {"source": self._loader.source, "ray_idx": self._perm, "offset": self._offset, "batch": self._count}
+        return {"source": self._loader.source, "ray_idx": self._perm, "offset": self._offset, "batch": self._count,
+                "extrinsic": self._feat_key == "xyz"}
 
     @property
     def batch_size(self):
@@ -116,8 +125,8 @@ class RayDataLoader:
 
     def __init__(self, features, feature_strategy, vertex_idxs_of_hit_faces, barycentric_coords, expected_rgbs,
                  unit_ray_dirs, face_idxs, batch_size, shuffle, drop_last, device="cuda"):
-        if feature_strategy != "efuncs":
-            raise NotImplementedError("only the intrinsic 'efuncs' feature strategy is on this build's hot path")
+        if feature_strategy not in ("efuncs", "ff", "rff", "xyz"):
+            raise ValueError(f"Unknown input feature strategy: {feature_strategy}")
         self.device = device
         self.features = features.to(self.device).to(torch.float32).contiguous()
         self.feature_strategy = feature_strategy

@@ -43,12 +43,15 @@ class Renderer:
 
     def __init__(self, model, mesh, eigenfunctions=None, feature_strategy="efuncs", background="white", device="cpu",
                  *, H, W, ray_tracer=None):
-        if feature_strategy != "efuncs":
-            raise ValueError(f"Unknown feature strategy: {feature_strategy}")
         self.model = model
         self.mesh = mesh
         self.feature_strategy = feature_strategy
-        self.features = eigenfunctions
+        if feature_strategy == "efuncs":
+            self.features = eigenfunctions
+        elif feature_strategy in ("ff", "rff", "xyz"):  # renderer.py:44-45: the vertex positions
+            self.features = torch.as_tensor(mesh.vertices).to(dtype=torch.float32)
+        else:
+            raise ValueError(f"Unknown feature strategy: {feature_strategy}")
         self.H = H
         self.W = W
         self.background = background

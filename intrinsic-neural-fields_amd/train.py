@@ -40,7 +40,14 @@ def main():
     if args.data_parallel and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import dp
         return dp.main_distributed(config, seed)
-    mesh = None  # only the extrinsic strategies need the mesh (outside this build's scope)
+    # train.py:38 loads the mesh: the renderer casts against it and the extrinsic
+    # strategies read its vertex positions
+    mesh_path = config["data"].get("mesh_path")
+    if mesh_path is not None and os.path.exists(mesh_path):
+        from mesh import load_mesh
+        mesh = load_mesh(mesh_path)
+    else:
+        mesh = None
     data = get_data(config, device)
     model, optim = get_model_and_optim(config, mesh, device)
     model_summary(model, data)

@@ -53,6 +53,37 @@ def gather(E: np.ndarray, vids: np.ndarray, bary: np.ndarray) -> np.ndarray:
     return acc.astype(E.dtype, copy=False)
 
 
+def interp_xyz(verts: np.ndarray, vids: np.ndarray, bary: np.ndarray) -> np.ndarray:
+    """ray_dataloader.py:134-136 (ff/rff/xyz strategies): the hit position
+    bmm(bary[B,1,3], verts[vids] [B,3,3]) -- the same barycentric sum as `gather` over the
+    V x 3 vertex table."""
+    return gather(verts, vids, bary)
+
+
+def rff_encode(x: np.ndarray, B: np.ndarray, include_input: bool = True) -> np.ndarray:
+    """layers.py:28-39 RandomFourierFeatEnc.forward: e = (2 pi x) @ B (B is 3 x k, drawn as
+    randn(3, k) * std at construction), features [cos e | sin e | x]."""
+    e = (2 * np.pi * x.astype(np.float64)) @ B.astype(np.float64)
+    parts = [np.cos(e), np.sin(e)] + ([x.astype(np.float64)] if include_input else [])
+    return np.concatenate(parts, -1).astype(x.dtype)
+
+
+def ff_bands(k: int, use_logspace: bool = False, max_freq=None) -> np.ndarray:
+    """layers.py:11-18 FourierFeatEnc frequency bands (fp32, as the reference's buffer)."""
+    if use_logspace:
+        return (2.0 ** np.arange(0, k) * np.float32(np.pi)).astype(np.float32)
+    assert max_freq is not None
+    return (2.0 ** np.linspace(0, max_freq, k + 1, dtype=np.float32)[:-1] * np.float32(np.pi)).astype(np.float32)
+
+
+def ff_encode(x: np.ndarray, bands: np.ndarray, include_input: bool = True) -> np.ndarray:
+    """layers.py:21-25 FourierFeatEnc.forward: e[b, c*k + f] = x[b, c] * bands[f], features
+    [cos e | sin e | x]."""
+    e = (x.astype(np.float64)[..., None] * bands.astype(np.float64)).reshape(x.shape[0], -1)
+    parts = [np.cos(e), np.sin(e)] + ([x.astype(np.float64)] if include_input else [])
+    return np.concatenate(parts, -1).astype(x.dtype)
+
+
 # ------------------------------------------------------------------------------------
 # MLP (TextureField) forward / backward
 # ------------------------------------------------------------------------------------

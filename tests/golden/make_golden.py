@@ -21,9 +21,12 @@ Fixtures:
   g6_psnr.npz                        psnr / epoch_psnr                    evaluation_metrics.py:5-26
   g7_render.npz                      Renderer.render MLP slice + scatter  renderer.py:64-146
   g8_train_curve.npz                 tiny synthetic texture-recon run     trainer.py:164-187,232-283
+  g9_frontend_{rff,rffni,xyz}.npz    xyz loader + (R)FF encoder + 1 step  ray_dataloader.py:134-136, layers.py:6-39,
+                                                                          model.py:33-40,98-104
 
 Run:  python tests/golden/make_golden.py
 """
+import copy
 import os
 import sys
 import types
@@ -83,6 +86,7 @@ import config as ref_config                  # noqa: E402
 import trainer as ref_trainer                # noqa: E402
 import renderer as ref_renderer              # noqa: E402
 import evaluation_metrics as ref_metrics     # noqa: E402
+import layers as ref_layers                  # noqa: E402
 
 K_LIST_1023 = list(range(0, 256)) + list(range(1793, 2304)) + list(range(3840, 4096))
 assert len(K_LIST_1023) == 1023
@@ -359,6 +363,61 @@ def g8_train_curve():
          batch=np.int64(512))
 
 
+FRONTENDS = {
+    "rff": {"feature_strategy": "rff", "k": 16, "embed_std": 8.0, "embed_include_input": True},
+    "rffni": {"feature_strategy": "rff", "k": 24, "embed_std": 2.0, "embed_include_input": False},
+    "xyz": {"feature_strategy": "xyz", "k": 170},
+}
+
+
+def g9_frontends():
+    """The extrinsic front-ends: the loader's interpolated hit
+    positions, the encoders, make_model's seeded init (the RFF matrix is drawn before the
+    layers) and one L1 train step."""
+    rng = np.random.default_rng(11)
+    V, N, B = 40, 48, 16
+    verts = (rng.random((V, 3)) * 2 - 1).astype(np.float32)
+    vids, bary = synthetic_rays(rng, V, N)
+    rgb = rng.random((N, 3)).astype(np.float32)
+    for tag, fe in FRONTENDS.items():
+        ld = ref_loader.RayDataLoader(torch.from_numpy(verts), fe["feature_strategy"], torch.from_numpy(vids),
+                                      torch.from_numpy(bary), torch.from_numpy(rgb), None, None, B, False, False,
+                                      device="cpu")
+        xyz = torch.cat([b["xyz"] for b in ld]).numpy()
+        mcfg = dict(fe, num_layers=4, mlp_hidden_dim=64, skip_layer_idx=2, batchnorm=False)
+        cfg = {"model": mcfg, "training": {"lr": 1e-3, "loss_type": "L1"}}
+        torch.manual_seed(0)
+        model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+        w0 = state_dict_arrays(model, "w:")
+        with torch.no_grad():
+            feats = (model.embedding(torch.from_numpy(xyz)) if model.embedding is not None
+                     else torch.from_numpy(xyz)).numpy()
+            pred = model({"xyz": torch.from_numpy(xyz)}).numpy()
+        batch = {"xyz": torch.from_numpy(xyz[:B]), "expected_rgbs": torch.from_numpy(rgb[:B])}
+        m2 = copy.deepcopy(model)
+        l2 = ref_config.get_loss_fn(cfg)(m2(batch), batch["expected_rgbs"])
+        l2.backward()
+        grads = {"g:" + n: p.grad.numpy().copy() for n, p in m2.named_parameters()}
+        tr = _bare_trainer(model, optim, ref_config.get_loss_fn(cfg))
+        loss, pred1 = tr._train_step(batch)
+        save(f"g9_frontend_{tag}.npz", verts=verts, vids=vids, bary=bary, rgb=rgb, xyz=xyz, features=feats,
+             pred=pred, loss=np.float32(loss), pred_step=pred1.detach().numpy(), **w0, **grads,
+             **state_dict_arrays(model, "w1:"))
+    # TextureField builds FourierFeatEnc without max_freq, which its constructor asserts
+    # (layers.py:11-17 via model.py:33-35): the 'ff' strategy cannot be instantiated.
+    try:
+        ref_model.make_model({"feature_strategy": "ff", "k": 4, "num_layers": 4, "mlp_hidden_dim": 8,
+                              "skip_layer_idx": 2})
+        ff_raises = False
+    except AssertionError:
+        ff_raises = True
+    enc = ref_layers.FourierFeatEnc(5, include_input=True, use_logspace=True)
+    enc2 = ref_layers.FourierFeatEnc(6, include_input=False, use_logspace=False, max_freq=3.0)
+    x = torch.from_numpy(verts[:10])
+    save("g9_ff_encoder.npz", ff_strategy_raises=np.bool_(ff_raises), x=verts[:10], log5=enc(x).numpy(),
+         lin6=enc2(x).numpy(), bands_log5=enc.freq_bands.numpy(), bands_lin6=enc2.freq_bands.numpy())
+
+
 if __name__ == "__main__":
     import tempfile
     torch.set_num_threads(8)
@@ -372,3 +431,4 @@ if __name__ == "__main__":
         g6_psnr()
         g7_render()
         g8_train_curve()
+        g9_frontends()

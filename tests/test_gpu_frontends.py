@@ -1,0 +1,151 @@
+"""GPU parity of the extrinsic front-ends: the loader's
+interpolated hit positions (ray_dataloader.py:134-136), RandomFourierFeatEnc /
+FourierFeatEnc (layers.py:6-39) and the TextureField forward / training step fed by them
+(model.py:33-40,98-104), against the reference's own outputs (tests/golden/g9_*.npz).
+
+Tolerances: encoded features 5e-5 abs (the RFF arguments reach ~100 rad, where the
+reference's fp32 product itself rounds by ~1e-5); fp32-mode RGB 1e-4 abs; L1 loss 1e-5;
+weights after one Adam step (lr 1e-3) 1e-5 abs; bf16 mode RGB 2e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import inf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FRONTENDS = {
+    "rff": {"feature_strategy": "rff", "k": 16, "embed_std": 8.0, "embed_include_input": True},
+    "rffni": {"feature_strategy": "rff", "k": 24, "embed_std": 2.0, "embed_include_input": False},
+    "xyz": {"feature_strategy": "xyz", "k": 170},
+}
+
+
+def cfg_of(tag, mode="fp32"):
+    return {"model": dict(FRONTENDS[tag], num_layers=4, mlp_hidden_dim=64, skip_layer_idx=2,
+                          kernels={"mode": mode}),
+            "training": {"lr": 1e-3, "loss_type": "L1"}}
+
+
+def model_and_optim(tag, mode="fp32"):
+    import config
+    torch.manual_seed(0)
+    model, optim = config.get_model_and_optim(cfg_of(tag, mode), None, "cuda")
+    model.kernel_mode = mode
+    return model, optim
+
+
+def cu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("tag", ["rff", "rffni", "xyz"])
+def test_encode_kernel_matches_reference(tag):
+    """inf_encode: gather + interpolate + encode in one launch, and the positions form."""
+    from inf_hip import runtime
+    d = golden(f"g9_frontend_{tag}.npz")
+    if tag == "xyz":
+        enc = runtime.Encoding("xyz")
+    else:
+        Bm = d["w:embedding.B"]
+        enc = runtime.Encoding("rff", Bm.shape[1], cu(Bm), include_input=(tag == "rff"))
+    f1 = runtime.encode(enc, cu(d["verts"]), cu(d["vids"]), cu(d["bary"])).cpu().numpy()
+    f2 = runtime.encode(enc, cu(d["xyz"])).cpu().numpy()
+    np.testing.assert_allclose(f1, d["features"], atol=5e-5)
+    np.testing.assert_allclose(f2, d["features"], atol=5e-5)
+    if tag != "xyz":  # against the float64 oracle on the same fp32 positions
+        np.testing.assert_allclose(f2, O.rff_encode(d["xyz"].astype(np.float64), Bm.astype(np.float64),
+                                                    tag == "rff"), atol=5e-5)
+
+
+def test_ff_encoder_matches_reference():
+    import layers
+    d = golden("g9_ff_encoder.npz")
+    x = cu(d["x"])
+    e1 = layers.FourierFeatEnc(5, include_input=True, use_logspace=True).cuda()
+    e2 = layers.FourierFeatEnc(6, include_input=False, max_freq=3.0).cuda()
+    np.testing.assert_allclose(e1(x).cpu().numpy(), d["log5"], atol=2e-5)
+    np.testing.assert_allclose(e2(x).cpu().numpy(), d["lin6"], atol=2e-5)
+    # ragged leading shape and an empty batch
+    assert e1(x.view(2, 5, 3)).shape == (2, 5, 33)
+    assert e1(x[:0]).shape == (0, 33)
+
+
+@pytest.mark.parametrize("tag", ["rff", "rffni", "xyz"])
+def test_forward_and_step_match_reference(tag):
+    """model({"xyz"}) and one autograd L1 step (trainer.py:71-84) through the HIP plan."""
+    import config
+    d = golden(f"g9_frontend_{tag}.npz")
+    model, optim = model_and_optim(tag)
+    with torch.no_grad():
+        pred = model({"xyz": cu(d["xyz"])}).cpu().numpy()
+    np.testing.assert_allclose(pred, d["pred"], atol=1e-4)
+    B = 16
+    batch = {"xyz": cu(d["xyz"][:B]), "expected_rgbs": cu(d["rgb"][:B])}
+    loss_fn = config.get_loss_fn(cfg_of(tag))
+    p = model(batch)
+    lval = loss_fn(p, batch["expected_rgbs"])
+    optim.zero_grad(set_to_none=True)
+    lval.backward()
+    assert abs(lval.item() - float(d["loss"])) < 1e-5
+    for n, prm in model.named_parameters():
+        ref = d["g:" + n]
+        err = np.abs(prm.grad.cpu().numpy() - ref).max() / max(np.abs(ref).max(), 1e-12)
+        assert err < 1e-3, (n, err)
+    optim.step()
+    for n, prm in model.named_parameters():
+        np.testing.assert_allclose(prm.detach().cpu().numpy(), d["w1:" + n], atol=1e-5, err_msg=n)
+
+
+@pytest.mark.parametrize("tag", ["rff", "xyz"])
+def test_loader_fused_step_matches_reference(tag):
+    """RayDataLoader over the vertex positions + Trainer._train_step's fused path (gather +
+    encode + forward + L1 + backward + Adam in the plan's launch sequence)."""
+    import config
+    import ray_dataloader as RL
+    from trainer import Trainer
+    d = golden(f"g9_frontend_{tag}.npz")
+    ld = RL.RayDataLoader(cu(d["verts"]), FRONTENDS[tag]["feature_strategy"], cu(d["vids"]), cu(d["bary"]),
+                          cu(d["rgb"]), None, None, 16, False, False, device="cuda")
+    batches = list(ld)
+    xyz = torch.cat([b["xyz"] for b in batches]).cpu().numpy()
+    np.testing.assert_allclose(xyz, d["xyz"], atol=1e-6)
+    model, optim = model_and_optim(tag)
+    tr = Trainer.__new__(Trainer)
+    tr.model, tr.optim, tr.loss_fn = model, optim, config.get_loss_fn(cfg_of(tag))
+    tr.device = "cuda"
+    batch = next(iter(ld))
+    assert tr._can_fuse(batch)
+    loss, pred = tr._train_step(batch)
+    assert abs(float(loss) - float(d["loss"])) < 1e-5
+    np.testing.assert_allclose(pred.detach().cpu().numpy(), d["pred"][:16], atol=1e-4)
+    for n, prm in model.named_parameters():
+        np.testing.assert_allclose(prm.detach().cpu().numpy(), d["w1:" + n], atol=1e-5, err_msg=n)
+
+
+def test_bf16_mode_close_to_fp32():
+    d = golden("g9_frontend_rff.npz")
+    model, _ = model_and_optim("rff", "bf16")
+    with torch.no_grad():
+        pred = model({"xyz": cu(d["xyz"])}).cpu().numpy()
+    np.testing.assert_allclose(pred, d["pred"], atol=2e-2)
+
+
+def test_render_hits_extrinsic():
+    """Renderer over precomputed hits for an rff model (renderer.py:86-146): the hits'
+    positions interpolated and encoded inside the plan, scattered into a white image."""
+    import mesh as MS
+    from renderer import Renderer
+    d = golden("g9_frontend_rff.npz")
+    model, _ = model_and_optim("rff")
+    F = np.array([[0, 1, 2]], dtype=np.int64)
+    r = Renderer(model, MS.TriMesh(d["verts"].astype(np.float64), F), feature_strategy="rff", device="cuda",
+                 H=8, W=8, ray_tracer=lambda *a, **k: None)
+    hit = np.array([3, 9, 17, 20, 33, 40, 41, 63], dtype=np.int64)
+    n = hit.shape[0]
+    img = r.render_hits(cu(d["vids"][:n]), cu(d["bary"][:n]), cu(hit), return_tensor=True).cpu().numpy()
+    exp = np.ones((64, 3), np.float32)
+    exp[hit] = d["pred"][:n]
+    np.testing.assert_allclose(img.reshape(64, 3), exp, atol=1e-4)

@@ -29,9 +29,10 @@ def test_make_model_seed0_init_matches_reference(name):
 def test_make_model_rejects_out_of_scope():
     import model as M
     with pytest.raises(NotImplementedError):
-        M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2, "feature_strategy": "xyz"})
-    with pytest.raises(NotImplementedError):
         M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2, "activation": "sine"})
+    with pytest.raises(NotImplementedError):
+        M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2,
+                      "view_dependence": {"strategy": "intrinsic"}})
     with pytest.raises(AssertionError):
         M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 3})
 
@@ -42,6 +43,9 @@ def test_forward_refuses_cpu_tensors():
     m = M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2})
     with pytest.raises(RuntimeError, match="HIP"):
         m({"eigenfunctions": torch.zeros(4, 8)})
+    mx = M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2, "feature_strategy": "rff"})
+    with pytest.raises(RuntimeError, match="HIP"):
+        mx({"xyz": torch.zeros(4, 3)})
 
 
 def test_load_first_k_eigenfunctions_matches_reference(tmp_path):
@@ -117,3 +121,29 @@ def test_dp_shard_span():
             chunks = torch.arange(B).chunk(world)
             for r, ch in enumerate(chunks):
                 assert spans[r] == (int(ch[0]), int(ch[-1]) + 1)
+
+
+@pytest.mark.parametrize("tag", ["rff", "rffni", "xyz"])
+def test_frontend_model_init_matches_reference(tag):
+    """make_model for the extrinsic strategies (model.py:33-40,199-258): same parameter and
+    buffer names, and the same seeded values -- the RFF matrix is drawn before the layers."""
+    import model as M
+    d = golden(f"g9_frontend_{tag}.npz")
+    fe = {"rff": {"feature_strategy": "rff", "k": 16, "embed_std": 8.0, "embed_include_input": True},
+          "rffni": {"feature_strategy": "rff", "k": 24, "embed_std": 2.0, "embed_include_input": False},
+          "xyz": {"feature_strategy": "xyz", "k": 170}}[tag]
+    torch.manual_seed(0)
+    m = M.make_model(dict(fe, num_layers=4, mlp_hidden_dim=64, skip_layer_idx=2))
+    sd = m.state_dict()
+    ref = {k[2:]: d[k] for k in d.files if k.startswith("w:")}
+    assert set(sd) == set(ref)
+    for k, v in ref.items():
+        np.testing.assert_array_equal(sd[k].numpy(), v, err_msg=k)
+
+
+def test_ff_strategy_rejected_like_reference():
+    """TextureField's FourierFeatEnc has no max_freq: the reference's constructor asserts."""
+    import model as M
+    assert bool(golden("g9_ff_encoder.npz")["ff_strategy_raises"])
+    with pytest.raises(AssertionError):
+        M.make_model({"feature_strategy": "ff", "k": 4, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2})

@@ -127,3 +127,41 @@ def test_train_curve():
             sse += float(np.sum((p - d["va_rgb"][idx]) ** 2))
         val.append(O.epoch_psnr(sse / d["va_vids"].shape[0]))
     np.testing.assert_allclose(val, d["val_psnr"], atol=0.05)
+
+
+@pytest.mark.parametrize("tag", ["rff", "rffni", "xyz"])
+def test_frontends(tag):
+    """G9: xyz interpolation (ray_dataloader.py:134-136), RFF encoding (layers.py:28-39) and
+    the TextureField forward + one L1 step on the encoded features (model.py:98-104)."""
+    d = golden(f"g9_frontend_{tag}.npz")
+    xyz = O.interp_xyz(d["verts"], d["vids"], d["bary"])
+    np.testing.assert_allclose(xyz, d["xyz"], atol=1e-6)
+    w0 = weights(d)
+    if tag == "xyz":
+        feats = d["xyz"]
+    else:
+        feats = O.rff_encode(d["xyz"], w0.pop("embedding.B"), include_input=(tag == "rff"))
+        assert "w1:embedding.B" in d.files
+    # |e| reaches ~100 rad: the reference's fp32 product rounds the argument by ~1e-5
+    np.testing.assert_allclose(feats, d["features"], atol=5e-5)
+    pred, _ = O.mlp_forward(w0, d["features"], 4, 2)
+    np.testing.assert_allclose(pred, d["pred"], atol=1e-6)
+    tr = O.OracleTrainer(w0, 4, 2, 1e-3, "L1")
+    B = 16
+    lval, p1, grads = tr.step(d["features"][:B], d["rgb"][:B])
+    assert abs(lval - float(d["loss"])) < 1e-6
+    for n in O.layer_names(4, 2):
+        ref = d["g:" + n]
+        assert np.abs(grads[n] - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-12) + 1e-9, n
+        np.testing.assert_allclose(tr.w[n], d["w1:" + n], atol=1e-6, err_msg=n)
+
+
+def test_ff_encoder():
+    """G9: FourierFeatEnc (layers.py:6-25) in both band modes; TextureField's 'ff' strategy
+    trips the encoder's own max_freq assertion in the reference (model.py:33-35)."""
+    d = golden("g9_ff_encoder.npz")
+    assert bool(d["ff_strategy_raises"])
+    np.testing.assert_array_equal(O.ff_bands(5, use_logspace=True), d["bands_log5"])
+    np.testing.assert_array_equal(O.ff_bands(6, max_freq=3.0), d["bands_lin6"])
+    np.testing.assert_allclose(O.ff_encode(d["x"], d["bands_log5"], True), d["log5"], atol=2e-5)
+    np.testing.assert_allclose(O.ff_encode(d["x"], d["bands_lin6"], False), d["lin6"], atol=2e-5)
