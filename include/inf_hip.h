@@ -141,6 +141,22 @@ int inf_encode(const float* table, int64_t num_rows, const void* vids, int vid_d
 /* in_dim of an encoding (3, 2k + 3*inc, 6k + 3*inc); -1 for a bad encoding */
 int inf_encoded_dim(int encoding, int enc_k, int include_input);
 
+/* ---- evaluation metrics (evaluation_metrics.py:5-34), images fp32 [H][W][C] ------ */
+/* dssim = (1 - mean_c SSIM_c) / 2 with skimage structural_similarity(multichannel=True)
+ * defaults (7 x 7 uniform window, K1 0.01, K2 0.03, sample covariance, border of 3
+ * cropped); out[c] = channel c's mean SSIM (fp64, device).  data_range: 2.0 for float
+ * images (skimage's dtype range of a float image), 255 for uint8-valued ones.
+ * workspace: inf_ssim_workspace_bytes(H, W, C) bytes of device memory.               */
+int64_t inf_ssim_workspace_bytes(int height, int width, int channels);
+int inf_ssim(const float* fake, const float* real, int height, int width, int channels, double data_range,
+             void* workspace, double* out, inf_stream_t stream);
+/* psnr's masked mean square error (evaluation_metrics.py:5-22): out[0] = sum over the
+ * pixels with mask != 0 (all when mask is NULL) of the squared channel differences,
+ * out[1] = the number of those pixels (fp64, device).                                */
+int64_t inf_masked_sse_workspace_bytes(void);
+int inf_masked_sse(const float* fake, const float* real, const uint8_t* mask, int64_t num_pixels, int channels,
+                   void* workspace, double* out, inf_stream_t stream);
+
 /* ---- plan: one TextureField (model.py:12-112) + its training step ---------------- */
 typedef struct inf_plan inf_plan;
 

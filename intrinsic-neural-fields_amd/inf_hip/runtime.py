@@ -120,6 +120,42 @@ def encode(enc: Encoding, points: torch.Tensor, vids: torch.Tensor | None = None
     return out
 
 
+def ssim(fake: torch.Tensor, real: torch.Tensor, data_range: float = 2.0) -> float:
+    """Mean SSIM over channels of two fp32 [H, W, C] device images (csrc/metrics.hip)."""
+    require_hip(fake, real)
+    if fake.shape != real.shape or fake.dim() != 3:
+        raise ValueError("images must be [H, W, C] of the same shape")
+    a = fake.to(torch.float32).contiguous()
+    b = real.to(torch.float32).contiguous()
+    H, W, C = a.shape
+    ws = int(lib.inf_ssim_workspace_bytes(H, W, C))
+    if ws < 0:
+        raise ValueError("ssim needs images of at least 7 x 7 with 1..4 channels")
+    work = torch.empty(max(ws, 8), dtype=torch.uint8, device=a.device)
+    out = torch.empty(C, dtype=torch.float64, device=a.device)
+    check(lib.inf_ssim(ptr(a), ptr(b), H, W, C, float(data_range), ptr(work), ptr(out), stream_handle()), "ssim")
+    return float(out.mean().item())
+
+
+def masked_sse(fake: torch.Tensor, real: torch.Tensor, mask: torch.Tensor | None = None):
+    """(sum of squared differences over the masked pixels, pixel count) of [.., C] images."""
+    require_hip(fake, real, mask)
+    a = fake.to(torch.float32).contiguous()
+    b = real.to(torch.float32).contiguous()
+    C = a.shape[-1]
+    n = a.numel() // C
+    m = None
+    if mask is not None:
+        if mask.numel() != n:
+            raise ValueError("mask must have one entry per pixel")
+        m = mask.reshape(-1).to(torch.uint8).contiguous()
+    work = torch.empty(int(lib.inf_masked_sse_workspace_bytes()), dtype=torch.uint8, device=a.device)
+    out = torch.empty(2, dtype=torch.float64, device=a.device)
+    check(lib.inf_masked_sse(ptr(a), ptr(b), ptr(m), n, C, ptr(work), ptr(out), stream_handle()), "masked_sse")
+    s, c = out.tolist()
+    return s, int(c)
+
+
 def pack_table(E: torch.Tensor, k_pad: int, dtype: torch.dtype) -> torch.Tensor:
     """Device copy of the V x k table with zero columns up to k_pad (the GEMM tile),
     in the GEMM dtype (mesh.py:53-108 produces E; this is the upload of it)."""

@@ -248,6 +248,37 @@ def psnr(fake, real, obj_mask_1d=None):
     return 20 * np.log10(1.0 / np.sqrt(mse))
 
 
+def structural_similarity(a: np.ndarray, b: np.ndarray, data_range: float = 2.0, win_size: int = 7) -> float:
+    """evaluation_metrics.py:33 calls skimage.metrics.structural_similarity(fake, real,
+    multichannel=True) with the defaults: per channel, uniform win_size^2 window
+    (scipy.ndimage.uniform_filter), K1 = 0.01, K2 = 0.03, sample covariance
+    NP / (NP - 1), data_range = the dtype range of the input (2 for float images), S
+    averaged over the image cropped by (win_size - 1) // 2; channels averaged.
+    scikit-image is not installed here: PARITY UNPINNED beyond known-answer checks."""
+    from scipy.ndimage import uniform_filter
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape and a.ndim == 3
+    NP = win_size ** 2
+    cov_norm = NP / (NP - 1)
+    C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+    pad = (win_size - 1) // 2
+    out = []
+    for c in range(a.shape[2]):
+        x, y = a[..., c], b[..., c]
+        ux, uy = uniform_filter(x, win_size), uniform_filter(y, win_size)
+        uxx, uyy, uxy = uniform_filter(x * x, win_size), uniform_filter(y * y, win_size), uniform_filter(x * y, win_size)
+        vx, vy, vxy = cov_norm * (uxx - ux * ux), cov_norm * (uyy - uy * uy), cov_norm * (uxy - ux * uy)
+        S = ((2 * ux * uy + C1) * (2 * vxy + C2)) / ((ux ** 2 + uy ** 2 + C1) * (vx + vy + C2))
+        out.append(S[pad:S.shape[0] - pad, pad:S.shape[1] - pad].mean())
+    return float(np.mean(out))
+
+
+def dssim(fake, real, data_range: float = 2.0) -> float:
+    """evaluation_metrics.py:29-34: (1 - SSIM) / 2."""
+    return (1 - structural_similarity(fake, real, data_range)) / 2
+
+
 def epoch_psnr(epoch_mse):
     """evaluation_metrics.py:25-26 (callers divide summed sq. error by rays, trainer.py:263)."""
     return -10 * np.log10(epoch_mse)

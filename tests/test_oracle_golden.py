@@ -165,3 +165,33 @@ def test_ff_encoder():
     np.testing.assert_array_equal(O.ff_bands(6, max_freq=3.0), d["bands_lin6"])
     np.testing.assert_allclose(O.ff_encode(d["x"], d["bands_log5"], True), d["log5"], atol=2e-5)
     np.testing.assert_allclose(O.ff_encode(d["x"], d["bands_lin6"], False), d["lin6"], atol=2e-5)
+
+
+def test_ssim_oracle_known_answers():
+    """skimage structural_similarity restated (PARITY UNPINNED: scikit-image absent):
+    identity, constant images (closed form), symmetry and a brute-force window loop."""
+    rng = np.random.default_rng(0)
+    a = rng.random((20, 24, 3)).astype(np.float32)
+    b = np.clip(a + 0.1 * rng.standard_normal(a.shape), 0, 1).astype(np.float32)
+    assert O.structural_similarity(a, a) == pytest.approx(1.0, abs=1e-12)
+    assert O.dssim(a, a) == pytest.approx(0.0, abs=1e-12)
+    c1, c2, C1 = 0.3, 0.7, 0.02 ** 2
+    A, B = np.full((10, 10, 3), c1), np.full((10, 10, 3), c2)
+    assert O.structural_similarity(A, B) == pytest.approx((2 * c1 * c2 + C1) / (c1 * c1 + c2 * c2 + C1), abs=1e-12)
+    assert O.structural_similarity(a, b) == pytest.approx(O.structural_similarity(b, a), abs=1e-12)
+    # brute force: every interior 7 x 7 window, sample covariance
+    x, y = a.astype(np.float64), b.astype(np.float64)
+    H, W, _ = x.shape
+    tot = []
+    for c in range(3):
+        acc = []
+        for i in range(H - 6):
+            for j in range(W - 6):
+                wx, wy = x[i:i + 7, j:j + 7, c].ravel(), y[i:i + 7, j:j + 7, c].ravel()
+                ux, uy = wx.mean(), wy.mean()
+                vx, vy = wx.var(ddof=1), wy.var(ddof=1)
+                vxy = ((wx - ux) * (wy - uy)).sum() / 48
+                acc.append((2 * ux * uy + 0.02 ** 2) * (2 * vxy + 0.06 ** 2) /
+                           ((ux ** 2 + uy ** 2 + 0.02 ** 2) * (vx + vy + 0.06 ** 2)))
+        tot.append(np.mean(acc))
+    assert O.structural_similarity(a, b) == pytest.approx(np.mean(tot), abs=1e-10)
