@@ -285,6 +285,24 @@ int inf_raycast_rays(const inf_bvh* bvh, const float* origins, const float* dirs
 int inf_compact_hits(const inf_bvh* bvh, const int32_t* hit_face, const float* bary, int64_t num_rays,
                      int32_t* scratch, int64_t* num_hits, int64_t* out_vids, float* out_bary, int64_t* out_ray,
                      int64_t* out_face, inf_stream_t stream);
+/* The same compaction against an explicit face table faces [F][3] int32 (the vertex ids
+ * written to out_vids; texture baking maps UV-mesh faces to eigenfunction-mesh ids). */
+int inf_compact_faces(const int32_t* faces, const int32_t* hit_face, const float* bary, int64_t num_rays,
+                      int32_t* scratch, int64_t* num_hits, int64_t* out_vids, float* out_bary, int64_t* out_ray,
+                      int64_t* out_face, inf_stream_t stream);
+
+/* ---- texture baking (bake_texture_field.py:96-264,334-420) ------------------------ */
+/* Texel -> UV triangle search and barycentrics.  uv_px [Nv][2] f64: texel coordinates
+ * ((W-1) u, (H-1)(1-v)); faces [F][3] int32 into uv_px.  A texel (x, y) takes the
+ * triangle of UV area >= min_area that strictly contains it (point_in_tri_matched :66-93)
+ * with the nearest centroid (get_tris_fast :134-161); texel_face [H*W] int32 (-1 none),
+ * texel_bary [H*W][3] f32 by bary_matched (:196-228).  keys: device u64 [H*W] scratch. */
+int inf_uv_raster(const double* uv_px, int64_t num_uv_vertices, const int32_t* faces, int64_t num_faces, int height,
+                  int width, double min_area, uint64_t* keys, int32_t* texel_face, float* texel_bary,
+                  inf_stream_t stream);
+/* uv_fill_holes (:245-264) of an fp32 [H][W][3] texture, then (255 * CC).astype(uint8)
+ * into out_u8 and/or the filled fp32 texture into out_f. */
+int inf_uv_fill_holes(const float* img, int height, int width, uint8_t* out_u8, float* out_f, inf_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -482,7 +482,15 @@ int inf_raycast_rays(const inf_bvh* bvh, const float* origins, const float* dirs
 int inf_compact_hits(const inf_bvh* bvh, const int32_t* hit_face, const float* bary, int64_t num_rays,
                      int32_t* scratch, int64_t* num_hits, int64_t* out_vids, float* out_bary, int64_t* out_ray,
                      int64_t* out_face, inf_stream_t stream) {
-  INF_CHECK_ARG(bvh != nullptr && num_hits != nullptr && num_rays >= 0, "compact_hits: arguments");
+  INF_CHECK_ARG(bvh != nullptr, "compact_hits: null bvh");
+  return inf_compact_faces(bvh->faces, hit_face, bary, num_rays, scratch, num_hits, out_vids, out_bary, out_ray,
+                           out_face, stream);
+}
+
+int inf_compact_faces(const int32_t* faces, const int32_t* hit_face, const float* bary, int64_t num_rays,
+                      int32_t* scratch, int64_t* num_hits, int64_t* out_vids, float* out_bary, int64_t* out_ray,
+                      int64_t* out_face, inf_stream_t stream) {
+  INF_CHECK_ARG(faces != nullptr && num_hits != nullptr && num_rays >= 0, "compact_hits: arguments");
   hipStream_t st = (hipStream_t)stream;
   if (num_rays == 0) {
     INF_HIP_TRY(hipMemsetAsync(num_hits, 0, sizeof(int64_t), st));
@@ -496,7 +504,7 @@ int inf_compact_hits(const inf_bvh* bvh, const int32_t* hit_face, const float* b
   INF_LAUNCH_CHECK();
   hit_scan_kernel<<<1, 1024, 0, st>>>(scratch, (int)nb, num_hits);
   INF_LAUNCH_CHECK();
-  hit_scatter_kernel<<<dim3((unsigned)nb), dim3(CP_THREADS), 0, st>>>(hit_face, bary, num_rays, scratch, bvh->faces,
+  hit_scatter_kernel<<<dim3((unsigned)nb), dim3(CP_THREADS), 0, st>>>(hit_face, bary, num_rays, scratch, faces,
                                                                        out_vids, out_bary, out_ray, out_face);
   INF_LAUNCH_CHECK();
   return INF_OK;

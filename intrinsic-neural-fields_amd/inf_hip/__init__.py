@@ -69,6 +69,11 @@ _SIGNATURES = {
     "inf_ssim_workspace_bytes": (c_int64, [c_int, c_int, c_int]),
     "inf_ssim": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_void_p, c_void_p]),
     "inf_masked_sse_workspace_bytes": (c_int64, []),
+    "inf_compact_faces": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
+    "inf_uv_raster": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, ctypes.c_double, c_void_p, c_void_p,
+                              c_void_p, c_void_p]),
+    "inf_uv_fill_holes": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "inf_masked_sse": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "inf_plan_create": (c_int, [ctypes.POINTER(MlpDesc), c_int, ctypes.POINTER(c_void_p)]),
     "inf_plan_destroy": (None, [c_void_p]),

@@ -156,6 +156,53 @@ def masked_sse(fake: torch.Tensor, real: torch.Tensor, mask: torch.Tensor | None
     return s, int(c)
 
 
+def uv_raster(uv_px: torch.Tensor, faces: torch.Tensor, H: int, W: int, min_area: float = 1e-4):
+    """Texel -> UV triangle + barycentrics (csrc/bake.hip): (texel_face [H*W] int32, -1 =
+    none; texel_bary [H*W, 3] f32).  uv_px [Nv, 2] f64 texel coordinates, faces [F, 3]."""
+    require_hip(uv_px, faces)
+    uv = uv_px.to(torch.float64).contiguous()
+    f = faces.to(torch.int32).contiguous()
+    dev = uv.device
+    keys = torch.empty(H * W, dtype=torch.int64, device=dev)
+    tf = torch.empty(H * W, dtype=torch.int32, device=dev)
+    tb = torch.empty((H * W, 3), dtype=torch.float32, device=dev)
+    check(lib.inf_uv_raster(ptr(uv), uv.shape[0], ptr(f), f.shape[0], int(H), int(W), float(min_area), ptr(keys),
+                            ptr(tf), ptr(tb), stream_handle()), "uv_raster")
+    return tf, tb
+
+
+def compact_faces(faces: torch.Tensor, face: torch.Tensor, bary: torch.Tensor):
+    """Hit lists (vids [M, 3] int64 from `faces`, bary [M, 3], index [M], face [M]) of the
+    entries with face >= 0, in order."""
+    require_hip(faces, face, bary)
+    fa = faces.to(torch.int32).contiguous()
+    n = face.shape[0]
+    dev = face.device
+    scratch = torch.empty(max((n + 255) // 256, 1), dtype=torch.int32, device=dev)
+    count = torch.zeros(1, dtype=torch.int64, device=dev)
+    vids = torch.empty((n, 3), dtype=torch.int64, device=dev)
+    ob = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    idx = torch.empty(n, dtype=torch.int64, device=dev)
+    fc = torch.empty(n, dtype=torch.int64, device=dev)
+    check(lib.inf_compact_faces(ptr(fa), ptr(face), ptr(bary.contiguous()), n, ptr(scratch), ptr(count), ptr(vids),
+                                ptr(ob), ptr(idx), ptr(fc), stream_handle()), "compact_faces")
+    m = int(count.item())
+    return vids[:m], ob[:m], idx[:m], fc[:m]
+
+
+def uv_fill_holes(img: torch.Tensor):
+    """uv_fill_holes + 8-bit quantisation of an [H, W, 3] texture: (uint8, filled f32)."""
+    require_hip(img)
+    a = img.to(torch.float32).contiguous()
+    H, W, C = a.shape
+    if C != 3:
+        raise ValueError("texture must be [H, W, 3]")
+    u8 = torch.empty((H, W, 3), dtype=torch.uint8, device=a.device)
+    f = torch.empty((H, W, 3), dtype=torch.float32, device=a.device)
+    check(lib.inf_uv_fill_holes(ptr(a), H, W, ptr(u8), ptr(f), stream_handle()), "uv_fill_holes")
+    return u8, f
+
+
 def pack_table(E: torch.Tensor, k_pad: int, dtype: torch.dtype) -> torch.Tensor:
     """Device copy of the V x k table with zero columns up to k_pad (the GEMM tile),
     in the GEMM dtype (mesh.py:53-108 produces E; this is the upload of it)."""

@@ -83,3 +83,36 @@ def test_mesh_readers_obj_ply(tmp_path):
     m2 = MS.load_mesh(str(ply))
     np.testing.assert_allclose(m2.vertices, V.astype(np.float32))
     np.testing.assert_array_equal(m2.faces, F)
+
+
+def test_bake_oracle_known_answers():
+    """Texel search (strict interior: edge texels match nothing, as the reference's sign
+    test), bary_matched reconstruction and hole filling on hand-checkable cases."""
+    from oracle import bake_oracle as B
+    uv = np.array([[0.0, 0.0], [4.0, 0.0], [0.0, 4.0], [4.0, 4.0]])
+    faces = np.array([[0, 1, 2], [1, 3, 2]])
+    face, bary = B.texel_faces(uv, faces, 5, 5)
+    f = face.reshape(5, 5)
+    assert f[1, 1] == 0 and f[3, 3] == 1 and f[0, 0] == -1 and f[2, 2] == -1  # (2,2) lies on the diagonal
+    hit = face >= 0
+    P = np.stack(np.meshgrid(np.arange(5), np.arange(5)), -1).reshape(-1, 2)[hit]
+    rec = (bary[hit][:, :, None] * uv[faces[face[hit]]]).sum(1)
+    np.testing.assert_allclose(rec, P, atol=1e-12)
+    CC = np.zeros((5, 5, 3))
+    CC[2, 2] = [0.5, 0.25, 1.0]
+    out = B.uv_fill_holes(CC)
+    np.testing.assert_allclose(out[2, 3], [0.5, 0.25, 1.0])  # one filled neighbour: its colour
+    assert (out[0, 0] == 0.5 * np.array([1, 0.5, 2])).all()  # within the 5 x 5 reach
+    np.testing.assert_array_equal(out[2, 2], CC[2, 2])
+
+
+def test_uv_mesh_loader(tmp_path):
+    import bake_texture_field as BK
+    from oracle import bake_oracle as B
+    text, P, F = B.grid_uv_scene(4)
+    p = tmp_path / "grid.obj"
+    p.write_text(text)
+    m = BK.load_uv_mesh(str(p))
+    assert m.faces.shape == F.shape and m.vertices.shape[0] == 4 * 16  # every cell its own 4 corners
+    idx = BK.correspondences(m, np.round(P, 9))
+    np.testing.assert_array_equal(idx[m.faces], F)
