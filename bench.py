@@ -307,6 +307,61 @@ def render_e2e_bench(args, device):
             "bvh_build_s": build_s, "timing": "host wall clock per Renderer.render call (incl. the hit-count readback)"}
 
 
+def rff_bench(args, device, B=4096, reps=6):
+    """Secondary line: the extrinsic RFF configuration (configs tf_rff_*: k = 510 RFF
+    features -> in_dim 1023, 6 x 128 MLP, skip 3, L1, Adam), fused gather + encode + step,
+    graph-replayed like the headline.  Synthetic V x 3 positions in [-1, 1]^3."""
+    import model as M
+    from inf_hip import runtime
+    torch.manual_seed(0)
+    m = M.make_model({"feature_strategy": "rff", "k": 510, "embed_std": 8, "num_layers": 6, "mlp_hidden_dim": 128,
+                      "skip_layer_idx": 3, "kernels": {"mode": args.mode}}).to(device)
+    m.kernel_mode = args.mode
+    rt = m.hip_runtime()
+    rt.ensure_optimizer_arenas()
+    plan = runtime.Plan(m.in_dim, 128, 6, 3, args.mode, "L1", B, rt.arena, rt.grads, rt.exp_avg, rt.exp_avg_sq)
+    plan.encoding = m._encoding()
+    plan.set_lr(1e-4)
+    G = 8
+    nb = 4 * G
+    N = nb * B
+    g = torch.Generator(device="cpu").manual_seed(3)
+    P = (torch.rand((args.verts, 3), generator=g) * 2 - 1).to(device)
+    vids = torch.randint(0, args.verts, (N, 3), generator=g).to(device)
+    bary = -torch.log(torch.rand((N, 3), generator=g).clamp_min(1e-12))
+    bary = (bary / bary.sum(1, keepdim=True)).to(device)
+    rgb = torch.rand((N, 3), generator=g).to(device)
+    src = runtime.RaySource(P, vids, bary, rgb)
+    perm = torch.randperm(N, device=device)
+    b = plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B, offset_from_ctrl=True, loss="L1")
+    plan.set_batch_index(0)
+    plan.train_step(b, None, apply_adam=True, advance=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gm = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gm, stream=s):
+            for _ in range(G):
+                plan.train_step(b, None, apply_adam=True, advance=True)
+    torch.cuda.current_stream().wait_stream(s)
+    plan.set_batch_index(0)
+    for _ in range(2):
+        gm.replay()
+    plan.set_batch_index(0)
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for i in range(reps):
+        if (i * G) % nb == 0:
+            plan.set_batch_index(0)
+        gm.replay()
+    t1.record()
+    torch.cuda.synchronize()
+    ms = t0.elapsed_time(t1) / (reps * G)
+    return {"config": "tf_rff: rff k=510 (in_dim 1023), 6x128 skip 3, L1, Adam", "rays_per_step": B,
+            "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s"}
+
+
 def cpu_baseline(args):
     """The CPU oracle (numpy fp32 restatement of the reference step, oracle/inf_oracle.py)
     on this host's cores, config B at batch 4096: bounded sample of ~cpu_seconds."""
@@ -401,12 +456,13 @@ def main():
                           "dw_gemm_tflops": d_fl / (d_ms * 1e-3) / 1e12}
         tr = tr2
 
-    render = None
+    render = extrinsic = None
     if not args.no_render and rank == 0:
         del tr
         torch.cuda.empty_cache()
         render = render_bench(args, device)
         render["end_to_end"] = render_e2e_bench(args, device)
+        extrinsic = rff_bench(args, device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -445,6 +501,7 @@ def main():
             "host_wall_ms_per_step": wall_ms,
             "large_batch": extra,
             "render": render,
+            "extrinsic_rff": extrinsic,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

@@ -263,6 +263,28 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       rbary[rl * 3 + i] = w;
       rvid[BM * 4 + tid] = ok;
     }
+    // extrinsic front-end: thread (ray, coordinate c) forms x_c of its ray (the gather's
+    // fma order) into activation buffer 0, unused until phase 1; [BM][4] = x, live
+    if (a.encoding != INF_ENC_NONE && tid < BM * 3) {
+      float* rx = reinterpret_cast<float*>(act);
+      int64_t offset = a.idx_offset;
+      if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
+      const int rl = tid / 3, c = tid % 3;
+      const int b = b0 + rl;
+      float x = 0.f;
+      const bool live = b < a.batch && ray_in_range(offset, b, a.num_rays);
+      if (live) {
+        const int64_t rr = ray_row(a.ray_idx, a.idx_dtype, offset, b);
+        const int64_t v0 = vid_at(a.vids, a.vid_dtype, 3 * rr), v1 = vid_at(a.vids, a.vid_dtype, 3 * rr + 1),
+                      v2 = vid_at(a.vids, a.vid_dtype, 3 * rr + 2);
+        const float w0 = a.bary[3 * rr], w1 = a.bary[3 * rr + 1], w2 = a.bary[3 * rr + 2];
+        const uint64_t nv = (uint64_t)a.num_vertices;
+        if ((uint64_t)v0 < nv && (uint64_t)v1 < nv && (uint64_t)v2 < nv)
+          x = fmaf(w2, a.pos[3 * v2 + c], fmaf(w1, a.pos[3 * v1 + c], w0 * a.pos[3 * v0 + c]));
+      }
+      rx[rl * 4 + c] = x;
+      if (c == 0) rx[rl * 4 + 3] = live ? 1.f : 0.f;
+    }
     // the first block's fragments, in k order (the loop's waits assume that order); issued
     // after the dependent ray-record loads so those are not queued behind them
     {
@@ -280,6 +302,61 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // ---- gather: the feature tile, 16-byte chunks (8 columns) per thread ---------------
     // fp32 FMA in the reference order b0 e0 + b1 e1 + b2 e2, rounded to bf16 once (the
     // gather kernel's numerics); every load of a round is issued before any use
+    if (a.encoding != INF_ENC_NONE) {
+      // extrinsic front-end: RFF / FF / xyz columns of the rays' positions x (LDS, above),
+      // bitwise gather.hip encode_kernel's values, rounded to bf16.  A thread keeps one
+      // 8-column chunk (ch = tid % cpr when cpr divides the thread count) across its rays,
+      // so its projection coefficients are loaded once.
+      const float* rx = reinterpret_cast<const float*>(act);
+      const int cpr = k_pad >> 3;
+      const int nch = BM * cpr;
+      const int ne = a.enc_ne, ek = a.enc_k;
+      const bool rff = a.encoding == INF_ENC_RFF;
+      const int ch0 = tid % cpr;
+      float pc[8][3];
+      auto coef = [&](int ch, float (&pcv)[8][3]) {
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) {
+          const int c = ch * 8 + e8;
+          const int j = c < ne ? c : c - ne;
+          const bool t = c < 2 * ne;
+          pcv[e8][0] = t ? (rff ? a.enc_proj[j] : a.enc_proj[j % ek]) : 0.f;
+          pcv[e8][1] = t && rff ? a.enc_proj[ek + j] : 0.f;
+          pcv[e8][2] = t && rff ? a.enc_proj[2 * ek + j] : 0.f;
+        }
+      };
+      coef(ch0, pc);
+#pragma unroll 1
+      for (int q = tid; q < nch; q += C3_CT) {
+        const int r = q / cpr, ch = q % cpr;
+        float pq[8][3];
+        if (ch != ch0) coef(ch, pq);
+        const float x[3] = {rx[r * 4], rx[r * 4 + 1], rx[r * 4 + 2]};
+        const bool live = rx[r * 4 + 3] != 0.f;
+        const float tp = 6.283185307179586f;
+        const float px[3] = {tp * x[0], tp * x[1], tp * x[2]};
+        u16x8 o;
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) {
+          const int c = ch * 8 + e8;
+          const float p0 = ch == ch0 ? pc[e8][0] : pq[e8][0];
+          const float p1 = ch == ch0 ? pc[e8][1] : pq[e8][1];
+          const float p2 = ch == ch0 ? pc[e8][2] : pq[e8][2];
+          float v = 0.f;
+          if (c < 2 * ne) {
+            const int j = c < ne ? c : c - ne;
+            const float e = rff ? fmaf(px[2], p2, fmaf(px[1], p1, px[0] * p0)) : pick3(x, j / ek) * p0;
+            float sn, cs;
+            fast_sincos(e, &sn, &cs);
+            v = c < ne ? cs : sn;
+          } else if (c < a.enc_in_dim) {
+            v = pick3(x, c - 2 * ne);
+          }
+          o[e8] = bf_bits3(live ? v : 0.f);
+        }
+        *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
+      }
+    } else
     {
       const int cpr = k_pad >> 3;          // chunks per row
       const int nch = BM * cpr;            // chunks of the tile
@@ -743,8 +820,11 @@ int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream) {
   INF_CHECK_ARG(a.rows % bm == 0 && a.rows >= bm, "chain3: rows must be a multiple of the tile height");
   INF_CHECK_ARG(a.nphase == 2 * a.L - 3, "chain3: phases");
   INF_CHECK_ARG(a.nblk >= 1 && a.nblk <= C3_MAX_BLOCKS, "chain3: weight-stream blocks");
-  INF_CHECK_ARG(a.rgb != nullptr && a.table != nullptr && a.vids != nullptr && a.bary != nullptr && a.XT != nullptr,
+  INF_CHECK_ARG(a.rgb != nullptr && (a.encoding != INF_ENC_NONE ? a.pos != nullptr : a.table != nullptr) &&
+                    a.vids != nullptr && a.bary != nullptr && a.XT != nullptr,
                 "chain3: inputs");
+  INF_CHECK_ARG(a.encoding == INF_ENC_NONE || a.encoding == INF_ENC_XYZ || a.enc_proj != nullptr,
+                "chain3: encoding projection missing");
   INF_CHECK_ARG(a.vid_dtype == INF_DTYPE_I32 || a.vid_dtype == INF_DTYPE_I64, "chain3: vertex id dtype");
   INF_CHECK_ARG(a.num_vertices * (int64_t)a.k_pad * 2 < (int64_t)1 << 31, "chain3: table exceeds 2 GiB");
   for (int i = 0; i < a.nblk; ++i) INF_CHECK_ARG(a.blk[i].img != nullptr, "chain3: weight image missing");

@@ -38,6 +38,11 @@ struct Chain3Args {
   int64_t idx_offset;
   int64_t num_rays;  // bound on idx_offset + b (0 = unchecked)
   int32_t offset_from_ctrl;
+  // extrinsic front-end (INF_ENC_*, model.py:33-40): the feature tile is the encoding of
+  // the rays' interpolated positions pos[V][3] (gather.hip encode_kernel's numerics)
+  int32_t encoding, enc_k, enc_ne, enc_in_dim;
+  const float* enc_proj;
+  const float* pos;
   // weight stream: phases 0..L-2 forward layer p, L-1.. dX of layer (L-2) - (p - (L-1))
   C3Block blk[C3_MAX_BLOCKS];
   int32_t nblk, nphase;

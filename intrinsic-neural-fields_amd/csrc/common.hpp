@@ -72,6 +72,31 @@ __device__ __forceinline__ int64_t vid_at(const void* vids, int vid_dtype, int64
   return reinterpret_cast<const int32_t*>(vids)[i];
 }
 
+// ---- encoders (gather.hip, chain3.hip) --------------------------------------------
+__device__ __forceinline__ float pick3(const float (&x)[3], int i) { return i == 0 ? x[0] : (i == 1 ? x[1] : x[2]); }
+
+// sin and cos of e: three-constant Cody-Waite reduction by pi/2, minimax polynomials on
+// [-pi/4, pi/4] (<= 1e-7 abs for |e| < 2^15); larger arguments take ocml's sincosf.
+__device__ __forceinline__ void fast_sincos(float e, float* s, float* c) {
+  if (!(fabsf(e) < 32768.f)) {
+    sincosf(e, s, c);
+    return;
+  }
+  const float n = rintf(e * 0.636619772367581343f);
+  float r = fmaf(-n, 1.5703125f, e);  // pi/2 split: 1.5703125 + 4.837512969970703125e-4 + ...
+  r = fmaf(-n, 4.837512969970703125e-4f, r);
+  r = fmaf(-n, 7.54978995489188216e-8f, r);
+  const float r2 = r * r;
+  const float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f), r2 * r, r);
+  const float cp = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2,
+                                   4.166664568298827e-2f), r2, -0.5f), r2, 1.0f);
+  const int q = (int)n & 3;
+  const float ss = (q & 1) ? cp : sp;
+  const float cc = (q & 1) ? sp : cp;
+  *s = (q & 2) ? -ss : ss;
+  *c = ((q + 1) & 2) ? -cc : cc;
+}
+
 // ---- kernel launch wrappers (defined in the .hip files) --------------------------
 int encoded_dim(int enc, int k, int inc);
 int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype, const float* bary,

@@ -237,24 +237,27 @@ int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t 
 // x = sum_i bary_i * P[vid_i] over the V x 3 vertex table (ray_dataloader.py:134-136),
 // then RandomFourierFeatEnc / FourierFeatEnc (layers.py:6-39), written straight into the
 // plan's X / X^T tiles (or an fp32 feature matrix): the B x in_dim encoding never exists
-// as a separate tensor.  Lanes as in gather_kernel (4 lanes per ray, 16 columns each);
-// each lane recomputes its ray's x (3 x 12 B of L2-resident vertex rows) and evaluates
-// cos/sin with the precise ocml routines (the arguments reach ~1e3 rad).
+// as a separate tensor.
+//
+// Tiles and stores as in gather_kernel (64 rays x 64 columns, whole-line vector stores
+// of X and, through LDS, X^T -- scattered 2-byte stores made this kernel 8x slower).
+// Each lane recomputes its ray's x (3 x 12 B of L2-resident vertex rows); sincos uses a
+// three-constant Cody-Waite reduction by pi/2 and minimax polynomials on [-pi/4, pi/4]
+// (<= 1e-7 abs for |e| < 2^15; larger arguments take ocml's sincosf).
 namespace {
-__device__ __forceinline__ float pick3(const float (&x)[3], int i) { return i == 0 ? x[0] : (i == 1 ? x[1] : x[2]); }
-
+template <typename OutT, bool VEC>
 __global__ __launch_bounds__(GT_THREADS) void encode_kernel(
     const float* __restrict__ table, int64_t V, const void* __restrict__ vids, int vid_dtype,
     const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype, int64_t idx_offset,
     const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int batch, int enc, int ek,
-    const float* __restrict__ proj, int inc, int in_dim, float* __restrict__ outf, bf16* __restrict__ outb,
-    int64_t ld_out, int rows_out, float* __restrict__ outf_t, bf16* __restrict__ outb_t, int64_t ld_out_t) {
+    const float* __restrict__ proj, int in_dim, int ne, OutT* __restrict__ out, int64_t ld_out, int rows_out,
+    OutT* __restrict__ out_t, int64_t ld_out_t) {
   __shared__ float tile[GT_COLS][GT_ROWS + 1];
   const int t = threadIdx.x;
   const int r = t >> 2;
   const int cq = (t & 3) * 16;
   const int b = blockIdx.x * GT_ROWS + r;
-  const int64_t c0 = (int64_t)blockIdx.y * GT_COLS + cq;
+  const int c0 = (int)blockIdx.y * GT_COLS + cq;
   int64_t offset = idx_offset;
   if (ctrl_batch_index != nullptr) offset += (int64_t)(*ctrl_batch_index) * batch;
 
@@ -284,32 +287,27 @@ __global__ __launch_bounds__(GT_THREADS) void encode_kernel(
     // RFF: (2 * torch.pi * x) is an fp32 product with the fp32-rounded 2 pi
     const float tp = 6.283185307179586f;
     const float px[3] = {tp * x[0], tp * x[1], tp * x[2]};
-    const int ne = enc == INF_ENC_RFF ? ek : 3 * ek;  // embedding width before cos/sin
-#pragma unroll 4
+#pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int c = (int)c0 + i;
-      if (c >= in_dim) break;
-      float v;
-      if (enc == INF_ENC_XYZ) {
-        v = pick3(x, c);
-      } else if (c >= 2 * ne) {
-        v = pick3(x, c - 2 * ne);  // include_input tail
-      } else {
+      const int c = c0 + i;
+      float v = 0.f;
+      if (c < 2 * ne) {
         const int j = c < ne ? c : c - ne;
         float e;
         if (enc == INF_ENC_RFF)
           e = fmaf(px[2], proj[2 * ek + j], fmaf(px[1], proj[ek + j], px[0] * proj[j]));
         else
           e = pick3(x, j / ek) * proj[j % ek];
-        v = c < ne ? cosf(e) : sinf(e);
+        float sn, cs;
+        fast_sincos(e, &sn, &cs);
+        v = c < ne ? cs : sn;
+      } else if (c < in_dim) {
+        v = pick3(x, c - 2 * ne);  // the include_input tail (or the xyz strategy itself)
       }
       acc[i] = v;
     }
   }
-  if (outf != nullptr || outf_t != nullptr)
-    store_tile<float, false>(acc, tile, outf, ld_out, rows_out, outf_t, ld_out_t);
-  else
-    store_tile<bf16, false>(acc, tile, outb, ld_out, rows_out, outb_t, ld_out_t);
+  store_tile<OutT, VEC>(acc, tile, out, ld_out, rows_out, out_t, ld_out_t);
 }
 }  // namespace
 
@@ -338,12 +336,22 @@ int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype
                 "encode: ray_idx must be int32/int64");
   INF_CHECK_ARG(out_dtype == INF_DTYPE_F32 || out_dtype == INF_DTYPE_BF16, "encode: out dtype must be f32/bf16");
   if (rows_out == 0) return INF_OK;
+  const int ne = enc == INF_ENC_XYZ ? 0 : (enc == INF_ENC_RFF ? enc_k : 3 * enc_k);  // arguments per ray
   dim3 grid((unsigned)ceil_div(rows_out, GT_ROWS), (unsigned)ceil_div(ld_out, GT_COLS));
-  const bool of = out_dtype == INF_DTYPE_F32;
-  encode_kernel<<<grid, GT_THREADS, 0, stream>>>(
-      table, V, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_batch_index, num_rays, batch, enc, enc_k,
-      proj, inc, in_dim, of ? (float*)out : nullptr, of ? nullptr : (bf16*)out, ld_out, rows_out,
-      of ? (float*)out_t : nullptr, of ? nullptr : (bf16*)out_t, ld_out_t);
+  const bool vec = (ld_out % 16 == 0) && (out_t == nullptr || ld_out_t % 16 == 0) && ((uintptr_t)out % 16 == 0) &&
+                   ((uintptr_t)out_t % 16 == 0);
+#define INF_ENC_LAUNCH(T, V)                                                                                      \
+  encode_kernel<T, V><<<grid, GT_THREADS, 0, stream>>>(table, V_rows, vids, vid_dtype, bary, ray_idx, idx_dtype,   \
+                                                       idx_offset, ctrl_batch_index, num_rays, batch, enc, enc_k, \
+                                                       proj, in_dim, ne, (T*)out, ld_out, rows_out, (T*)out_t,    \
+                                                       ld_out_t)
+  const int64_t V_rows = V;
+  if (out_dtype == INF_DTYPE_F32) {
+    if (vec) INF_ENC_LAUNCH(float, true); else INF_ENC_LAUNCH(float, false);
+  } else {
+    if (vec) INF_ENC_LAUNCH(bf16, true); else INF_ENC_LAUNCH(bf16, false);
+  }
+#undef INF_ENC_LAUNCH
   INF_LAUNCH_CHECK();
   return INF_OK;
 }

@@ -684,7 +684,9 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   // the fused gather reads a device-resident bf16 table; the dW lgemm streams
   // K = Bp / dw_splits rays per block in 256-ray steps
   return use_chain(p) && chain3_supported(p->H, p->L, p->k_pad, Bp) && w1 != nullptr && w1->f_off >= 0 &&
-         w0->f_off >= 0 && b->table != nullptr && b->encoding == INF_ENC_NONE && b->table_dtype == INF_DTYPE_BF16 &&
+         w0->f_off >= 0 && b->table != nullptr &&
+         (b->encoding == INF_ENC_NONE ? b->table_dtype == INF_DTYPE_BF16
+                                      : (b->table_dtype == INF_DTYPE_F32 && b->vids != nullptr)) &&
          (Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0 && std::getenv("INF_NO_CHAIN3") == nullptr;
 }
 
@@ -703,8 +705,20 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.k_pad = p->k_pad;
   a.rows = Bp;
   a.batch = b->batch;
-  INF_CHECK_ARG(b->table != nullptr && b->table_dtype == INF_DTYPE_BF16, "chain3: bf16 table batch required");
-  a.table = reinterpret_cast<const bf16*>(b->table);
+  if (b->encoding != INF_ENC_NONE) {
+    INF_CHECK_ARG(b->table != nullptr && b->table_dtype == INF_DTYPE_F32 && b->vids != nullptr,
+                  "chain3: encoded batches need the fp32 vertex table and vertex ids");
+    a.encoding = b->encoding;
+    a.enc_k = b->enc_k;
+    a.enc_ne = b->encoding == INF_ENC_XYZ ? 0 : (b->encoding == INF_ENC_RFF ? b->enc_k : 3 * b->enc_k);
+    a.enc_in_dim = encoded_dim(b->encoding, b->enc_k, b->enc_include_input);
+    INF_CHECK_ARG(a.enc_in_dim == p->d.in_dim, "encoding width does not match the model's in_dim");
+    a.enc_proj = b->enc_proj;
+    a.pos = reinterpret_cast<const float*>(b->table);
+  } else {
+    INF_CHECK_ARG(b->table != nullptr && b->table_dtype == INF_DTYPE_BF16, "chain3: bf16 table batch required");
+    a.table = reinterpret_cast<const bf16*>(b->table);
+  }
   a.num_vertices = b->num_vertices;
   a.vids = b->vids;
   a.vid_dtype = b->vid_dtype;

@@ -149,3 +149,53 @@ def test_render_hits_extrinsic():
     exp = np.ones((64, 3), np.float32)
     exp[hit] = d["pred"][:n]
     np.testing.assert_allclose(img.reshape(64, 3), exp, atol=1e-4)
+
+
+@pytest.mark.parametrize("B", [1024, 4096])
+def test_rff_bf16_chain3_matches_layered(B, monkeypatch):
+    """tf_rff shape (k = 510 -> in_dim 1023, 6 x 128, skip 3): the fused chain3 step with
+    the encoding computed inside its gather stage vs the encode kernel + chain.hip and +
+    layered bf16 kernels: predictions within 1e-4 on >= 99.9 % of the values and 2e-3
+    everywhere (the skip layer's two K segments are summed in another order, so a bf16
+    activation can round the other way: 6.7e-4 seen on 2 of 12288 at 4096 rays), reduced
+    gradients 1e-2 of each tensor's max; all within the bf16 bars of
+    test_gpu_kernels against the fp32 oracle on the encoded features."""
+    import model as M
+    from inf_hip import runtime
+    rng = np.random.default_rng(5)
+    V = 3000
+    P = (rng.random((V, 3)) * 2 - 1).astype(np.float32)
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    src = runtime.RaySource(cu(P), cu(vids), cu(bary), cu(rgb))
+    out = {}
+    for tag in ("chain3", "chain", "layered"):
+        if tag == "chain":
+            monkeypatch.setenv("INF_NO_CHAIN3", "1")
+        if tag == "layered":
+            monkeypatch.setenv("INF_NO_CHAIN", "1")
+        torch.manual_seed(0)
+        m = M.make_model({"feature_strategy": "rff", "k": 510, "embed_std": 8, "num_layers": 6,
+                          "mlp_hidden_dim": 128, "skip_layer_idx": 3, "kernels": {"mode": "bf16"}}).cuda()
+        m.kernel_mode = "bf16"
+        rt = m.hip_runtime()
+        rt.ensure_optimizer_arenas()
+        plan = runtime.Plan(m.in_dim, 128, 6, 3, "bf16", "L1", B, rt.arena, rt.grads, rt.exp_avg, rt.exp_avg_sq)
+        plan.encoding = m._encoding()
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, batch=B, loss="L1"), pred, apply_adam=False)
+        out[tag] = (pred.cpu().numpy(), plan.grads.cpu().numpy().copy(), list(zip(plan.offsets, plan.numels)))
+        w = {n: p.detach().cpu().numpy().astype(np.float64) for n, p in m.named_parameters()}
+        Bm = m.embedding.B.cpu().numpy()
+    feats = O.rff_encode(O.interp_xyz(P.astype(np.float64), vids, bary.astype(np.float64)), Bm.astype(np.float64))
+    p_ref, _ = O.mlp_forward(w, feats, 6, 3)
+    for tag in out:
+        assert np.abs(out[tag][0] - p_ref).max() < 2e-2, tag
+    for tag in ("chain", "chain3"):
+        d = np.abs(out[tag][0] - out["layered"][0])
+        assert d.max() < 2e-3 and (d > 1e-4).mean() < 1e-3, (tag, d.max())
+        for off, n in out[tag][2]:
+            ref = out["layered"][1][off:off + n]
+            got = out[tag][1][off:off + n]
+            assert np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-12) < 1e-2, (tag, off)

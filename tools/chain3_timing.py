@@ -2,6 +2,7 @@
 wave 0 of the first and the last workgroup, plus the stage's HIP-event time.
 
     python tools/chain3_timing.py [batch] [k] [hidden] [layers] [skip]
+    C3T_RFF=1: the input is the RFF encoding (k = 2 * k_rff + 3) of interpolated positions
 """
 import ctypes
 import os
@@ -22,7 +23,13 @@ params = torch.from_numpy((rng.standard_normal(P) * 0.03).astype(np.float32)).cu
 plan = runtime.Plan(k, H, L, s, "bf16", "L2", B, params, grads=torch.zeros_like(params),
                     exp_avg=torch.zeros_like(params), exp_avg_sq=torch.zeros_like(params))
 V, N = 50000, B
-E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32)).cuda()
+if os.environ.get("C3T_RFF"):
+    ek = (k - 3) // 2
+    Bm = torch.from_numpy((rng.standard_normal((3, ek)) * 8).astype(np.float32)).cuda()
+    plan.encoding = runtime.Encoding("rff", ek, Bm, True)
+    E = torch.from_numpy((rng.random((V, 3)) * 2 - 1).astype(np.float32)).cuda()
+else:
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32)).cuda()
 src = runtime.RaySource(E, torch.from_numpy(rng.integers(0, V, (N, 3))).cuda(),
                         torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32)).cuda(),
                         torch.from_numpy(rng.random((N, 3)).astype(np.float32)).cuda())
