@@ -53,6 +53,31 @@ def allreduce_scalars(values, device) -> list:
     return [float(x) for x in t.cpu()]
 
 
+def render_distributed(renderer, camCv2world, K, obj_mask_1d=None, group=None):
+    """One frame rendered by all ranks (SURVEY.md §8(e) render row; renderer.py:64-146):
+    rank r casts and shades only the pixel rows shard_span(H, r, world) -- its own rays,
+    hits and MLP rows, no exchange on the data path -- then the row slices are assembled
+    by one all_gather of equal-height (padded) slices.  Returns the H x W x 3 image as a
+    tensor on the renderer's device, identical on every rank."""
+    H, W = renderer.H, renderer.W
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    lo, hi = shard_span(H, rank, world)
+    mask = torch.zeros(H * W, dtype=torch.bool)
+    mask[lo * W:hi * W] = True
+    if obj_mask_1d is not None:
+        mask &= torch.as_tensor(obj_mask_1d).reshape(-1).bool().cpu()
+    img = renderer.render_device(camCv2world, K, obj_mask_1d=mask)  # H x W x 3, rows lo..hi shaded
+    if world == 1:
+        return img
+    rows = math.ceil(H / world)
+    part = torch.empty((rows, W, 3), dtype=img.dtype, device=img.device)
+    part[:hi - lo] = img[lo:hi]
+    parts = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(parts, part, group=group)
+    return torch.cat([parts[r][:shard_span(H, r, world)[1] - shard_span(H, r, world)[0]] for r in range(world)])
+
+
 class DataParallelTrainer:
     """Fused training epochs of one TextureField replica (see module docstring)."""
 

@@ -139,6 +139,17 @@ class Renderer:
     def render(self, camCv2world, K, obj_mask_1d=None, eval_render=False, distortion_coeffs=None,
                distortion_type=None):
         """Reference renderer.py:64-146: camera rays cast on the device (or `self.ray_tracer`)."""
+        img, hit_ray_idxs = self._render(camCv2world, K, obj_mask_1d, distortion_coeffs, distortion_type)
+        if eval_render:
+            return _to_host(img), hit_ray_idxs
+        return _to_host(img).numpy()
+
+    @torch.no_grad()
+    def render_device(self, camCv2world, K, obj_mask_1d=None):
+        """render() without the host read-back: the H x W x 3 image on the device."""
+        return self._render(camCv2world, K, obj_mask_1d, None, None)[0]
+
+    def _render(self, camCv2world, K, obj_mask_1d, distortion_coeffs, distortion_type):
         if self.ray_tracer is not None:
             vids, bary, hit_ray_idxs = self.ray_tracer(camCv2world, K, obj_mask_1d=obj_mask_1d, H=self.H, W=self.W,
                                                        distortion_coeffs=distortion_coeffs,
@@ -152,6 +163,4 @@ class Renderer:
         else:
             raise ValueError("Renderer.render needs a mesh (or a ray_tracer); render_hits takes precomputed hits")
         img = self.render_hits(vids, bary, hit_ray_idxs, obj_mask_1d, return_tensor=True)
-        if eval_render:
-            return _to_host(img), hit_ray_idxs
-        return _to_host(img).numpy()
+        return img, hit_ray_idxs

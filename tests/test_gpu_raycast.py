@@ -159,3 +159,33 @@ def test_view_preprocessor_writes_reference_format(tmp_path):
         np.testing.assert_allclose(d["unit_ray_dirs"].numpy(), np.concatenate(ref["d"]), atol=1e-6)
     else:  # a grazing ray flipped: compare the colours as multisets of the agreeing part
         assert np.isin(d["face_idxs"].numpy(), np.concatenate(ref["f"])).mean() > 0.995
+
+
+def test_row_sharded_render_assembles_to_full_frame():
+    """dp.render_distributed's per-rank work: the row shards of a frame, each cast and
+    shaded on its own (as ranks 0..2 would), assembled equal the single-rank render; at
+    world size 1 render_distributed is Renderer.render on the device."""
+    import dp
+    import mesh as MS
+    import model as M
+    from renderer import Renderer
+    V, F, cam, K = _scene()
+    H, W = 50, 64
+    rng = np.random.default_rng(8)
+    E = torch.from_numpy(rng.standard_normal((V.shape[0], 64)).astype(np.float32))
+    torch.manual_seed(0)
+    m = M.make_model({"k": 64, "num_layers": 4, "mlp_hidden_dim": 128, "skip_layer_idx": 2,
+                      "kernels": {"mode": "fp32"}}).cuda()
+    m.kernel_mode = "fp32"
+    r = Renderer(m, MS.TriMesh(V, F), eigenfunctions=E, H=H, W=W, device="cuda")
+    c, Kt = torch.from_numpy(cam).float(), torch.from_numpy(K).float()
+    full = r.render_device(c, Kt)
+    parts = []
+    for rank in range(3):
+        lo, hi = dp.shard_span(H, rank, 3)
+        mask = torch.zeros(H * W, dtype=torch.bool)
+        mask[lo * W:hi * W] = True
+        parts.append(r.render_device(c, Kt, obj_mask_1d=mask)[lo:hi])
+    torch.testing.assert_close(torch.cat(parts), full, atol=0, rtol=0)
+    torch.testing.assert_close(dp.render_distributed(r, c, Kt), full, atol=0, rtol=0)
+    np.testing.assert_array_equal(r.render(c, Kt), full.cpu().numpy())
