@@ -23,6 +23,7 @@ Fixtures:
   g8_train_curve.npz                 tiny synthetic texture-recon run     trainer.py:164-187,232-283
   g9_frontend_{rff,rffni,xyz}.npz    xyz loader + (R)FF encoder + 1 step  ray_dataloader.py:134-136, layers.py:6-39,
                                                                           model.py:33-40,98-104
+  g10_rff_curve.npz                  12-epoch synthetic run, rff strategy  trainer.py:164-187,232-283 + the above
 
 Run:  python tests/golden/make_golden.py
 """
@@ -418,6 +419,42 @@ def g9_frontends():
          lin6=enc2(x).numpy(), bands_log5=enc.freq_bands.numpy(), bands_lin6=enc2.freq_bands.numpy())
 
 
+def g10_rff_curve():
+    """G8's synthetic texture-reconstruction run with the extrinsic RFF front-end: a
+    colour field of the 3-D positions, learnt through (2 pi x) @ B features."""
+    rng = np.random.default_rng(12)
+    V = 3000
+    verts = (rng.random((V, 3)) * 2 - 1).astype(np.float32)
+    proj = rng.standard_normal((3, 3)).astype(np.float32) * 2.0
+    vert_rgb = 0.5 + 0.5 * np.sin(verts @ proj)
+    def rays(n):
+        vids, bary = synthetic_rays(rng, V, n, include_edges=False)
+        rgb = np.einsum("ni,nic->nc", bary, vert_rgb[vids]).astype(np.float32)
+        return vids, bary, rgb
+    tr_v, tr_b, tr_rgb = rays(8192)
+    va_v, va_b, va_rgb = rays(2048)
+    mcfg = {"feature_strategy": "rff", "k": 64, "embed_std": 2.0, "num_layers": 4, "mlp_hidden_dim": 64,
+            "skip_layer_idx": 2, "batchnorm": False}
+    cfg = {"model": mcfg, "training": {"lr": 1e-3, "loss_type": "L1"}}
+    torch.manual_seed(0)
+    model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+    tr = _bare_trainer(model, optim, ref_config.get_loss_fn(cfg))
+    Pt = torch.from_numpy(verts)
+    train_ld = ref_loader.RayDataLoader(Pt, "rff", torch.from_numpy(tr_v), torch.from_numpy(tr_b),
+                                        torch.from_numpy(tr_rgb), None, None, 512, False, True, device="cpu")
+    tr.val_data_loader = ref_loader.RayDataLoader(Pt, "rff", torch.from_numpy(va_v), torch.from_numpy(va_b),
+                                                  torch.from_numpy(va_rgb), None, None, 512, False, False,
+                                                  device="cpu")
+    val_psnr = []
+    for epoch in range(12):
+        for batch in train_ld:
+            tr._train_step(batch)
+        _, vp = tr.evaluate(epoch)
+        val_psnr.append(vp)
+    save("g10_rff_curve.npz", verts=verts, tr_vids=tr_v, tr_bary=tr_b, tr_rgb=tr_rgb, va_vids=va_v, va_bary=va_b,
+         va_rgb=va_rgb, val_psnr=np.array(val_psnr), lr=np.float32(1e-3), batch=np.int64(512))
+
+
 if __name__ == "__main__":
     import tempfile
     torch.set_num_threads(8)
@@ -432,3 +469,4 @@ if __name__ == "__main__":
         g7_render()
         g8_train_curve()
         g9_frontends()
+        g10_rff_curve()

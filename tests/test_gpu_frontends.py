@@ -199,3 +199,35 @@ def test_rff_bf16_chain3_matches_layered(B, monkeypatch):
             ref = out["layered"][1][off:off + n]
             got = out[tag][1][off:off + n]
             assert np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-12) < 1e-2, (tag, off)
+
+
+@pytest.mark.parametrize("mode,tol", [("fp32", 0.05), ("bf16", 0.2)])
+def test_trainer_rff_training_curve(tmp_path, mode, tol):
+    """Statistical PSNR parity of the RFF front-end: trainer.Trainer over 12 epochs of the
+    reference's own synthetic run (G10) -- loader over positions, fused gather + encode +
+    step, evaluation -- val epoch-PSNR within 0.05 dB (fp32) / 0.2 dB (bf16)."""
+    import json
+    import os
+
+    import config
+    from ray_dataloader import RayDataLoader
+    from trainer import Trainer
+    d = golden("g10_rff_curve.npz")
+    B = int(d["batch"])
+    cfg = {"seed": 0, "data": {"img_height": 8, "img_width": 8},
+           "model": {"feature_strategy": "rff", "k": 64, "embed_std": 2.0, "num_layers": 4, "mlp_hidden_dim": 64,
+                     "skip_layer_idx": 2, "kernels": {"mode": mode}},
+           "training": {"out_dir": str(tmp_path), "batch_size": B, "lr": float(d["lr"]), "loss_type": "L1",
+                        "render_every": 1000, "print_every": 1000, "epochs": 12, "checkpoint_every": 100}}
+    P = torch.from_numpy(d["verts"])
+    train = RayDataLoader(P, "rff", torch.from_numpy(d["tr_vids"]), torch.from_numpy(d["tr_bary"]),
+                          torch.from_numpy(d["tr_rgb"]), None, None, B, False, True, device="cuda")
+    val = RayDataLoader(P, "rff", torch.from_numpy(d["va_vids"]), torch.from_numpy(d["va_bary"]),
+                        torch.from_numpy(d["va_rgb"]), None, None, B, False, False, device="cuda")
+    torch.manual_seed(0)
+    model, optim = config.get_model_and_optim(cfg, None, "cuda")
+    model.kernel_mode = mode
+    Trainer(model, optim, config.get_loss_fn(cfg), None, {"train": train, "val": val}, None, cfg, "cuda").train()
+    rows = [json.loads(x) for x in open(os.path.join(tmp_path, "logs", "scalars.jsonl"))]
+    curve = [r["value"] for r in rows if r["tag"] == "Val Epoch-PSNR"]
+    np.testing.assert_allclose(curve, d["val_psnr"], atol=tol)
