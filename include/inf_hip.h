@@ -157,6 +157,28 @@ int64_t inf_masked_sse_workspace_bytes(void);
 int inf_masked_sse(const float* fake, const float* real, const uint8_t* mask, int64_t num_pixels, int channels,
                    void* workspace, double* out, inf_stream_t stream);
 
+/* ---- generic fp32 dense layers: the view-dependent texture field
+ *      (model.py:115-191 TextureFieldWithViewDependency; no config enables it) -------- */
+/* C[m][n] = act(sum_k A(m,k) B(n,k) + bias[n] + beta C[m][n]), A(m,k) = A[m sam + k sak],
+ * B(n,k) = B[n sbn + k sbk]; act 0 none, 1 ReLU, 2 sigmoid (nn.Linear + activation). */
+int inf_dense_gemm(int M, int N, int K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbn,
+                   int64_t sbk, const float* bias, int act, float beta, float* C, int64_t ldc, inf_stream_t stream);
+/* dZ = dY * act'(Y) (autograd of ReLU / Sigmoid through their outputs). */
+int inf_dense_act_bwd(int64_t n, const float* Y, const float* dY, int act, float* dZ, inf_stream_t stream);
+/* out[n] (+)= sum_m X[m ldx + n] (bias gradients). */
+int inf_colsum(int M, int N, const float* X, int64_t ldx, float* out, int accumulate, inf_stream_t stream);
+/* acos(F.cosine_similarity(-unit_dirs, face_normals[face_idxs])) (model.py:164-169). */
+int inf_view_angle(int64_t n, const float* unit_dirs, const int64_t* face_idxs, const float* face_normals,
+                   int64_t num_faces, float* out, inf_stream_t stream);
+/* FourierFeatEnc.forward (layers.py:21-25) of [n][d] inputs: [cos e | sin e | x?],
+ * e[r][c k + f] = x[r][c] bands[f]. */
+int inf_ff_encode(int64_t n, int d, const float* x, const float* bands, int k, int include_input, float* out,
+                  int64_t ld_out, inf_stream_t stream);
+/* torch.optim.Adam (config.py:108) step `step` (1-based) of one parameter tensor that is
+ * not in a plan arena: the plan update's arithmetic (adam_dev.hpp adam_elem). */
+int inf_adam_dense(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int step,
+                   float lr, float beta1, float beta2, float eps, inf_stream_t stream);
+
 /* ---- plan: one TextureField (model.py:12-112) + its training step ---------------- */
 typedef struct inf_plan inf_plan;
 

@@ -88,7 +88,8 @@ def get_model_and_optim(config, mesh, device):
     """Reference config.py:102-110 (model.to(device) before the optimizer)."""
     model = make_model(config["model"], mesh=mesh)
     model = model.to(device)
-    model.max_batch_hint = max(model.max_batch_hint, int(config.get("training", {}).get("batch_size", 0) or 0))
+    if hasattr(model, "max_batch_hint"):  # fused-plan models size their workspace for the batch
+        model.max_batch_hint = max(model.max_batch_hint, int(config.get("training", {}).get("batch_size", 0) or 0))
     optim = Adam(model.parameters(), lr=config["training"]["lr"])
     return model, optim
 

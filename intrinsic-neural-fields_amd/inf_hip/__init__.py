@@ -73,6 +73,14 @@ _SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p]),
     "inf_uv_raster": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, ctypes.c_double, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
+    "inf_dense_gemm": (c_int, [c_int, c_int, c_int, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+                               c_void_p, c_int, c_float, c_void_p, c_int64, c_void_p]),
+    "inf_dense_act_bwd": (c_int, [c_int64, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "inf_colsum": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
+    "inf_view_angle": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "inf_adam_dense": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float,
+                               c_float, c_void_p]),
+    "inf_ff_encode": (c_int, [c_int64, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p]),
     "inf_uv_fill_holes": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "inf_masked_sse": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "inf_plan_create": (c_int, [ctypes.POINTER(MlpDesc), c_int, ctypes.POINTER(c_void_p)]),

@@ -31,7 +31,9 @@ class Adam(torch.optim.Adam):
                                       "amsgrad=False, maximize=False")
 
     def _runtime_of(self, params):
-        rts = {}
+        """(runtime, params) groups of arena-bound parameters, and the free ones (layers on
+        the generic dense kernels, e.g. the view-dependent field)."""
+        rts, free = {}, []
         for p in params:
             rt = None
             for base, r in list(_model._RUNTIMES.items()):
@@ -39,10 +41,27 @@ class Adam(torch.optim.Adam):
                     rt = r
                     break
             if rt is None:
-                raise RuntimeError("HIP Adam only updates TextureField parameters bound to a HIP arena "
-                                   "(run a forward on the device first). There is no CPU fallback.")
+                if not p.is_cuda:
+                    raise RuntimeError("HIP Adam updates device parameters only. There is no CPU fallback.")
+                free.append(p)
+                continue
             rts.setdefault(id(rt), (rt, []))[1].append(p)
-        return list(rts.values())
+        return list(rts.values()), free
+
+    def _step_free(self, p, group):
+        """torch.optim.Adam's single-tensor step for one parameter outside a plan arena
+        (csrc/dense.hip inf_adam_dense, the plan update's arithmetic)."""
+        import dense
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        step = int(st["step"].item()) + 1
+        b1, b2 = group["betas"]
+        g = p.grad.to(torch.float32).contiguous()
+        dense.adam_step(p.data, g, st["exp_avg"], st["exp_avg_sq"], step, group["lr"], b1, b2, group["eps"])
+        st["step"] += 1
 
     def _bind_state(self, module, rt, group):
         """Make every parameter's exp_avg/exp_avg_sq a view into the runtime's arenas
@@ -116,7 +135,10 @@ class Adam(torch.optim.Adam):
             with_grad = [p for p in group["params"] if p.grad is not None]
             if not with_grad:
                 continue
-            for rt, ps in self._runtime_of(with_grad):
+            groups, free = self._runtime_of(with_grad)
+            for p in free:
+                self._step_free(p, group)
+            for rt, ps in groups:
                 module = rt.module_ref()
                 mparams, offs, _ = module._layout()
                 if len(ps) != len(mparams):

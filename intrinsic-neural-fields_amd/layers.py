@@ -43,7 +43,12 @@ class FourierFeatEnc(nn.Module):
         self.include_input = include_input
 
     def forward(self, x):
-        return _encode("ff", self, x)
+        if x.shape[-1] == 3:
+            return _encode("ff", self, x)
+        import dense  # view directions as angles (model.py:168): any input width
+        if not x.is_cuda:
+            raise RuntimeError("the encoders run on the HIP device only; there is no CPU fallback")
+        return dense.ff_encode(x, self.freq_bands, self.include_input)
 
 
 class RandomFourierFeatEnc(nn.Module):

@@ -113,6 +113,22 @@ class TriMesh:
     def __init__(self, vertices, faces):
         self.vertices = np.asarray(vertices, dtype=np.float64).reshape(-1, 3)
         self.faces = np.asarray(faces, dtype=np.int64).reshape(-1, 3)
+        self._face_normals = None
+
+    @property
+    def face_normals(self):
+        """trimesh.Trimesh.face_normals (make_model's view dependence, model.py:244): unit
+        (v1 - v0) x (v2 - v0) per face."""
+        if self._face_normals is None:
+            t = self.vertices[self.faces]
+            n = np.cross(t[:, 1] - t[:, 0], t[:, 2] - t[:, 0])
+            ln = np.linalg.norm(n, axis=1, keepdims=True)
+            self._face_normals = n / np.where(ln > 0, ln, 1.0)
+        return self._face_normals
+
+    @face_normals.setter
+    def face_normals(self, value):
+        self._face_normals = np.asarray(value, dtype=np.float64)
 
 
 def _read_obj(path):

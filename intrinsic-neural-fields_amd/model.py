@@ -17,6 +17,7 @@ from __future__ import annotations
 import os
 import weakref
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -74,8 +75,10 @@ class TextureField(nn.Module):
             raise NotImplementedError("batchnorm=True is not used by any intrinsic config and is not implemented")
         if activation is not nn.ReLU:
             raise NotImplementedError("only the ReLU activation is implemented")
-        if not return_rgb or out_dim != RGB_COLOR_DIM:
-            raise NotImplementedError("only the sigmoid RGB head is implemented")
+        # the fused plan serves the sigmoid RGB head; the ReLU bottleneck of the view-dependent
+        # field's spatial MLP (model.py:115-160) runs on the generic dense layers (dense.py)
+        self.return_rgb = return_rgb
+        self.dense_mode = not return_rgb or out_dim != RGB_COLOR_DIM
         self.skip_layer_idx = skip_layer_idx
         self.input_feature_embed = input_feature_embed
         # model.py:33-40: the encoder (and its RNG draw) precedes the layers
@@ -98,7 +101,7 @@ class TextureField(nn.Module):
                                                             activation=activation))
             else:
                 layers.append(nn.Sequential(nn.Linear(hidden_dim, hidden_dim), activation()))
-        layers.append(nn.Sequential(nn.Linear(hidden_dim, out_dim), nn.Sigmoid()))
+        layers.append(nn.Sequential(nn.Linear(hidden_dim, out_dim), nn.Sigmoid() if return_rgb else activation()))
         self.layers = nn.ModuleList(layers)
 
         self.kernel_mode = os.environ.get("INF_MODE", "fp32")
@@ -192,7 +195,35 @@ class TextureField(nn.Module):
             new.__dict__[k] = None if k == "_rt" else _copy.deepcopy(v, memo)
         return new
 
+    def _input_features(self, batch):
+        """model.py:98-104: the MLP input of a batch (materialised) for the dense path."""
+        if self.extrinsic:
+            x = batch["xyz"]
+            if self.input_feature_embed == "xyz":
+                return x.to(torch.float32)
+            return self.embedding(x)
+        return batch["eigenfunctions"].to(torch.float32)
+
+    def _dense_forward(self, batch):
+        import dense
+        x = self._input_features(batch)
+        if not x.is_cuda:
+            raise RuntimeError("TextureField runs on MI355X (HIP) devices only. There is no CPU fallback.")
+        h = x
+        n = len(self.layers)
+        for i, layer in enumerate(self.layers):
+            if i == self.skip_layer_idx:
+                h = dense.linear([(h, 0, 0), (x, 1, 0)], [layer.Lx.weight, layer.Ly.weight],
+                                 [layer.Lx.bias, layer.Ly.bias], "relu")
+            else:
+                lin = layer[0]
+                act = "relu" if i < n - 1 or not self.return_rgb else "sigmoid"
+                h = dense.linear([(h, 0, 0)], [lin.weight], [lin.bias], act)
+        return h
+
     def forward(self, batch):
+        if self.dense_mode:
+            return self._dense_forward(batch)
         params = list(self.parameters())
         needs = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         lazy = getattr(batch, "is_lazy_rays", None)
@@ -292,6 +323,55 @@ class _TextureFieldFn(torch.autograd.Function):
         return (None, None, None, None, None, *out)
 
 
+class TextureFieldWithViewDependency(nn.Module):
+    """Reference model.py:115-191: a TextureField with a ReLU bottleneck output, the
+    viewing direction (its angle to the hit face's normal, "intrinsic", or the direction
+    itself, "extrinsic") Fourier-encoded, and a two-layer directional MLP with a sigmoid
+    RGB head.  Same module tree and parameter order as the reference; every layer runs on
+    the generic fp32 dense kernels (dense.py / csrc/dense.hip) -- no config in configs/
+    enables view dependence, so it is off the fused hot path."""
+
+    def __init__(self, num_layers, in_dim, hidden_dim, skip_layer_idx, bottleneck_vec_dim, in_dim_view_dir,
+                 include_view_dir, view_dir_embedding_size, directional_hidden_dim, input_feature_embed=None,
+                 embed_dim=None, embed_include_input=True, embed_std=1., face_normals=None,
+                 view_dir_strategy="intrinsic", batchnorm=False, activation=nn.ReLU):
+        super().__init__()
+        self.view_dir_strategy = view_dir_strategy
+        if face_normals is not None:
+            self.register_buffer("face_normals", face_normals, persistent=False)
+        self.spatial_mlp = TextureField(num_layers, in_dim, hidden_dim, skip_layer_idx,
+                                        input_feature_embed=input_feature_embed, embed_dim=embed_dim,
+                                        embed_include_input=embed_include_input, embed_std=embed_std,
+                                        return_rgb=False, out_dim=bottleneck_vec_dim, batchnorm=batchnorm,
+                                        activation=activation)
+        self.embedding = FourierFeatEnc(view_dir_embedding_size, include_input=include_view_dir, use_logspace=True)
+        embedding_size = in_dim_view_dir * view_dir_embedding_size * 2 + (in_dim_view_dir if include_view_dir else 0)
+        self.bottleneck_vec_dim = bottleneck_vec_dim
+        self.directional_mlp = nn.Sequential(nn.Linear(bottleneck_vec_dim + embedding_size, directional_hidden_dim),
+                                             activation(), nn.Linear(directional_hidden_dim, RGB_COLOR_DIM),
+                                             nn.Sigmoid())
+
+    def _get_embedded_view_dir(self, batch):
+        """model.py:162-172."""
+        import dense
+        if self.view_dir_strategy == "intrinsic":
+            angles = dense.view_angles(batch["unit_ray_dirs"], batch["hit_face_idxs"], self.face_normals)
+            return self.embedding(angles.unsqueeze(-1))
+        if self.view_dir_strategy == "extrinsic":
+            return self.embedding(batch["unit_ray_dirs"].to(torch.float32))
+        raise RuntimeError("Unknown viewing direction strategy.")
+
+    def forward(self, batch):
+        """model.py:174-177; the concatenation is two column ranges of the first
+        directional weight."""
+        import dense
+        bottleneck = self.spatial_mlp(batch)
+        view = self._get_embedded_view_dir(batch)
+        l0, l2 = self.directional_mlp[0], self.directional_mlp[2]
+        h = dense.linear([(bottleneck, 0, 0), (view, 0, self.bottleneck_vec_dim)], [l0.weight], [l0.bias], "relu")
+        return dense.linear([(h, 0, 0)], [l2.weight], [l2.bias], "sigmoid")
+
+
 def init_weights(m):
     """Reference model.py:194-196."""
     if isinstance(m, nn.Linear):
@@ -304,8 +384,6 @@ def make_model(model_config, mesh=None):
     feature_strategy = model_config.get("feature_strategy", "efuncs")
     if model_config.get("type") == "neutex":
         raise NotImplementedError("the NeuTex baseline is outside this build's scope")
-    if view_dependence_config is not None:
-        raise NotImplementedError("view-dependent heads are outside this build's scope (no config uses them)")
     if feature_strategy == "xyz":
         in_dim = 3
     elif isinstance(model_config["k"], int):
@@ -316,12 +394,26 @@ def make_model(model_config, mesh=None):
     activation_fn = model_config.get("activation", "relu")
     if activation_fn != "relu":
         raise NotImplementedError(f"Activation function {activation_fn} not yet implemented.")
-    model = TextureField(model_config["num_layers"], in_dim, model_config["mlp_hidden_dim"],
-                         model_config["skip_layer_idx"], input_feature_embed=feature_strategy,
-                         embed_dim=model_config.get("k"),
-                         embed_include_input=model_config.get("embed_include_input", True),
-                         embed_std=model_config.get("embed_std", 1.), batchnorm=model_config.get("batchnorm", False),
-                         activation=nn.ReLU)
+    if view_dependence_config is None:
+        model = TextureField(model_config["num_layers"], in_dim, model_config["mlp_hidden_dim"],
+                             model_config["skip_layer_idx"], input_feature_embed=feature_strategy,
+                             embed_dim=model_config.get("k"),
+                             embed_include_input=model_config.get("embed_include_input", True),
+                             embed_std=model_config.get("embed_std", 1.),
+                             batchnorm=model_config.get("batchnorm", False), activation=nn.ReLU)
+    else:  # model.py:240-256
+        assert mesh is not None
+        face_normals = torch.from_numpy(np.array(mesh.face_normals, copy=True)).to(dtype=torch.float32)
+        v = view_dependence_config
+        model = TextureFieldWithViewDependency(model_config["num_layers"], in_dim, model_config["mlp_hidden_dim"],
+                                               model_config["skip_layer_idx"], v["bottleneck_vec_dim"],
+                                               v["in_dim_view_dir"], v["include_view_dir"], v["embed_size"],
+                                               v["directional_hidden_dim"], input_feature_embed=feature_strategy,
+                                               embed_dim=model_config.get("k"),
+                                               embed_include_input=model_config.get("embed_include_input", True),
+                                               embed_std=model_config.get("embed_std", 1.), face_normals=face_normals,
+                                               view_dir_strategy=v["strategy"],
+                                               batchnorm=model_config.get("batchnorm", False), activation=nn.ReLU)
     model.apply(init_weights)
     kernels = model_config.get("kernels") or {}
     model.kernel_mode = os.environ.get("INF_MODE", kernels.get("mode", "fp32"))

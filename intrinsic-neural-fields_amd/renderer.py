@@ -94,6 +94,24 @@ class Renderer:
         return self._dev_features
 
     @torch.no_grad()
+    def _render_generic(self, vids, bary, hit, face, unit_dirs, obj_mask_1d):
+        """renderer.py:86-146 for models outside the fused plan (the view-dependent field):
+        features of the hits, model(batch) over chunks (renderer.py:104-110), placement."""
+        from inf_hip import runtime
+        dev = vids.device
+        feats = runtime.gather(self._features_on_device(dev), vids.contiguous(), bary.to(torch.float32).contiguous())
+        key = "eigenfunctions" if self.feature_strategy == "efuncs" else "xyz"
+        fill = 1.0 if self.background == "white" else 0.0
+        img = torch.full((self.H * self.W, 3), fill, dtype=torch.float32, device=dev)
+        preds = [self.model({key: feats[lo:lo + RENDER_CHUNK], "unit_ray_dirs": unit_dirs[lo:lo + RENDER_CHUNK],
+                             "hit_face_idxs": face[lo:lo + RENDER_CHUNK]})
+                 for lo in range(0, feats.shape[0], RENDER_CHUNK)]
+        if preds:
+            pix = hit if obj_mask_1d is None else torch.nonzero(torch.as_tensor(obj_mask_1d).to(dev)).reshape(-1)[hit]
+            img[pix] = torch.cat(preds)
+        return img.reshape(self.H, self.W, 3)
+
+    @torch.no_grad()
     def render_hits(self, vertex_idxs_of_hit_faces, barycentric_coords, hit_ray_idxs, obj_mask_1d=None,
                     return_tensor=False):
         """Colours of precomputed hits placed into an H x W x 3 image (renderer.py:112-146)."""
@@ -150,6 +168,13 @@ class Renderer:
         return self._render(camCv2world, K, obj_mask_1d, None, None)[0]
 
     def _render(self, camCv2world, K, obj_mask_1d, distortion_coeffs, distortion_type):
+        if not hasattr(self.model, "hip_plan"):  # view-dependent field: model(batch) per chunk
+            if distortion_type is not None:
+                raise NotImplementedError("lens undistortion (mesh.py:186-193) is outside this build's scope")
+            from mesh import cast_camera_rays
+            vids, bary, hit, face, dirs = cast_camera_rays(self.ray_mesh_intersector, camCv2world, K, obj_mask_1d,
+                                                           H=self.H, W=self.W)
+            return self._render_generic(vids, bary, hit, face, dirs[hit], obj_mask_1d), hit
         if self.ray_tracer is not None:
             vids, bary, hit_ray_idxs = self.ray_tracer(camCv2world, K, obj_mask_1d=obj_mask_1d, H=self.H, W=self.W,
                                                        distortion_coeffs=distortion_coeffs,

@@ -24,6 +24,7 @@ Fixtures:
   g9_frontend_{rff,rffni,xyz}.npz    xyz loader + (R)FF encoder + 1 step  ray_dataloader.py:134-136, layers.py:6-39,
                                                                           model.py:33-40,98-104
   g10_rff_curve.npz                  12-epoch synthetic run, rff strategy  trainer.py:164-187,232-283 + the above
+  g11_viewdep_{intrinsic,extrinsic}.npz  view-dependent field fwd + 1 step model.py:115-191,240-256
 
 Run:  python tests/golden/make_golden.py
 """
@@ -455,6 +456,42 @@ def g10_rff_curve():
          va_rgb=va_rgb, val_psnr=np.array(val_psnr), lr=np.float32(1e-3), batch=np.int64(512))
 
 
+def g11_viewdep():
+    """TextureFieldWithViewDependency (model.py:115-191) built by make_model (:240-256) with
+    a stand-in mesh that only carries face_normals: seed-0 init, forward, one L1 step."""
+    rng = np.random.default_rng(13)
+    k, B, F = 64, 48, 50
+    normals = rng.standard_normal((F, 3))
+    normals /= np.linalg.norm(normals, axis=1, keepdims=True)
+    feats = (rng.standard_normal((B, k)) * 0.3).astype(np.float32)
+    dirs = rng.standard_normal((B, 3))
+    dirs = (dirs / np.linalg.norm(dirs, axis=1, keepdims=True)).astype(np.float32)
+    faces = rng.integers(0, F, B).astype(np.int64)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    mesh = types.SimpleNamespace(face_normals=normals)
+    for strategy, dview in (("intrinsic", 1), ("extrinsic", 3)):
+        mcfg = {"k": k, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2, "batchnorm": False,
+                "view_dependence": {"bottleneck_vec_dim": 16, "in_dim_view_dir": dview, "include_view_dir": True,
+                                    "embed_size": 4, "directional_hidden_dim": 32, "strategy": strategy}}
+        cfg = {"model": mcfg, "training": {"lr": 1e-3, "loss_type": "L1"}}
+        torch.manual_seed(0)
+        model, optim = ref_config.get_model_and_optim(cfg, mesh, "cpu")
+        w0 = state_dict_arrays(model, "w:")
+        batch = {"eigenfunctions": torch.from_numpy(feats), "unit_ray_dirs": torch.from_numpy(dirs),
+                 "hit_face_idxs": torch.from_numpy(faces), "expected_rgbs": torch.from_numpy(rgb)}
+        with torch.no_grad():
+            pred = model(batch).numpy()
+        m2 = copy.deepcopy(model)
+        l2 = ref_config.get_loss_fn(cfg)(m2(batch), batch["expected_rgbs"])
+        l2.backward()
+        grads = {"g:" + n: p.grad.numpy().copy() for n, p in m2.named_parameters()}
+        tr = _bare_trainer(model, optim, ref_config.get_loss_fn(cfg))
+        loss, _ = tr._train_step(batch)
+        save(f"g11_viewdep_{strategy}.npz", normals=normals.astype(np.float32), features=feats, dirs=dirs,
+             faces=faces, rgb=rgb, pred=pred, loss=np.float32(loss), **w0, **grads,
+             **state_dict_arrays(model, "w1:"))
+
+
 if __name__ == "__main__":
     import tempfile
     torch.set_num_threads(8)
@@ -470,3 +507,4 @@ if __name__ == "__main__":
         g8_train_curve()
         g9_frontends()
         g10_rff_curve()
+        g11_viewdep()

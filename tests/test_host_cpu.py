@@ -30,7 +30,7 @@ def test_make_model_rejects_out_of_scope():
     import model as M
     with pytest.raises(NotImplementedError):
         M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2, "activation": "sine"})
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(AssertionError):  # model.py:243: view dependence needs the mesh's face normals
         M.make_model({"k": 8, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2,
                       "view_dependence": {"strategy": "intrinsic"}})
     with pytest.raises(AssertionError):
@@ -147,3 +147,24 @@ def test_ff_strategy_rejected_like_reference():
     assert bool(golden("g9_ff_encoder.npz")["ff_strategy_raises"])
     with pytest.raises(AssertionError):
         M.make_model({"feature_strategy": "ff", "k": 4, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2})
+
+
+@pytest.mark.parametrize("strategy", ["intrinsic", "extrinsic"])
+def test_viewdep_model_init_matches_reference(strategy):
+    """make_model with view_dependence (model.py:240-256): the reference's module tree and
+    seed-0 weights (G11), face normals as a non-persistent buffer."""
+    import types
+
+    import model as M
+    d = golden(f"g11_viewdep_{strategy}.npz")
+    torch.manual_seed(0)
+    m = M.make_model({"k": 64, "num_layers": 4, "mlp_hidden_dim": 64, "skip_layer_idx": 2,
+                      "view_dependence": {"bottleneck_vec_dim": 16, "in_dim_view_dir": 1 if strategy == "intrinsic"
+                                          else 3, "include_view_dir": True, "embed_size": 4,
+                                          "directional_hidden_dim": 32, "strategy": strategy}},
+                     mesh=types.SimpleNamespace(face_normals=d["normals"].astype(np.float64)))
+    sd = m.state_dict()
+    ref = {k[2:]: d[k] for k in d.files if k.startswith("w:")}
+    assert list(sd) == list(ref)
+    for k, v in ref.items():
+        np.testing.assert_array_equal(sd[k].numpy(), v, err_msg=k)
