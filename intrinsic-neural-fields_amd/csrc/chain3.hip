@@ -178,7 +178,9 @@ __device__ __forceinline__ float col_sum4(float v) {
 // would add `s_waitcnt vmcnt(0)` and stall on the weight fragments in flight)
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int H, int LOSS>
+// ENC: the extrinsic front-end (Chain3Args::encoding != INF_ENC_NONE) -- a separate
+// instantiation so the eigenfunction gather's code and registers stay as they were
+template <int H, int LOSS, bool ENC>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
   using C = L3<H>;
   constexpr int BM = C::BM, TN = C::TN, UPL = C::UPL;
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     }
     // extrinsic front-end: thread (ray, coordinate c) forms x_c of its ray (the gather's
     // fma order) into activation buffer 0, unused until phase 1; [BM][4] = x, live
-    if (a.encoding != INF_ENC_NONE && tid < BM * 3) {
+    if (ENC && tid < BM * 3) {
       float* rx = reinterpret_cast<float*>(act);
       int64_t offset = a.idx_offset;
       if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
@@ -302,7 +304,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // ---- gather: the feature tile, 16-byte chunks (8 columns) per thread ---------------
     // fp32 FMA in the reference order b0 e0 + b1 e1 + b2 e2, rounded to bf16 once (the
     // gather kernel's numerics); every load of a round is issued before any use
-    if (a.encoding != INF_ENC_NONE) {
+    if constexpr (ENC) {
       // extrinsic front-end: RFF / FF / xyz columns of the rays' positions x (LDS, above),
       // bitwise gather.hip encode_kernel's values, rounded to bf16.  A thread keeps one
       // 8-column chunk (ch = tid % cpr when cpr divides the thread count) across its rays,
@@ -787,20 +789,25 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   }
 }
 
-template <int H, int LOSS>
-int launch3_loss(const Chain3Args& a, hipStream_t stream) {
+template <int H, int LOSS, bool ENC>
+int launch3_enc(const Chain3Args& a, hipStream_t stream) {
   using C = L3<H>;
   const int lds = C::lds_bytes(a.L, a.k_pad);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    lds));
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
-  chain3_kernel<H, LOSS><<<dim3((unsigned)(a.rows / C3BM)), dim3(C3_THREADS), lds, stream>>>(a);
+  chain3_kernel<H, LOSS, ENC><<<dim3((unsigned)(a.rows / C3BM)), dim3(C3_THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
+}
+
+template <int H, int LOSS>
+int launch3_loss(const Chain3Args& a, hipStream_t stream) {
+  return a.encoding != INF_ENC_NONE ? launch3_enc<H, LOSS, true>(a, stream) : launch3_enc<H, LOSS, false>(a, stream);
 }
 
 // the loss is a template parameter: one branch-free head per loss type keeps the compute
@@ -826,7 +833,8 @@ int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream) {
   INF_CHECK_ARG(a.encoding == INF_ENC_NONE || a.encoding == INF_ENC_XYZ || a.enc_proj != nullptr,
                 "chain3: encoding projection missing");
   INF_CHECK_ARG(a.vid_dtype == INF_DTYPE_I32 || a.vid_dtype == INF_DTYPE_I64, "chain3: vertex id dtype");
-  INF_CHECK_ARG(a.num_vertices * (int64_t)a.k_pad * 2 < (int64_t)1 << 31, "chain3: table exceeds 2 GiB");
+  INF_CHECK_ARG(a.encoding != INF_ENC_NONE || a.num_vertices * (int64_t)a.k_pad * 2 < (int64_t)1 << 31,
+                "chain3: table exceeds 2 GiB");
   for (int i = 0; i < a.nblk; ++i) INF_CHECK_ARG(a.blk[i].img != nullptr, "chain3: weight image missing");
   // bias / output-layer rows are read as H/64-float vectors per lane
   for (int l = 0; l < a.L - 1; ++l) INF_CHECK_ARG((uintptr_t)a.bias[l] % 16 == 0, "chain3: bias alignment");
