@@ -231,3 +231,26 @@ def test_trainer_rff_training_curve(tmp_path, mode, tol):
     rows = [json.loads(x) for x in open(os.path.join(tmp_path, "logs", "scalars.jsonl"))]
     curve = [r["value"] for r in rows if r["tag"] == "Val Epoch-PSNR"]
     np.testing.assert_allclose(curve, d["val_psnr"], atol=tol)
+
+
+def test_encode_kernel_ff_and_edges():
+    """inf_encode's FF mode (layers.py:6-25, 3-wide positions) against the oracle; an empty
+    batch; an out-of-range vertex id reads as the zero position (cos 1, sin 0, x 0), as the
+    gather reads it as a zero feature row."""
+    from inf_hip import runtime
+    rng = np.random.default_rng(9)
+    V, N, k = 50, 40, 6
+    P = (rng.random((V, 3)) * 2 - 1).astype(np.float32)
+    vids = rng.integers(0, V, (N, 3))
+    vids[3, 1] = V + 7
+    bary = rng.dirichlet([1, 1, 1], N).astype(np.float32)
+    bands = torch.from_numpy(O.ff_bands(k, use_logspace=True)).cuda()
+    enc = runtime.Encoding("ff", k, bands, include_input=True)
+    f = runtime.encode(enc, cu(P), cu(vids), cu(bary)).cpu().numpy()
+    x = O.interp_xyz(P.astype(np.float64), vids.clip(0, V - 1), bary.astype(np.float64))
+    x[3] = 0.0
+    ref = O.ff_encode(x, O.ff_bands(k, use_logspace=True).astype(np.float64), True)
+    assert f.shape == (N, 6 * k + 3)
+    np.testing.assert_allclose(f, ref, atol=5e-5)
+    np.testing.assert_array_equal(f[3, :3 * k], 1.0)
+    assert runtime.encode(enc, cu(P), cu(vids[:0].copy()), cu(bary[:0].copy())).shape == (0, 6 * k + 3)
