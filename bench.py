@@ -95,15 +95,44 @@ class Trainer:
                                           offset_from_ctrl=True, loss_count=3 * B * world)
         self.graphs = None
         self.i = 0
+        # the data-parallel step shape (flat-gradient all-reduce between the update and Adam);
+        # INF_BENCH_DP=1 runs it at world 1 too (rehearses RCCL capture on a one-GPU box)
+        self.dp = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
+        self.ar_in_graph = False
 
     GRAPH_STEPS = 8  # steps per replayed graph on one GPU (divides nb)
 
     def _launch(self):
-        if self.world == 1:
+        if not self.dp:
             # Adam + the batch-index advance ride in the step's update launch
             self.plan.train_step(self.batch, None, apply_adam=True, advance=True)
         else:
             self.plan.train_step(self.batch, None, apply_adam=False)
+
+    def _dp_tail(self):
+        """all-reduce of the flat gradient bucket, then the replicated Adam + batch advance"""
+        if torch.distributed.is_initialized():
+            torch.distributed.all_reduce(self.plan.grads)
+        self.plan.adam(0, 0.0)
+        self.plan.ctrl_advance()
+
+    def _capture_dp_steps(self, s):
+        """GRAPH_STEPS whole data-parallel steps (RCCL all-reduce included) in one graph: no
+        host round trip per step.  INF_DP_EAGER_AR=1 keeps the all-reduce outside the graphs."""
+        if os.environ.get("INF_DP_EAGER_AR"):
+            return None
+        try:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, stream=s):
+                for _ in range(self.GRAPH_STEPS):
+                    self._launch()
+                    self._dp_tail()
+            self.ar_in_graph = True
+            return gm
+        except Exception as exc:  # capture refused: per-step replays around an eager all-reduce
+            print(f"[bench] all-reduce graph capture failed ({exc}); eager all-reduce", file=sys.stderr)
+            torch.cuda.synchronize()
+            return None
 
     def capture(self):
         # one eager step: settles the plan's tables before capture
@@ -117,7 +146,8 @@ class Trainer:
             with torch.cuda.graph(g1, stream=s):
                 self._launch()
             g2 = gm = None
-            if self.world > 1:
+            if self.dp:
+                gm = self._capture_dp_steps(s)
                 g2 = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g2, stream=s):
                     self.plan.adam(0, 0.0)
@@ -141,10 +171,8 @@ class Trainer:
     def step_eager(self):
         self._wrap()
         self._launch()
-        if self.world > 1:
-            torch.distributed.all_reduce(self.plan.grads)
-            self.plan.adam(0, 0.0)
-            self.plan.ctrl_advance()
+        if self.dp:
+            self._dp_tail()
         self.i += 1
 
     def step(self):
@@ -154,7 +182,8 @@ class Trainer:
         g1, g2, _ = self.graphs
         g1.replay()
         if g2 is not None:
-            torch.distributed.all_reduce(self.plan.grads)
+            if torch.distributed.is_initialized():
+                torch.distributed.all_reduce(self.plan.grads)
             g2.replay()
         self.i += 1
 
@@ -402,15 +431,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or os.environ.get("INF_BENCH_DP"):
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl")
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
     tr = Trainer(args, device, args.batch, rank, world)
     tr.capture()
     ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
+    tr_ar_in_graph = tr.ar_in_graph
     value = world * args.batch / (ms * 1e-3)
 
     from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
@@ -488,7 +518,8 @@ def main():
             "config": {"workload": f"cat texture_reconstruction k={k} {L}x{H} MLP skip {args.skip}, L2, Adam "
                                    f"lr 1e-4, fused gather+fwd+bwd+Adam step",
                        "rays_per_gpu_per_step": args.batch, "global_batch": args.batch * world,
-                       "verts": args.verts, "parallelism": f"dp{world}", "graph": not args.no_graph},
+                       "verts": args.verts, "parallelism": f"dp{world}", "graph": not args.no_graph,
+                       "allreduce_in_graph": tr_ar_in_graph},
             "model_tflops": flops_ray * value / 1e12,
             "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES[dom],
                          "achieved": achieved, "peak": PEAK[args.mode], "unit": "TFLOP/s",
@@ -505,7 +536,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 
