@@ -244,8 +244,11 @@ def render_bench(args, device):
     m = build_model(args, device)
     rt = m.hip_runtime()
     nhit = H * W // 2
-    chunk = 1 << 18
-    plan = runtime.Plan(args.k, args.hidden, args.layers, args.skip, args.mode, "L2", chunk, rt.arena)
+    chunk = int(os.environ.get("INF_RENDER_CHUNK", 1 << 18))
+    nstreams = int(os.environ.get("INF_RENDER_STREAMS", "1"))
+    plans = [runtime.Plan(args.k, args.hidden, args.layers, args.skip, args.mode, "L2", chunk, rt.arena)
+             for _ in range(nstreams)]
+    plan = plans[0]
     g = torch.Generator(device="cpu").manual_seed(7)
     E = torch.randn((V, args.k), generator=g)
     E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
@@ -257,12 +260,22 @@ def render_bench(args, device):
     del E
     hit = torch.randperm(H * W, device=device)[:nhit]
     img = torch.empty((H * W, 3), device=device)
-    batches = [plan.make_batch(source=src, offset=o, batch=min(chunk, nhit - o)) for o in range(0, nhit, chunk)]
+    offs = list(range(0, nhit, chunk))
+    batches = [plans[j % nstreams].make_batch(source=src, offset=o, batch=min(chunk, nhit - o))
+               for j, o in enumerate(offs)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
 
     def frame():
         img.fill_(1.0)
-        for o, b in zip(range(0, nhit, chunk), batches):
-            plan.render(b, hit[o:o + b.batch], None, img)
+        cur = torch.cuda.current_stream()
+        for st in streams[1:]:
+            st.wait_stream(cur)
+        # chunks round-robin over the plans/streams: one chunk's gather overlaps another's chain
+        for j, (o, b) in enumerate(zip(offs, batches)):
+            with torch.cuda.stream(streams[j % nstreams]):
+                plans[j % nstreams].render(b, hit[o:o + b.batch], None, img)
+        for st in streams[1:]:
+            cur.wait_stream(st)
 
     frame()
     torch.cuda.synchronize()
@@ -275,7 +288,7 @@ def render_bench(args, device):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
-            "hits": nhit, "verts": V, "chunk": chunk}
+            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams}
 
 
 def torus_mesh(nu=640, nv=320, R=1.0, r=0.4):

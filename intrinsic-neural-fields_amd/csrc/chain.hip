@@ -76,7 +76,11 @@ struct CT {
   static constexpr int OFF_W7 = OFF_RED + 128;          // [3][H] f32, then b7[3] (+pad)
   static constexpr int OFF_VEC = OFF_W7 + 3 * H * 4 + 16;
   static constexpr int MASK_BYTES = BM * H / 8;  // one layer of ReLU bits
-  static int lds_bytes(int L) { return OFF_VEC + L * H * 4 + (L > 2 ? (L - 2) : 0) * MASK_BYTES; }
+  // the ReLU masks exist only for the backward chain: a forward-only (render) launch
+  // leaves their LDS to a deeper weight ring
+  static int lds_bytes(int L, bool train) {
+    return OFF_VEC + L * H * 4 + (train && L > 2 ? (L - 2) : 0) * MASK_BYTES;
+  }
   static_assert(W_BYTES % (1024 * NW) == 0, "weight stage must split into whole wave instructions");
   static_assert(X_BYTES % 1024 == 0, "feature stage must be whole wave instructions");
   static_assert(NS >= 2 && MAXWAIT <= 40, "ring depth");
@@ -516,7 +520,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
 template <int H, int BM, int BK, int NS>
 int launch_typed(const ChainArgs& a, hipStream_t stream) {
   using C = CT<H, BM, BK, NS>;
-  const int lds = C::lds_bytes(a.L);
+  const int lds = C::lds_bytes(a.L, a.train != 0);
   INF_CHECK_ARG(lds <= LDS_CAP, "chain: LDS budget exceeded for this depth");
   static int attr_set = 0;
   if (attr_set < lds) {
@@ -532,7 +536,7 @@ int launch_typed(const ChainArgs& a, hipStream_t stream) {
 // deepest ring that fits the LDS for this depth
 template <int H, int BM, int BK, int NS_HI, int NS_LO>
 int launch_fit(const ChainArgs& a, hipStream_t stream) {
-  if (CT<H, BM, BK, NS_HI>::lds_bytes(a.L) <= LDS_CAP) return launch_typed<H, BM, BK, NS_HI>(a, stream);
+  if (CT<H, BM, BK, NS_HI>::lds_bytes(a.L, a.train != 0) <= LDS_CAP) return launch_typed<H, BM, BK, NS_HI>(a, stream);
   return launch_typed<H, BM, BK, NS_LO>(a, stream);
 }
 

@@ -1,6 +1,8 @@
 // Fused per-ray-tile MLP chain (bf16 perf mode), see chain.hip.
 #pragma once
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace inf {
@@ -71,6 +73,10 @@ inline bool chain_supported(int H) { return H == 128 || H == 256; }
 // small (every workgroup streams all weights, so more tiles = more CUs streaming), then
 // taller tiles that do more MFMA work per streamed weight byte.
 inline int chain_bm(int64_t rows) {
+  if (const char* e = std::getenv("INF_CHAIN_BM")) {  // tuning: 64 or 128 (partials stay per 64 rays)
+    const int v = std::atoi(e);
+    if ((v == 64 || v == 128) && rows % v == 0 && rows > 16384) return v;
+  }
   if (rows <= 4096) return 16;
   if (rows <= 8192) return 32;
   if (rows <= 16384) return 64;

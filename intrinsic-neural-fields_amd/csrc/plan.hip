@@ -194,7 +194,11 @@ int build_layout(inf_plan* p) {
   // bf16 steps of the register-streamed chain reduce their weight gradients with lgemm
   // (896-block grid at 4096 rays already): fewer, longer splits halve the slab traffic
   // the update launch reads (4096 rays: dW + update 30.8 -> 25.2 us at 4 splits vs 8)
+  // 4096 rays: 2 splits (224 blocks of 8 k-steps, one per CU) beat 4 (448 blocks of 4 on
+  // 256 CUs, the same 8-step critical path) by the halved slab bytes: step 73.0 -> 71.3 us
+  // (tools/split_sweep.sh)
   if (d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
+  if (d.mode == INF_MODE_BF16 && mb <= 4096 && S > 2) S = 2;
   if (const char* e = std::getenv("INF_DW_SPLITS")) {  // tuning experiments
     const int want = std::atoi(e);
     if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 128) S = want;
