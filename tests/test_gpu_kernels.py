@@ -337,3 +337,40 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
     for a_, b_ in zip(out["separate"][:4], out["fused"][:4]):
         assert np.array_equal(a_, b_)
     assert out["separate"][4] == out["fused"][4]
+
+
+def test_dp_step_shape_bitwise_equals_fused_step():
+    """The data-parallel step shape bench.py captures for --gpus N (update writes the
+    reduced gradient -> all-reduce -> separate Adam launch -> batch advance; the all-reduce
+    is the identity at world 1) is bitwise the fused single-GPU step (Adam + advance inside
+    the update launch) over several bf16 chain3 steps of config B."""
+    rng = np.random.default_rng(33)
+    k, H, L, s = CFG["B"]
+    B, nb, V = 4096, 3, 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    N = nb * B
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (N, 3))).cuda(),
+                         torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32)).cuda(),
+                         torch.from_numpy(rng.random((N, 3)).astype(np.float32)).cuda())
+    perm = torch.from_numpy(rng.permutation(N)).cuda()
+    out = {}
+    for shape in ("fused", "dp"):
+        plan, params, _ = make_plan("B", mode="bf16", max_batch=B, adam=True)
+        plan.set_lr(1e-3)
+        b = plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B, offset_from_ctrl=True, loss_count=3 * B)
+        for _ in range(nb):
+            if shape == "fused":
+                plan.train_step(b, None, apply_adam=True, advance=True)
+            else:
+                plan.train_step(b, None, apply_adam=False)
+                plan.adam(0, 0.0)
+                plan.ctrl_advance()
+        c = plan.read_ctrl()
+        out[shape] = (params.cpu().numpy(), plan.exp_avg.cpu().numpy(), plan.exp_avg_sq.cpu().numpy(),
+                      c["step"], c["batch_index"], c["epoch_loss"])
+    f, d = out["fused"], out["dp"]
+    assert f[3] == d[3] == nb and f[4] == d[4] == nb
+    for a, b_ in zip(f[:3], d[:3]):
+        np.testing.assert_array_equal(a, b_)
+    assert f[5] == d[5]
