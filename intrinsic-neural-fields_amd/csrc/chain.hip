@@ -38,6 +38,10 @@
 // 16l..16l+15 of the instruction's 1 KiB), so the swizzle goes on the source address.
 #include "chain.hpp"
 
+#ifndef CHAIN_X_CPOL
+#define CHAIN_X_CPOL 0  // cache policy of the feature-tile loads (2: non-temporal)
+#endif
+
 namespace inf {
 namespace {
 
@@ -230,7 +234,7 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
         const int r0 = (wv + C::NW * i) * C::RPI;
         const int row = r0 + lrow;
         const bf16* src = a.X + (int64_t)(b0 + row) * a.k_pad + k0 + ((lslot ^ stage_swz<BK>(row)) << 3);
-        if (GOK(src, 16, 3)) __builtin_amdgcn_global_load_lds(src, (lds_void*)(xs + r0 * C::ROWB), 16, 0, 0);
+        if (GOK(src, 16, 3)) __builtin_amdgcn_global_load_lds(src, (lds_void*)(xs + r0 * C::ROWB), 16, 0, CHAIN_X_CPOL);
       }
     } else {
       xbits &= ~(1u << slot);

@@ -1,6 +1,9 @@
 #!/bin/bash
-# render slice variants (GPU box): fused LDS-ring chain vs layered GEMMs
+# render slice + large-batch step under library variants (GPU box): tools/render_sweep.sh [lib ...]
 set -uo pipefail
-for v in "" "INF_NO_CHAIN=1"; do echo "== $v"; env $v timeout -k 10 120 python -u tools/render_step.py 2>/dev/null | grep '^{' | cut -c1-100 || exit 1; done
-export TMPDIR=/tmp
-INF_NO_CHAIN=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_render_layered -o run --output-format csv -- python3 tools/render_step.py > /dev/null 2>&1
+L=intrinsic-neural-fields_amd/inf_hip
+for lib in "$L/libinf_hip.so" "$@"; do
+  echo "== $lib"
+  INF_LIB=$lib timeout -k 10 120 python -u tools/render_step.py 2>/dev/null | grep '^{' | cut -c1-100 || exit 1
+  INF_LIB=$lib timeout -k 10 120 python -u bench.py --batch 65536 --steps 20 --warmup 3 --no-render --no-cpu-baseline --extra-batches "" 2>/dev/null | grep '^{' | cut -c1-160 || exit 1
+done
