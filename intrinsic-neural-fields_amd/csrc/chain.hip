@@ -33,7 +33,7 @@
 // LDS swizzles (16-byte chunk c of row r):
 //   activation rows (>= 256 B): c ^ (r & 15)
 //   stage rows of 128 B:        c ^ ((r >> 1) & 7)
-//   stage rows of  64 B:        c ^ ((r >> 2) & 3)
+//   stage rows of  64 B:        c ^ (3 * ((r >> 3) & 1))
 // The stage image is lane-linear (lane l of a direct-to-LDS load writes bytes
 // 16l..16l+15 of the instruction's 1 KiB), so the swizzle goes on the source address.
 #include "chain.hpp"
@@ -93,7 +93,11 @@ struct CT {
 template <int BK>
 __device__ __forceinline__ int stage_swz(int row) {
   if constexpr (BK == 64) return (row >> 1) & 7;
-  else return (row >> 2) & 3;
+  // 64-B rows: a ds_read_b128 lane group {0-3,12-15,20-27} reads rows 0-3 and 12-15 at
+  // chunk c and rows 4-11 at chunk c+1 (4 rows per 256-B bank row); XOR 0 for row blocks
+  // 0-1 and 3 for blocks 2-3 puts those 16 reads on 16 distinct slots (the old (r>>2)&3
+  // left two per slot: SQ_LDS_BANK_CONFLICT was 43 % of the render chain's LDS cycles)
+  else return ((row >> 3) & 1) * 3;
 }
 
 template <int BK>
