@@ -100,7 +100,8 @@ class Trainer:
         self.dp = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
         self.ar_in_graph = False
 
-    GRAPH_STEPS = 8  # steps per replayed graph on one GPU (divides nb)
+    # steps per replayed graph (divides nb)
+    GRAPH_STEPS = int(os.environ.get("INF_GRAPH_STEPS", "8"))
 
     def _launch(self):
         if not self.dp:
