@@ -405,6 +405,43 @@ def rff_bench(args, device, B=4096, reps=6):
             "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s"}
 
 
+def psnr_vs_ref(mode):
+    """'PSNR vs ref' of BASELINE.json's metric: the reference's own 12-epoch synthetic
+    training run (tests/golden/g8_train_curve.npz, produced by importing the reference:
+    k=64 4x128 skip 2, L1, Adam; no dataset is available offline) re-run through this
+    framework's Trainer (trainer.py mirror, fused HIP steps) -- validation epoch-PSNR curve
+    against the reference's."""
+    import tempfile
+
+    import config
+    from ray_dataloader import RayDataLoader
+    from trainer import Trainer
+    d = np.load(os.path.join(ROOT, "tests", "golden", "g8_train_curve.npz"))
+    with tempfile.TemporaryDirectory() as out:
+        cfg = {"seed": 0, "data": {"img_height": 8, "img_width": 8},
+               "model": {"k": 64, "num_layers": 4, "mlp_hidden_dim": 128, "skip_layer_idx": 2,
+                         "kernels": {"mode": mode}},
+               "training": {"out_dir": out, "batch_size": int(d["batch"]), "lr": float(d["lr"]), "loss_type": "L1",
+                            "render_every": 1000, "print_every": 1000, "epochs": len(d["val_psnr"]),
+                            "checkpoint_every": 1000}}
+        E = torch.from_numpy(d["E"])
+        mk = lambda p, drop: RayDataLoader(E, "efuncs", torch.from_numpy(d[f"{p}_vids"]), torch.from_numpy(d[f"{p}_bary"]),
+                                           torch.from_numpy(d[f"{p}_rgb"]), None, None, int(d["batch"]), False, drop,
+                                           device="cuda")
+        torch.manual_seed(0)
+        model, optim = config.get_model_and_optim(cfg, None, "cuda")
+        model.kernel_mode = mode
+        tr = Trainer(model, optim, config.get_loss_fn(cfg), None, {"train": mk("tr", True), "val": mk("va", False)},
+                     None, cfg, "cuda")
+        tr.train()
+        rows = [json.loads(x) for x in open(os.path.join(out, "logs", "scalars.jsonl"))]
+    val = np.array([r["value"] for r in rows if r["tag"] == "Val Epoch-PSNR"])
+    ref = np.asarray(d["val_psnr"], dtype=np.float64)
+    return {"workload": "reference synthetic run G8 (k=64 4x128 skip 2, L1, 12 epochs)", "mode": mode,
+            "ref_final_db": float(ref[-1]), "final_db": float(val[-1]), "delta_final_db": float(val[-1] - ref[-1]),
+            "max_abs_delta_db": float(np.abs(val - ref).max())}
+
+
 def cpu_baseline(args):
     """The CPU oracle (numpy fp32 restatement of the reference step, oracle/inf_oracle.py)
     on this host's cores, config B at batch 4096: bounded sample of ~cpu_seconds."""
@@ -508,6 +545,13 @@ def main():
         render["end_to_end"] = render_e2e_bench(args, device)
         extrinsic = rff_bench(args, device)
 
+    psnr = None
+    if rank == 0 and world == 1 and not args.no_render:
+        try:
+            psnr = [psnr_vs_ref(m) for m in ("bf16", "fp32")]
+        except Exception as exc:  # reported, never fatal to the throughput line
+            psnr = {"error": repr(exc)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -547,6 +591,7 @@ def main():
             "large_batch": extra,
             "render": render,
             "extrinsic_rff": extrinsic,
+            "psnr_vs_ref": psnr,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
