@@ -443,8 +443,9 @@ def psnr_vs_ref(mode):
 
 
 def cpu_baseline(args):
-    """The CPU oracle (numpy fp32 restatement of the reference step, oracle/inf_oracle.py)
-    on this host's cores, config B at batch 4096: bounded sample of ~cpu_seconds."""
+    """CPU baselines on this host's cores, config B at batch 4096, bounded samples of
+    ~cpu_seconds each: the reference's PyTorch-CPU op sequence (oracle/torch_cpu.py, the
+    reported value) and the numpy oracle (oracle/inf_oracle.py)."""
     from oracle import inf_oracle as O
     cores = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     rng = np.random.default_rng(0)
@@ -472,9 +473,36 @@ def cpu_baseline(args):
         one()
         n += 1
     dt = time.perf_counter() - t0
+    numpy_leg = {"value": n * B / dt, "unit": "rays/s", "cores": cores, "kind": "port",
+                 "sample": f"{n} oracle train steps (numpy fp32) of {B} rays, k={k} {L}x{H} skip {s}, V={V}, "
+                           f"{dt:.1f} s"}
+
+    # the reference's own op sequence on a CPU device (torch index + bmm gather, F.linear
+    # layers, mse_loss, autograd, torch.optim.Adam): oracle/torch_cpu.py
+    from oracle import torch_cpu as T
+    torch.set_num_threads(cores)
+    tt = T.TorchTrainer(w, L, s, 1e-4, "L2")
+    Et = torch.from_numpy(E)
+    g = torch.Generator().manual_seed(0)
+
+    def one_torch():
+        vids = torch.randint(0, V, (B, 3), generator=g)
+        u = torch.rand((B, 3), generator=g).clamp_min(1e-12)
+        bary = -torch.log(u)
+        bary = bary / bary.sum(1, keepdim=True)
+        tt.step(T.gather(Et, vids, bary), torch.rand((B, 3), generator=g))
+
+    one_torch()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < args.cpu_seconds and n < 400:
+        one_torch()
+        n += 1
+    dt = time.perf_counter() - t0
     return {"value": n * B / dt, "unit": "rays/s", "cores": cores, "kind": "port",
-            "sample": f"{n} oracle train steps (numpy fp32) of {B} rays, k={k} {L}x{H} skip {s}, V={V}, "
-                      f"{dt:.1f} s"}
+            "sample": f"{n} train steps of the reference's PyTorch-CPU op sequence (oracle/torch_cpu.py, fp32) of "
+                      f"{B} rays, k={k} {L}x{H} skip {s}, V={V}, {dt:.1f} s",
+            "numpy_oracle": numpy_leg}
 
 
 def main():

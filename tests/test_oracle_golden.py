@@ -195,3 +195,32 @@ def test_ssim_oracle_known_answers():
                            ((ux ** 2 + uy ** 2 + 0.02 ** 2) * (vx + vy + 0.06 ** 2)))
         tot.append(np.mean(acc))
     assert O.structural_similarity(a, b) == pytest.approx(np.mean(tot), abs=1e-10)
+
+
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("R", "cauchy"), ("B", "L2")])
+def test_torch_cpu_baseline_train_step(name, loss):
+    """oracle/torch_cpu.py (the bench's PyTorch-CPU baseline) against the reference's
+    one-step goldens: loss, prediction, gradients, parameters after Adam."""
+    import torch
+    from oracle import torch_cpu as T
+    d = golden(f"g3_step_{name}_{loss}.npz")
+    w0 = weights(golden(f"g2_forward_{name}.npz"))
+    _, L, s = CFG[name]
+    tr = T.TorchTrainer(w0, L, s, 1e-4, loss)
+    lval, pred, grads = tr.step(torch.from_numpy(d["features"]), torch.from_numpy(d["rgb"]))
+    assert abs(lval - float(d["loss"])) < 1e-6
+    np.testing.assert_allclose(pred.numpy(), d["pred"], atol=1e-6)
+    for n in O.layer_names(L, s):
+        ref = d["g:" + n]
+        scale = max(np.abs(ref).max(), 1e-12)
+        assert np.abs(grads[n].numpy() - ref).max() <= 1e-4 * scale + 1e-9, n
+        if "w1:" + n in d.files:
+            np.testing.assert_allclose(tr.p[n].detach().numpy(), d["w1:" + n], atol=1e-6, err_msg=n)
+
+
+def test_torch_cpu_gather_golden():
+    import torch
+    from oracle import torch_cpu as T
+    d = golden("g1_gather_k64.npz")
+    out = T.gather(torch.from_numpy(d["E"]), torch.from_numpy(d["vids"]), torch.from_numpy(d["bary"]))
+    np.testing.assert_allclose(out.numpy(), d["out"], atol=1e-6)
