@@ -49,13 +49,21 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra-batches", default="65536", help="comma list of extra per-GPU batch sizes to report")
+    ap.add_argument("--no-config-d", action="store_true")
+    ap.add_argument("--only", default="", help="debug: run only these comma-separated secondary sections "
+                                                "(configD, render, rff, psnr, cpu) after the headline")
     return ap.parse_args()
 
 
 def synthetic(V, k, N, seed, device):
     g = torch.Generator(device="cpu").manual_seed(seed)
-    E = torch.randn((V, k), generator=g)
-    E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
+    if V * k > (1 << 28):  # config D's 500k x 4096 table (8.2 GB fp32): drawn on the device
+        gd = torch.Generator(device=device).manual_seed(seed)
+        E = torch.randn((V, k), generator=gd, device=device)
+        E /= E.max(0, keepdim=True).values - E.min(0, keepdim=True).values
+    else:
+        E = torch.randn((V, k), generator=g)
+        E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
     vids = torch.randint(0, V, (N, 3), generator=g)
     u = torch.rand((N, 3), generator=g).clamp_min(1e-12)
     bary = -torch.log(u)
@@ -77,7 +85,7 @@ def build_model(args, device):
 class Trainer:
     """Graph-captured fused steps over one RaySource (one rank)."""
 
-    def __init__(self, args, device, B, rank, world):
+    def __init__(self, args, device, B, rank, world, nb=32):
         from inf_hip import runtime
         self.args, self.B, self.world = args, B, world
         self.model = build_model(args, device)
@@ -86,7 +94,7 @@ class Trainer:
         self.plan = runtime.Plan(args.k, args.hidden, args.layers, args.skip, args.mode, "L2", B, rt.arena,
                                  rt.grads, rt.exp_avg, rt.exp_avg_sq)
         self.plan.set_lr(1e-4)
-        self.nb = 32
+        self.nb = nb
         self.N = self.nb * B
         E, vids, bary, rgb = synthetic(args.verts, args.k, self.N, seed=1 + rank, device=device)
         self.src = runtime.RaySource(E, vids, bary, rgb)
@@ -234,6 +242,62 @@ def time_stage(plan, stage, reps=20, batch=None, layer=0):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps, flops, byts
+
+
+def flops_per_ray(k, H, L):
+    """Training FLOPs per ray: forward, dX chain and dW."""
+    return 2 * (2 * (2 * k * H + (L - 2) * H * H + 3 * H) + (L - 2) * H * H + 3 * H)
+
+
+def step_roofline(k, H, L, B, P, ms, table_bytes=2, weight_bytes=2, dtype="bf16"):
+    """Both t_min terms of one training step: FLOPs vs the dense MFMA
+    peak, algorithmic HBM bytes (3 table rows + ids/bary/rgb per ray; Adam's 28 B and three
+    weight passes per parameter per step) vs 8 TB/s.  frac = t_min / t_measured."""
+    k_pad = -(-k // 128) * 128
+    flops = B * flops_per_ray(k, H, L)
+    byts = B * (3 * k_pad * table_bytes + 36) + P * (28 + 3 * weight_bytes)
+    t_mfma = flops / (PEAK[dtype] * 1e12) * 1e3
+    t_hbm = byts / (HBM_PEAK * 1e9) * 1e3
+    return {"flops": flops, "bytes": byts, "t_mfma_ms": t_mfma, "t_hbm_ms": t_hbm,
+            "bound": "mfma" if t_mfma >= t_hbm else "hbm",
+            "mfma_frac": t_mfma / ms, "hbm_frac": t_hbm / ms, "frac": max(t_mfma, t_hbm) / ms,
+            "achieved_tflops": flops / (ms * 1e-3) / 1e12, "achieved_gbs": byts / (ms * 1e-3) / 1e9}
+
+
+def config_d_bench(args, device, B=4096, steps=40):
+    """Config D (configs/discretization_agnostic/human_dense.yaml):
+    k = 4096 eigenfunctions of a ~500k-vertex discretisation, 8 x 256 MLP, skip 4, L2, Adam;
+    the bf16 table is 4.1 GB, far beyond the 256 MB MALL, so every row of the gather is a
+    random HBM read.  Graph-replayed fused steps (chain3 with a chunked feature tile), the
+    per-kernel times, the standalone gather kernel's HBM rate on the same rays, and both
+    roofline terms of the step."""
+    import copy
+    from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
+    a = copy.copy(args)
+    a.k, a.verts, a.no_graph = 4096, 500_000, False
+    tr = Trainer(a, device, B, 0, 1, nb=8)
+    tr.capture()
+    ms, _ = time_steps(tr, steps, 8, 1)
+    path = tr.plan.last_step_path()
+    st = {"chain3": time_stage(tr.plan, STAGE_CHAIN, reps=10, batch=tr.batch),
+          "dw_gemm": time_stage(tr.plan, STAGE_DW_GEMM, reps=10),
+          "update": time_stage(tr.plan, STAGE_UPDATE, reps=10, layer=1)}
+    gms, _, gbytes = time_stage(tr.plan, STAGE_GATHER, reps=10, batch=tr.batch)
+    P = tr.plan.info.num_params
+    k_pad = tr.plan.in_pad
+    row_bytes = B * 3 * k_pad * 2
+    out = {"config": "human_dense D: k=4096 8x256 skip 4, L2, Adam lr 1e-4, V=500000, bf16 table 4.1 GB",
+           "rays_per_step": B, "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s", "path": path,
+           "roofline": step_roofline(4096, a.hidden, a.layers, B, P, ms),
+           "stages": {kk: {"ms": v[0], "tflops": v[1] / (v[0] * 1e-3) / 1e12} for kk, v in st.items()},
+           "gather_kernel": {"ms": gms, "table_row_bytes": row_bytes,
+                             "table_gbs": row_bytes / (gms * 1e-3) / 1e9,
+                             "table_hbm_frac": row_bytes / (gms * 1e-3) / 1e9 / HBM_PEAK,
+                             "note": "standalone gather (X and X^T written) of the step's rays; inside the "
+                                     "fused chain the rows go straight to LDS"}}
+    del tr
+    torch.cuda.empty_cache()
+    return out
 
 
 def render_bench(args, device):
@@ -551,8 +615,13 @@ def main():
         except Exception:
             traffic = None
 
+    only = {x for x in args.only.split(",") if x}
+
+    def want(section):
+        return not only or section in only
+
     extra = {}
-    for eb in [int(x) for x in args.extra_batches.split(",") if x]:
+    for eb in [int(x) for x in args.extra_batches.split(",") if x and want("large")]:
         if eb == args.batch:
             continue
         del tr
@@ -565,23 +634,29 @@ def main():
                           "dw_gemm_tflops": d_fl / (d_ms * 1e-3) / 1e12}
         tr = tr2
 
+    del tr
+    torch.cuda.empty_cache()
+    config_d = None
+    if rank == 0 and world == 1 and not args.no_config_d and args.mode == "bf16" and want("configD"):
+        config_d = config_d_bench(args, device)
+
     render = extrinsic = None
     if not args.no_render and rank == 0:
-        del tr
-        torch.cuda.empty_cache()
-        render = render_bench(args, device)
-        render["end_to_end"] = render_e2e_bench(args, device)
-        extrinsic = rff_bench(args, device)
+        if want("render"):
+            render = render_bench(args, device)
+            render["end_to_end"] = render_e2e_bench(args, device)
+        if want("rff"):
+            extrinsic = rff_bench(args, device)
 
     psnr = None
-    if rank == 0 and world == 1 and not args.no_render:
+    if rank == 0 and world == 1 and not args.no_render and want("psnr"):
         try:
             psnr = [psnr_vs_ref(m) for m in ("bf16", "fp32")]
         except Exception as exc:  # reported, never fatal to the throughput line
             psnr = {"error": repr(exc)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and want("cpu"):
         cpu = cpu_baseline(args)
 
     if rank == 0:
@@ -617,6 +692,7 @@ def main():
                        for k, v in stages.items()},
             "host_wall_ms_per_step": wall_ms,
             "large_batch": extra,
+            "config_D": config_d,
             "render": render,
             "extrinsic_rff": extrinsic,
             "psnr_vs_ref": psnr,

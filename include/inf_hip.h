@@ -222,10 +222,11 @@ enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2 };
 int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int flags,
                    inf_stream_t stream);
 
-/* Adam update from the bound `grads` arena (optim.step(), trainer.py:82).  step > 0
- * and lr > 0 are used as given (torch state["step"] after its increment, param_group
- * lr); otherwise both are read from ctrl (graph-replayed steps, where head_bwd has
- * already advanced ctrl->step). */
+/* Adam update from the bound `grads` arena (optim.step(), trainer.py:82).  step > 0:
+ * step and lr are used as given (torch state["step"] after its increment, param_group
+ * lr -- lr = 0 leaves the parameters unchanged, as torch does); step <= 0: both are read
+ * from ctrl (graph-replayed steps, where the fused step has already advanced
+ * ctrl->step). */
 int inf_adam(inf_plan* plan, int step, float lr, inf_stream_t stream);
 
 /* Render slice (renderer.py:112-146): forward of `batch` and placement of each
@@ -269,6 +270,12 @@ int inf_debug_timing(inf_plan* plan, unsigned long long* stamps_dev, int max_ste
  * [5] items decided, [6] / [7] around its update item (8 words per block).  Pass null to
  * turn it off. */
 int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
+
+/* Diagnostics: the kernel path the last inf_train_step took -- 0 layered GEMMs, 2 the
+ * LDS-ring chain (csrc/chain.hip), 3 the fused gather + register-streamed chain
+ * (csrc/chain3.hip), 4 the same with the feature tile streamed in chunks (k_pad > 1024);
+ * -1 before any step. */
+int inf_plan_last_step_path(const inf_plan* plan);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

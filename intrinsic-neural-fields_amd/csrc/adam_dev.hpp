@@ -250,8 +250,12 @@ __device__ __forceinline__ void matrix_items_pipelined(const AdamArgs& a, const 
   if (a.do_adam && tid == 0) {
     int t = a.step_host;
     float lr = a.lr_host;
-    if (t <= 0) t = a.ctrl->step;
-    if (!(lr > 0.f)) lr = a.ctrl->lr;
+    // host-driven step (step_host > 0): t and lr as given, lr = 0 included (a frozen
+    // group); otherwise both from ctrl (graph-replayed steps)
+    if (t <= 0) {
+      t = a.ctrl->step;
+      lr = a.ctrl->lr;
+    }
     const double bc1 = 1.0 - pow_int(a.beta1_d, t);
     const double bc2 = 1.0 - pow_int(a.beta2_d, t);
     sc.step_neg = (float)(-((double)lr / bc1));
@@ -362,8 +366,12 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
   if (a.do_adam && tid == 0) {
     int t = a.step_host;
     float lr = a.lr_host;
-    if (t <= 0) t = a.ctrl->step;
-    if (!(lr > 0.f)) lr = a.ctrl->lr;
+    // host-driven step (step_host > 0): t and lr as given, lr = 0 included (a frozen
+    // group); otherwise both from ctrl (graph-replayed steps)
+    if (t <= 0) {
+      t = a.ctrl->step;
+      lr = a.ctrl->lr;
+    }
     const double bc1 = 1.0 - pow_int(a.beta1_d, t);
     const double bc2 = 1.0 - pow_int(a.beta2_d, t);
     sc.step_neg = (float)(-((double)lr / bc1));

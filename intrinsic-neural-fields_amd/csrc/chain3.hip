@@ -85,9 +85,10 @@ struct L3 {
   static constexpr int OFF_RBARY = OFF_RAY + BM * 16 + BM * 12 + 16;  // [BM][3] barycentrics
   static constexpr int OFF_W7 = OFF_RBARY + BM * 12 + 16;  // [3][H] then b7[3]
   static constexpr int OFF_VEC = OFF_W7 + 3 * H * 4 + 16;  // biases [L-1][H], then Ly.bias [H]
+  // the feature tile holds kx columns: k_pad, or C3_KC when it is streamed in chunks
   __host__ __device__ static int off_x(int L) { return OFF_VEC + L * H * 4; }
-  __host__ __device__ static int off_stamp(int L, int k_pad) { return off_x(L) + BM * k_pad * 2; }
-  static int lds_bytes(int L, int k_pad) { return off_stamp(L, k_pad) + (7 * C3_MAX_PHASES + 8) * 8; }
+  __host__ __device__ static int off_stamp(int L, int kx) { return off_x(L) + BM * kx * 2; }
+  static int lds_bytes(int L, int kx) { return off_stamp(L, kx) + (7 * C3_MAX_PHASES + 8) * 8; }
   static_assert(TN >= 1 && TN * 4 <= 8, "ReLU bits of a lane: at most 8 per layer");
   static_assert(OFF_LS % 8 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
@@ -179,8 +180,14 @@ __device__ __forceinline__ float col_sum4(float v) {
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ENC: the extrinsic front-end (Chain3Args::encoding != INF_ENC_NONE) -- a separate
-// instantiation so the eigenfunction gather's code and registers stay as they were
-template <int H, int LOSS, bool ENC>
+// instantiation so the eigenfunction gather's code and registers stay as they were.
+// XC: the feature tile is streamed in C3_KC-column chunks (k_pad > C3_KC, config D's
+// k = 4096).  Phase 0 then runs BOTH input layers over each chunk -- Ly's product
+// W_y x is independent of h, so it is accumulated in a second register set (accy) while
+// the chunk is resident and added in the skip layer's epilogue; each chunk is gathered
+// once, at its first block (two barriers: everyone is done with the previous chunk /
+// the new one is in LDS), and the store wave copies its X^T between them.
+template <int H, int LOSS, bool ENC, bool XC>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
   using C = L3<H>;
   constexpr int BM = C::BM, TN = C::TN, UPL = C::UPL;
@@ -201,8 +208,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   float* rbary = reinterpret_cast<float*>(smem + C::OFF_RBARY);  // [BM][3]
   float* w7s = reinterpret_cast<float*>(smem + C::OFF_W7);
   float* vecs = reinterpret_cast<float*>(smem + C::OFF_VEC);
-  char* xs = smem + C::off_x(L);  // gathered features [BM][k_pad] bf16 (tile_off layout)
-  const int xrow = k_pad * 2;
+  char* xs = smem + C::off_x(L);  // gathered features [BM][kx] bf16 (tile_off layout)
+  const int kx = XC ? C3_KC : k_pad;  // columns resident in LDS
+  const int xrow = kx * 2;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -216,7 +224,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   // wave 0 records everything; the last compute wave and the store wave their B1 arrivals
   const bool stamp_wg = a.stamps != nullptr && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
   if (stamp_wg && (wave == 0 || wave == C3_CW - 1 || wave == C3_CW))
-    stl = reinterpret_cast<unsigned long long*>(smem + C::off_stamp(L, k_pad));
+    stl = reinterpret_cast<unsigned long long*>(smem + C::off_stamp(L, kx));
   const unsigned long long t_entry = stl != nullptr ? wall_clock64() : 0ull;
   auto stamp = [&](int i) {
     if (stl != nullptr) {
@@ -287,6 +295,61 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       rx[rl * 4 + c] = x;
       if (c == 0) rx[rl * 4 + 3] = live ? 1.f : 0.f;
     }
+    // gather of table columns [col0, col0 + ncols) of the 16 rays into the LDS feature tile,
+    // 16-byte chunks (8 columns) per thread: fp32 FMA in the reference order
+    // b0 e0 + b1 e1 + b2 e2, rounded to bf16 once (the gather kernel's numerics); every
+    // load of a round is issued before any use.  Tables below 4 GiB are read through one
+    // buffer descriptor (32-bit unsigned byte offsets); larger ones with 64-bit row
+    // addresses (BIGc, a uniform choice per launch).
+    // GRc: chunks per thread per round (4: 1024 columns in one round; 2 inside the weight
+    // stream of the chunked schedule, where the fragment ring and both accumulator sets
+    // are live)
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.table), (short)0, (int)0xFFFFFFFFu, 0x00020000);
+    auto gather_cols = [&](auto GRc, auto BIGc, int col0, int ncols) {
+      constexpr int GR = decltype(GRc)::value;
+      constexpr bool BIG = decltype(BIGc)::value;
+      const int cpr = ncols >> 3;          // chunks per row
+      const int nch = BM * cpr;            // chunks of the tile
+#pragma unroll 1
+      for (int q0 = tid; q0 < nch; q0 += C3_CT * GR) {
+        u16x8 ev[GR][3];
+        float wv[GR][3];
+        int okv[GR];
+#pragma unroll
+        for (int g = 0; g < GR; ++g) {
+          const int q = q0 + C3_CT * g;
+          const int r = (q < nch ? q : 0) / cpr, ch = (q < nch ? q : 0) % cpr;
+          okv[g] = q < nch ? (rvid[BM * 4 + r * 3] & rvid[BM * 4 + r * 3 + 1] & rvid[BM * 4 + r * 3 + 2]) : 0;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            wv[g][i] = rbary[r * 3 + i];
+            if constexpr (BIG) {
+              const bf16* src = a.table + (int64_t)rvid[r * 4 + i] * k_pad + col0 + ch * 8;
+              ev[g][i] = __builtin_bit_cast(u16x8, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src)));
+            } else {
+              const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + col0 + ch * 8) * 2u;
+              ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rt, off, 0, C3_GATHER_CPOL));
+            }
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < GR; ++g) {
+          const int q = q0 + C3_CT * g;
+          if (q < nch) {
+            const int r = q / cpr, ch = q % cpr;
+            u16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x = fmaf(wv[g][2], bf_val3(ev[g][2][e]), fmaf(wv[g][1], bf_val3(ev[g][1][e]),
+                                                                       wv[g][0] * bf_val3(ev[g][0][e])));
+              o[e] = bf_bits3(okv[g] ? x : 0.f);
+            }
+            *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
+          }
+        }
+      }
+    };
     // the first block's fragments, in k order (the loop's waits assume that order); issued
     // after the dependent ray-record loads so those are not queued behind them
     {
@@ -358,46 +421,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
         *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
       }
-    } else
-    {
-      const int cpr = k_pad >> 3;          // chunks per row
-      const int nch = BM * cpr;            // chunks of the tile
-      constexpr int GR = 4;                // chunks per thread per round (k_pad 1024: one round)
-      const __amdgpu_buffer_rsrc_t rt =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.table), (short)0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll 1
-      for (int q0 = tid; q0 < nch; q0 += C3_CT * GR) {
-        u16x8 ev[GR][3];
-        float wv[GR][3];
-        int okv[GR];
-#pragma unroll
-        for (int g = 0; g < GR; ++g) {
-          const int q = q0 + C3_CT * g;
-          const int r = (q < nch ? q : 0) / cpr, ch = (q < nch ? q : 0) % cpr;
-          okv[g] = q < nch ? (rvid[BM * 4 + r * 3] & rvid[BM * 4 + r * 3 + 1] & rvid[BM * 4 + r * 3 + 2]) : 0;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            wv[g][i] = rbary[r * 3 + i];
-            const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + ch * 8) * 2u;
-            ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rt, off, 0, C3_GATHER_CPOL));
-          }
-        }
-#pragma unroll
-        for (int g = 0; g < GR; ++g) {
-          const int q = q0 + C3_CT * g;
-          if (q < nch) {
-            const int r = q / cpr, ch = q % cpr;
-            u16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float x = fmaf(wv[g][2], bf_val3(ev[g][2][e]), fmaf(wv[g][1], bf_val3(ev[g][1][e]),
-                                                                       wv[g][0] * bf_val3(ev[g][0][e])));
-              o[e] = bf_bits3(okv[g] ? x : 0.f);
-            }
-            *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
-          }
-        }
-      }
+    } else {
+      const int n0 = XC ? min(C3_KC, k_pad) : k_pad;
+      if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, 0, n0);
+      else gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, 0, n0);
     }
     stamp(3 * nphase + 4);
     lbar();  // barrier 0: feature tile in LDS
@@ -454,9 +481,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (r16 < NV) dst[feat(idx >> 2) + (idx & 3)] = s;
     };
 
-    f32x4 acc[TN];
+    f32x4 acc[TN], accy[TN];  // accy: W_y x of the chunked schedule (XC)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[j] = accy[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
     for (int i = 0; i < a.nblk; ++i) {
@@ -465,6 +492,24 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (i == 0 || a.blk[i - 1].last) stamp(1 + 3 * B.phase);
       // ---- MFMAs of block i; slot kb % D refilled with k-block kb + D of this block or
       // of block i+1 (the last block reloads itself: harmless loads keep waits exact)
+      if constexpr (XC) {
+        if (B.flags & C3F_GATHER) {
+          const int c = B.flags >> C3F_CHUNK_SHIFT;
+          lbar();  // G1: every wave is done with the previous chunk (and the store wave with its X^T)
+          const int nc = min(C3_KC, k_pad - c * C3_KC);
+          if (a.table_big) gather_cols(std::integral_constant<int, 2>{}, std::true_type{}, c * C3_KC, nc);
+          else gather_cols(std::integral_constant<int, 2>{}, std::false_type{}, c * C3_KC, nc);
+          lbar();  // G2: chunk c in LDS
+        }
+        if (B.flags & C3F_SWAP) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const f32x4 t = acc[j];
+            acc[j] = accy[j];
+            accy[j] = t;
+          }
+        }
+      }
       const __amdgpu_buffer_rsrc_t crs = rsrc_of(B.img);
       const __amdgpu_buffer_rsrc_t nrs = rsrc_of(Bn.img);
       const bool from_x = B.a_x != 0;
@@ -516,7 +561,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           if (skip) yv = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v = acc[j][r] + bv[r];
+            float v = acc[j][r];
+            if (XC && skip) v += accy[j][r];
+            v += bv[r];
             if (skip) v += yv[r];
             v = fmaxf(v, 0.f);
             hq[j][r] = bf_val3(bf_bits3(v));
@@ -734,14 +781,28 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       }
     };
+    int x_tile0 = 0;  // first 16-feature tile held in LDS (chunked tile)
     auto x_addr = [&](int t, int r, int q) -> const char* {
-      return xs + r * xrow + (((2 * t + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
+      return xs + r * xrow + (((2 * (t - x_tile0) + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
     };
     // X^T for the dW GEMMs of layer 0 and Ly, copied while the compute waves stream the
     // long input-layer phases (W_0: phase 0, W_y: the skip phase s), half in each
     const int xs_total = k_pad / 32;
-    const int xs_mid = a.s >= 1 ? xs_total / 2 : xs_total;
-    copy_image(x_addr, k_pad, a.XT, 0, xs_mid);
+    const int xs_mid = XC ? xs_total : (a.s >= 1 ? xs_total / 2 : xs_total);
+    if constexpr (XC) {
+      // chunked tile: X^T of chunk c between barriers G2(c) and G1(c + 1) (x_tile0 shifts
+      // the image's tile index to the chunk's LDS columns)
+      for (int c = 0; c < a.nchunk; ++c) {
+        if (c > 0) {
+          lbar();  // G1(c)
+          lbar();  // G2(c)
+        }
+        x_tile0 = c * (C3_KC / 16);
+        copy_image(x_addr, k_pad, a.XT, c * (C3_KC / 32), min((c + 1) * C3_KC, k_pad) / 32);
+      }
+    } else {
+      copy_image(x_addr, k_pad, a.XT, 0, xs_mid);
+    }
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
       for (int c = lane * 16; c < bytes; c += 64 * 16)
@@ -769,7 +830,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (p < nfwd) {
         const int l = p;
         if (!head_phase) copy_image(act_addr, H, a.YT[l], 0, H / 32);
-        if (p == a.s - 1) copy_image(x_addr, k_pad, a.XT, xs_mid, xs_total);
+        if (!XC && p == a.s - 1) copy_image(x_addr, k_pad, a.XT, xs_mid, xs_total);
         if (head_phase) {
           copy_image(act_addr, H, a.dZT[L - 2], 0, H / 32);
           copy_out(cs, a.colsum[L - 2] + (int64_t)blockIdx.x * H, H * 4);
@@ -789,25 +850,27 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   }
 }
 
-template <int H, int LOSS, bool ENC>
+template <int H, int LOSS, bool ENC, bool XC>
 int launch3_enc(const Chain3Args& a, hipStream_t stream) {
   using C = L3<H>;
-  const int lds = C::lds_bytes(a.L, a.k_pad);
+  const int lds = C::lds_bytes(a.L, a.kc);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
-  chain3_kernel<H, LOSS, ENC><<<dim3((unsigned)(a.rows / C3BM)), dim3(C3_THREADS), lds, stream>>>(a);
+  chain3_kernel<H, LOSS, ENC, XC><<<dim3((unsigned)(a.rows / C3BM)), dim3(C3_THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
 
 template <int H, int LOSS>
 int launch3_loss(const Chain3Args& a, hipStream_t stream) {
-  return a.encoding != INF_ENC_NONE ? launch3_enc<H, LOSS, true>(a, stream) : launch3_enc<H, LOSS, false>(a, stream);
+  if (a.encoding != INF_ENC_NONE) return launch3_enc<H, LOSS, true, false>(a, stream);
+  if (a.kc < a.k_pad) return launch3_enc<H, LOSS, false, true>(a, stream);
+  return launch3_enc<H, LOSS, false, false>(a, stream);
 }
 
 // the loss is a template parameter: one branch-free head per loss type keeps the compute
@@ -821,7 +884,9 @@ int launch3_typed(const Chain3Args& a, hipStream_t stream) {
 
 }  // namespace
 
-int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream) {
+int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
+  Chain3Args a = a_in;
+  a.table_big = a.encoding == INF_ENC_NONE && a.num_vertices * (int64_t)a.k_pad * 2 >= ((int64_t)1 << 32);
   INF_CHECK_ARG(chain3_supported(a.H, a.L, a.k_pad, a.rows), "chain3: unsupported shape");
   INF_CHECK_ARG(bm == C3BM, "chain3: tile height");
   INF_CHECK_ARG(a.rows % bm == 0 && a.rows >= bm, "chain3: rows must be a multiple of the tile height");
@@ -833,8 +898,8 @@ int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream) {
   INF_CHECK_ARG(a.encoding == INF_ENC_NONE || a.encoding == INF_ENC_XYZ || a.enc_proj != nullptr,
                 "chain3: encoding projection missing");
   INF_CHECK_ARG(a.vid_dtype == INF_DTYPE_I32 || a.vid_dtype == INF_DTYPE_I64, "chain3: vertex id dtype");
-  INF_CHECK_ARG(a.encoding != INF_ENC_NONE || a.num_vertices * (int64_t)a.k_pad * 2 < (int64_t)1 << 31,
-                "chain3: table exceeds 2 GiB");
+  INF_CHECK_ARG(a.kc == a.k_pad || (a.kc == C3_KC && a.encoding == INF_ENC_NONE && a.nchunk == ceil_div(a.k_pad, C3_KC)),
+                "chain3: feature chunking");
   for (int i = 0; i < a.nblk; ++i) INF_CHECK_ARG(a.blk[i].img != nullptr, "chain3: weight image missing");
   // bias / output-layer rows are read as H/64-float vectors per lane
   for (int l = 0; l < a.L - 1; ++l) INF_CHECK_ARG((uintptr_t)a.bias[l] % 16 == 0, "chain3: bias alignment");

@@ -12,6 +12,11 @@ constexpr int C3_MAX_BLOCKS = 64;
 // operand of a block is the activation tile (a_x = 0) or the gathered feature tile X
 // (a_x = 1) from its 32-k block ak0 on; B is a fragment image (adam.hip WF / WTF) from
 // its k-block kb0 on.  `last`: the block ends phase `phase` (run its epilogue).
+// `flags` (chunked feature tile only, Chain3Args::kc < k_pad): C3F_SWAP exchanges the
+// layer-0 and Ly accumulators before the block; C3F_GATHER gathers feature chunk
+// flags >> C3F_CHUNK_SHIFT into the LDS tile first (both input layers stream over each
+// chunk once, so the table rows are read once per step).
+constexpr int C3F_SWAP = 1, C3F_GATHER = 2, C3F_CHUNK_SHIFT = 8;
 struct C3Block {
   const bf16* img;
   int32_t kb0;
@@ -19,7 +24,7 @@ struct C3Block {
   int32_t ak0;
   int32_t phase;
   int32_t last;
-  int32_t pad;
+  int32_t flags;
 };
 
 struct Chain3Args {
@@ -43,6 +48,10 @@ struct Chain3Args {
   int32_t encoding, enc_k, enc_ne, enc_in_dim;
   const float* enc_proj;
   const float* pos;
+  // feature columns held in LDS at a time: k_pad (whole tile) or C3_KC (chunked, k_pad >
+  // C3_KC: config D's k = 4096 tile is 128 KiB for 16 rays, above the LDS budget)
+  int32_t kc, nchunk;
+  int32_t table_big;  // table of 4 GiB or more: 64-bit row addresses (set by launch_chain3)
   // weight stream: phases 0..L-2 forward layer p, L-1.. dX of layer (L-2) - (p - (L-1))
   C3Block blk[C3_MAX_BLOCKS];
   int32_t nblk, nphase;
@@ -77,10 +86,16 @@ struct Chain3Args {
 inline int chain3_bm(int64_t) { return 16; }
 // Largest padded batch routed to it (above, the LDS-ring chain's taller tiles win).
 constexpr int64_t CHAIN3_MAX_ROWS = 8192;
+// Feature columns per LDS chunk when the whole 16 x k_pad tile does not fit (k_pad > C3_KC).
+constexpr int C3_KC = 1024;
+// Weight-stream blocks of a training step: the input layers' k_pad / (32 upl) blocks each,
+// one per hidden layer forward and backward.
+inline int chain3_blocks(int H, int L, int k_pad) { return 2 * (k_pad / H) + 2 * (L - 2); }
 inline bool chain3_supported(int H, int L, int k_pad, int64_t rows) {
   const int upl = H / 32;
   return (H == 128 || H == 256) && L >= 3 && L - 1 <= CHAIN_MAX_HIDDEN && rows <= CHAIN3_MAX_ROWS &&
-         k_pad % (32 * upl) == 0 && k_pad <= 1024;
+         k_pad % (32 * upl) == 0 && (k_pad <= C3_KC || C3_KC % (32 * upl) == 0) &&
+         chain3_blocks(H, L, k_pad) <= C3_MAX_BLOCKS;
 }
 
 int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream);

@@ -91,6 +91,7 @@ struct inf_plan {
   int saved_batch = 0, saved_bp = 0;
   bool saved = false;
   int last_chain = 0;  // fused chain of the last training step: 0 none, 2 LDS ring, 3 registers
+  bool stepped = false;
   const uint64_t* dbg_ranges = nullptr;
   int dbg_n = 0;
   unsigned long long* dbg_out = nullptr;
@@ -687,16 +688,20 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   const ParamSeg* w0 = p->weight_seg(0, 0);
   // the fused gather reads a device-resident bf16 table; the dW lgemm streams
   // K = Bp / dw_splits rays per block in 256-ray steps
+  // (the gather addresses table rows with 64-bit offsets: any table size; the extrinsic
+  // front-ends keep their encoded tile whole in LDS, in_dim <= C3_KC)
   return use_chain(p) && chain3_supported(p->H, p->L, p->k_pad, Bp) && w1 != nullptr && w1->f_off >= 0 &&
          w0->f_off >= 0 && b->table != nullptr &&
          (b->encoding == INF_ENC_NONE ? b->table_dtype == INF_DTYPE_BF16
-                                      : (b->table_dtype == INF_DTYPE_F32 && b->vids != nullptr)) &&
+                                      : (b->table_dtype == INF_DTYPE_F32 && b->vids != nullptr && p->k_pad <= C3_KC)) &&
          (Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0 && std::getenv("INF_NO_CHAIN3") == nullptr;
 }
 
 // Fused gather + forward + loss + dX chain of a bf16 training batch (csrc/chain3.hip).
 // Weight stream: layer 0 over X (k_pad / 32 k-blocks of W_0), the hidden layers (the skip
 // layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
+// k_pad > C3_KC (config D): X is streamed in C3_KC-column chunks and phase 0 runs W_y then
+// W_0 over each chunk (W_y x kept in the second accumulator set until the skip layer).
 int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
   const int H = p->H, L = p->L, s = p->s;
   const int upl = H / 32;
@@ -751,11 +756,32 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     return INF_OK;
   };
   int rc;
-  for (int i = 0; i < nx; ++i)
-    if ((rc = add(img(p->weight_seg(0, 0), true), i * upl, 1, i * upl, 0, i == nx - 1))) return rc;
+  const bool xc = p->k_pad > C3_KC;
+  a.kc = xc ? C3_KC : p->k_pad;
+  a.nchunk = (int)ceil_div(p->k_pad, a.kc);
+  if (!xc) {
+    for (int i = 0; i < nx; ++i)
+      if ((rc = add(img(p->weight_seg(0, 0), true), i * upl, 1, i * upl, 0, i == nx - 1))) return rc;
+  } else {
+    INF_CHECK_ARG(b->encoding == INF_ENC_NONE, "chain3: chunked feature tiles are eigenfunction tables only");
+    for (int c = 0; c < a.nchunk; ++c) {
+      const int nb = std::min(C3_KC, p->k_pad - c * C3_KC) / (32 * upl);  // stream blocks of the chunk
+      const int kb = c * (C3_KC / 32);
+      for (int i = 0; i < nb; ++i) {
+        if ((rc = add(img(p->weight_seg(s, 1), true), kb + i * upl, 1, i * upl, 0, 0))) return rc;
+        if (i == 0) a.blk[a.nblk - 1].flags = C3F_SWAP | (c > 0 ? C3F_GATHER | (c << C3F_CHUNK_SHIFT) : 0);
+      }
+      for (int i = 0; i < nb; ++i) {
+        if ((rc = add(img(p->weight_seg(0, 0), true), kb + i * upl, 1, i * upl, 0,
+                      c == a.nchunk - 1 && i == nb - 1)))
+          return rc;
+        if (i == 0) a.blk[a.nblk - 1].flags = C3F_SWAP;
+      }
+    }
+  }
   for (int l = 1; l <= L - 2; ++l) {
-    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, l != s))) return rc;
-    if (l == s)
+    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || l != s))) return rc;
+    if (l == s && !xc)
       for (int i = 0; i < nx; ++i)
         if ((rc = add(img(p->weight_seg(s, 1), true), i * upl, 1, i * upl, l, i == nx - 1))) return rc;
   }
@@ -1056,6 +1082,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     p->saved_bp = Bp;
     ck = 3;
     nloss = Bp / chain3_bm(Bp);
+    p->stepped = true;
     if (std::getenv("INF_FUSED_UPDATE") != nullptr) {
       p->last_chain = 3;
       if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
@@ -1084,6 +1111,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     if ((rc = run_backward_layers(p, Bp0, st))) return rc;
   }
   p->last_chain = ck;
+  p->stepped = true;
   const int Bp = p->saved_bp;
   if ((rc = refresh_tables(p, Bp, st, ck))) return rc;
   return launch_update(step_update(Bp, nloss), p->mode, st);
@@ -1216,6 +1244,11 @@ int inf_debug_timing(inf_plan* p, unsigned long long* stamps, int max_steps) {
   p->stamps = stamps;
   p->stamp_steps = max_steps;
   return INF_OK;
+}
+
+int inf_plan_last_step_path(const inf_plan* p) {
+  if (p == nullptr || !p->stepped) return -1;
+  return p->last_chain == 3 && p->k_pad > C3_KC ? 4 : p->last_chain;
 }
 
 int inf_ctrl_advance(inf_plan* p, inf_stream_t stream) {

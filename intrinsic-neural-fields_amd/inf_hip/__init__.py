@@ -96,6 +96,7 @@ _SIGNATURES = {
     "inf_adam": (c_int, [c_void_p, c_int, c_float, c_void_p]),
     "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
+    "inf_plan_last_step_path": (c_int, [c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "inf_debug_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "inf_debug_block_times": (c_int, [c_void_p, c_void_p]),

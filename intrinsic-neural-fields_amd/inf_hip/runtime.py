@@ -398,6 +398,11 @@ class Plan:
                                 ctypes.byref(f), ctypes.byref(by), stream_handle()), "run_stage")
         return f.value, by.value
 
+    def last_step_path(self) -> str:
+        """Kernel path of the last train_step: 'layered', 'chain', 'chain3', 'chain3_chunked'."""
+        return {-1: None, 0: "layered", 2: "chain", 3: "chain3", 4: "chain3_chunked"}[
+            int(lib.inf_plan_last_step_path(self.handle))]
+
     def ctrl_advance(self):
         check(lib.inf_ctrl_advance(self.handle, stream_handle()), "ctrl_advance")
 

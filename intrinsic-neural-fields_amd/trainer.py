@@ -76,7 +76,11 @@ class _FusedEpoch:
         rt.ensure_optimizer_arenas()
         plan = model.hip_plan(B, loss_type)
         use_graph = os.environ.get("INF_GRAPH", "1") != "0" and full >= 2
-        key = (id(plan), B, N, loss_type, id(loader.source))
+        # the captured graph bakes in the plan's workspace / ctrl / shadow pointers and the
+        # source's tables: the key holds the objects themselves (compared by identity), so a
+        # plan replaced by hip_plan() (a larger render batch, another kernel mode) is never
+        # freed and its address reused under a stale graph
+        key = (plan, B, N, loss_type, loader.source)
         if self.perm is None or self.perm.numel() != N or self.perm.device != rt.device:
             self.perm = torch.empty(N, dtype=torch.int64, device=rt.device)
         self.perm.copy_(loader.idxs)
@@ -85,7 +89,9 @@ class _FusedEpoch:
         done = 0
         if use_graph:
             optim.sync_runtime_state(model, rt, plan, group)
-            if self.graph is None or self.key != key:
+            stale = self.key is None or self.key[0] is not plan or self.key[4] is not loader.source or \
+                self.key[1:4] != key[1:4]
+            if self.graph is None or stale:
                 self._capture(plan, loader, B, loss_type)
                 self.key = key
             optim.sync_runtime_state(model, rt, plan, group)
