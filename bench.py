@@ -300,6 +300,44 @@ def config_d_bench(args, device, B=4096, steps=40):
     return out
 
 
+def _secondary_train(args, device, B, steps, **over):
+    """Graph-replayed fused steps of another configuration: rays/s, kernel path, step
+    roofline (both terms)."""
+    import copy
+    a = copy.copy(args)
+    for kk, v in over.items():
+        setattr(a, kk, v)
+    a.no_graph = False
+    tr = Trainer(a, device, B, 0, 1, nb=8)
+    tr.capture()
+    ms, _ = time_steps(tr, steps, 4, 1)
+    P = tr.plan.info.num_params
+    out = {"rays_per_step": B, "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s",
+           "path": tr.plan.last_step_path(), "dtype": a.mode,
+           "roofline": step_roofline(a.k, a.hidden, a.layers, B, P, ms, dtype=a.mode,
+                                     table_bytes=2 if a.mode == "bf16" else 4,
+                                     weight_bytes=2 if a.mode == "bf16" else 4)}
+    del tr
+    torch.cuda.empty_cache()
+    return out
+
+
+def config_a_bench(args, device):
+    """Config A (the reference's CPU-runnable cat case, k=64, 4x128, skip 2)
+    on the GPU, beside its CPU leg."""
+    out = _secondary_train(args, device, 4096, 80, k=64, layers=4, hidden=128, skip=2, verts=20_000)
+    out["config"] = "cat k=64 4x128 skip 2, L2, Adam, V=20000"
+    return out
+
+
+def fp32_mode_bench(args, device):
+    """The parity mode (exact-fp32 MFMA layered kernels: the mode that meets the 1e-4 RGB
+    bar) on the headline configuration, against the 157.3 TFLOP/s fp32 MFMA peak."""
+    out = _secondary_train(args, device, args.batch, 40, mode="fp32")
+    out["config"] = f"cat k={args.k} {args.layers}x{args.hidden} skip {args.skip}, L2, Adam, fp32 mode, V={args.verts}"
+    return out
+
+
 def render_bench(args, device):
     """Forward-only render slice (renderer.py:112-146) of a 2048x2048 frame at a 50 % hit
     rate over a V=400k table (config E): gather + MLP + placement into the image."""
@@ -352,8 +390,22 @@ def render_bench(args, device):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    # both t_min terms of the frame: forward FLOPs of the hits vs the
+    # dense MFMA peak; table rows + ids / bary / hit index per hit, the image (fill + pixel
+    # writes) and one pass of the bf16 weights vs HBM
+    L, Hd, k = args.layers, args.hidden, args.k
+    k_pad = -(-k // 128) * 128
+    fwd = 2 * (2 * k * Hd + (L - 2) * Hd * Hd + 3 * Hd)
+    flops = nhit * fwd
+    byts = nhit * (3 * k_pad * 2 + 12 + 12 + 8 + 12) + H * W * 12 + 2 * (2 * k_pad * Hd + (L - 2) * Hd * Hd)
+    t_mfma = flops / (PEAK[args.mode] * 1e12) * 1e3
+    t_hbm = byts / (HBM_PEAK * 1e9) * 1e3
+    roof = {"flops": flops, "bytes": byts, "t_mfma_ms": t_mfma, "t_hbm_ms": t_hbm,
+            "bound": "mfma" if t_mfma >= t_hbm else "hbm", "mfma_frac": t_mfma / ms, "hbm_frac": t_hbm / ms,
+            "frac": max(t_mfma, t_hbm) / ms, "achieved_tflops": flops / (ms * 1e-3) / 1e12,
+            "achieved_gbs": byts / (ms * 1e-3) / 1e9}
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
-            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams}
+            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams, "roofline": roof}
 
 
 def torus_mesh(nu=640, nv=320, R=1.0, r=0.4):
@@ -506,67 +558,85 @@ def psnr_vs_ref(mode):
             "max_abs_delta_db": float(np.abs(val - ref).max())}
 
 
-def cpu_baseline(args):
-    """CPU baselines on this host's cores, config B at batch 4096, bounded samples of
-    ~cpu_seconds each: the reference's PyTorch-CPU op sequence (oracle/torch_cpu.py, the
-    reported value) and the numpy oracle (oracle/inf_oracle.py)."""
-    from oracle import inf_oracle as O
-    cores = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
-    rng = np.random.default_rng(0)
-    k, H, L, s, B, V = args.k, args.hidden, args.layers, args.skip, 4096, 20000
-    names = O.layer_names(L, s)
-    torch.manual_seed(0)
+def _cpu_weights(k, H, L, s):
     import model as M
+    torch.manual_seed(0)
     m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s})
-    w = {n: p.detach().numpy().copy() for n, p in m.named_parameters()}
-    assert set(w) == set(names)
-    E = rng.standard_normal((V, k)).astype(np.float32)
-    E /= (E.max(0) - E.min(0))
-    tr = O.OracleTrainer(w, L, s, 1e-4, "L2")
+    return {n: p.detach().numpy().copy() for n, p in m.named_parameters()}
+
+
+def _cpu_table(V, k, seed, device):
+    """The GPU legs' synthetic table (randn + the reference's column rescale), on the host:
+    drawn on the device for the large tables and copied over."""
+    if V * k > (1 << 26):
+        g = torch.Generator(device=device).manual_seed(seed)
+        E = torch.randn((V, k), generator=g, device=device)
+        E /= E.max(0, keepdim=True).values - E.min(0, keepdim=True).values
+        out = E.cpu()
+        del E
+        torch.cuda.empty_cache()
+        return out
+    g = torch.Generator().manual_seed(seed)
+    E = torch.randn((V, k), generator=g)
+    return E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
+
+
+def cpu_leg(kind, k, H, L, s, V, B, seconds, device, max_iters=400):
+    """The reference's PyTorch-CPU op sequence (oracle/torch_cpu.py: index + bmm gather,
+    F.linear layers with the concatenating skip, mse_loss, autograd, torch.optim.Adam) on
+    this host's cores, same configuration and table size as the GPU leg, a bounded sample of
+    ~`seconds`.  kind "train": steps of B rays -> rays/s; "render": forward of 2^15-hit
+    batches (renderer.py:112-146's batchify size) and the scatter into the image -> hits/s."""
+    from oracle import torch_cpu as T
+    cores = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    w = _cpu_weights(k, H, L, s)
+    E = _cpu_table(V, k, 1, device)
+    g = torch.Generator().manual_seed(0)
+    tt = T.TorchTrainer(w, L, s, 1e-4, "L2")
+    img = torch.ones((2048 * 2048, 3)) if kind == "render" else None
+
+    def rays(n):
+        vids = torch.randint(0, V, (n, 3), generator=g)
+        u = torch.rand((n, 3), generator=g).clamp_min(1e-12)
+        bary = -torch.log(u)
+        return vids, bary / bary.sum(1, keepdim=True)
 
     def one():
-        vids = rng.integers(0, V, (B, 3))
-        bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
-        rgb = rng.random((B, 3)).astype(np.float32)
-        tr.step(O.gather(E, vids, bary), rgb)
+        if kind == "train":
+            vids, bary = rays(B)
+            tt.step(T.gather(E, vids, bary), torch.rand((B, 3), generator=g))
+        else:
+            vids, bary = rays(B)
+            hit = torch.randint(0, img.shape[0], (B,), generator=g)
+            with torch.no_grad():
+                img[hit] = tt.forward(T.gather(E, vids, bary))
 
     one()
     t0 = time.perf_counter()
     n = 0
-    while time.perf_counter() - t0 < args.cpu_seconds and n < 200:
+    while time.perf_counter() - t0 < seconds and n < max_iters:
         one()
         n += 1
     dt = time.perf_counter() - t0
-    numpy_leg = {"value": n * B / dt, "unit": "rays/s", "cores": cores, "kind": "port",
-                 "sample": f"{n} oracle train steps (numpy fp32) of {B} rays, k={k} {L}x{H} skip {s}, V={V}, "
-                           f"{dt:.1f} s"}
+    what = "train steps" if kind == "train" else "forward + scatter batches"
+    return {"value": n * B / dt, "unit": "rays/s" if kind == "train" else "hits/s", "cores": cores, "kind": "port",
+            "sample": f"{n} {what} of the reference's PyTorch-CPU op sequence (oracle/torch_cpu.py, fp32) of {B} "
+                      f"rays, k={k} {L}x{H} skip {s}, V={V}, {dt:.1f} s"}
 
-    # the reference's own op sequence on a CPU device (torch index + bmm gather, F.linear
-    # layers, mse_loss, autograd, torch.optim.Adam): oracle/torch_cpu.py
-    from oracle import torch_cpu as T
-    torch.set_num_threads(cores)
-    tt = T.TorchTrainer(w, L, s, 1e-4, "L2")
-    Et = torch.from_numpy(E)
-    g = torch.Generator().manual_seed(0)
 
-    def one_torch():
-        vids = torch.randint(0, V, (B, 3), generator=g)
-        u = torch.rand((B, 3), generator=g).clamp_min(1e-12)
-        bary = -torch.log(u)
-        bary = bary / bary.sum(1, keepdim=True)
-        tt.step(T.gather(Et, vids, bary), torch.rand((B, 3), generator=g))
-
-    one_torch()
-    t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < args.cpu_seconds and n < 400:
-        one_torch()
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n * B / dt, "unit": "rays/s", "cores": cores, "kind": "port",
-            "sample": f"{n} train steps of the reference's PyTorch-CPU op sequence (oracle/torch_cpu.py, fp32) of "
-                      f"{B} rays, k={k} {L}x{H} skip {s}, V={V}, {dt:.1f} s",
-            "numpy_oracle": numpy_leg}
+def cpu_baselines(args, device):
+    """CPU baselines of SURVEY.md §8(d): configs A, B, D (train) and E (forward + scatter),
+    each at the GPU leg's table size.  B (the headline) is `cpu_baseline` proper."""
+    sec = args.cpu_seconds
+    H, L, s = args.hidden, args.layers, args.skip
+    out = {"B": cpu_leg("train", args.k, H, L, s, args.verts, 4096, sec, device)}
+    out["A"] = cpu_leg("train", 64, 128, 4, 2, 20_000, 4096, sec / 2, device)
+    out["D"] = cpu_leg("train", 4096, H, L, s, 500_000, 4096, sec, device, max_iters=100)
+    e = cpu_leg("render", args.k, H, L, s, 400_000, 1 << 15, sec, device)
+    e["pixels_per_s"] = e["value"] * 2  # the GPU leg's frame: 50 % of the pixels hit
+    out["E"] = e
+    return out
 
 
 def main():
@@ -655,13 +725,52 @@ def main():
         except Exception as exc:  # reported, never fatal to the throughput line
             psnr = {"error": repr(exc)}
 
-    cpu = None
+    secondary = {}
+    if rank == 0 and world == 1 and want("configs"):
+        secondary["A"] = config_a_bench(args, device)
+        if args.mode == "bf16":
+            secondary["fp32_mode_B"] = fp32_mode_bench(args, device)
+
+    cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and want("cpu"):
-        cpu = cpu_baseline(args)
+        cpu_all = cpu_baselines(args, device)
+        cpu = dict(cpu_all["B"])
+        cpu["other_configs"] = {kk: v for kk, v in cpu_all.items() if kk != "B"}
 
     if rank == 0:
         L, H, k = args.layers, args.hidden, args.k
-        flops_ray = 2 * (2 * (2 * k * H + (L - 2) * H * H + 3 * H) + (L - 2) * H * H + 3 * H)
+        k_pad = -(-k // 128) * 128
+        flops_ray = flops_per_ray(k, H, L)
+        B = args.batch
+
+        def stage_line(name, v):
+            ms_, fl, by = v
+            d = {"ms": ms_, "tflops": fl / (ms_ * 1e-3) / 1e12 if fl else None}
+            if fl:
+                d["mfma_frac"] = d["tflops"] / PEAK[args.mode]
+            if name == "chain3":
+                # run_stage's byte count is the L2 -> CU stream (every workgroup re-reads the
+                # weight images) plus HBM rows: reported as such, NOT as an HBM fraction.  The
+                # HBM term uses the algorithmic bytes: the table rows and per-ray records, one
+                # pass over the weight images, and the X^T / Y^T / dZ^T images + partials the
+                # unfused dW GEMM reads back (listed separately as intermediates)
+                rows = B * (3 * k_pad * 2 + 36)
+                weights = 2 * (2 * k_pad * H + 2 * (L - 2) * H * H)
+                inter = B * (k_pad + (2 * L - 3) * H) * 2 + (B // 16) * 4 * ((L - 1) * H + 3 * H)
+                d["l2_to_cu_gbs"] = by / (ms_ * 1e-3) / 1e9
+                d["hbm_alg_bytes"] = rows + weights
+                d["hbm_intermediate_bytes"] = inter
+                d["hbm_gbs"] = (rows + weights + inter) / (ms_ * 1e-3) / 1e9
+                d["hbm_frac"] = d["hbm_gbs"] / HBM_PEAK
+            elif by:
+                d["hbm_gbs"] = by / (ms_ * 1e-3) / 1e9
+                d["hbm_frac"] = d["hbm_gbs"] / HBM_PEAK
+            return d
+
+        stage_lines = {kk: stage_line(kk, v) for kk, v in stages.items()}
+        P = sum(x for x in (
+            k * H + H, (L - 3) * (H * H + H), H * H + H + k * H + H, 3 * H + 3))
+        dom_line = stage_lines[dom]
         line = {
             "metric": "training rays/sec (k=1024, 8x256 MLP)",
             "value": value,
@@ -685,14 +794,19 @@ def main():
             "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES[dom],
                          "achieved": achieved, "peak": PEAK[args.mode], "unit": "TFLOP/s",
                          "frac": achieved / PEAK[args.mode], "traffic": traffic,
-                         "avg_ms": dom_ms, "flops_per_launch": dom_flops},
-            "stages": {k: {"ms": v[0], "tflops": v[1] / (v[0] * 1e-3) / 1e12 if v[1] else None,
-                           "gbs": v[2] / (v[0] * 1e-3) / 1e9 if v[2] else None,
-                           "hbm_frac": v[2] / (v[0] * 1e-3) / 1e9 / HBM_PEAK if v[2] else None}
-                       for k, v in stages.items()},
+                         "avg_ms": dom_ms, "flops_per_launch": dom_flops,
+                         "hbm_term": {"alg_bytes": dom_line.get("hbm_alg_bytes"),
+                                      "intermediate_bytes": dom_line.get("hbm_intermediate_bytes"),
+                                      "achieved_gbs": dom_line.get("hbm_gbs"), "peak_gbs": HBM_PEAK,
+                                      "frac": dom_line.get("hbm_frac")}},
+            "step_roofline": step_roofline(k, H, L, B, P, ms, dtype=args.mode,
+                                           table_bytes=2 if args.mode == "bf16" else 4,
+                                           weight_bytes=2 if args.mode == "bf16" else 4),
+            "stages": stage_lines,
             "host_wall_ms_per_step": wall_ms,
             "large_batch": extra,
             "config_D": config_d,
+            "secondary": secondary,
             "render": render,
             "extrinsic_rff": extrinsic,
             "psnr_vs_ref": psnr,
