@@ -204,6 +204,67 @@ class Trainer:
         loss = self.loss_fn(pred_rgbs, batch["expected_rgbs"])
         return loss, pred_rgbs
 
+    # ---- visualisation (trainer.py:86-162) ---------------------------------------------
+    def write_vis_metrics_to_tensorboard(self, img_name, rendered_img, gt_img, obj_mask_1d, epoch):
+        """Reference trainer.py:86-104: the rendered view, its PSNR over the object mask,
+        the 2D mean-distance image and the summed absolute distance."""
+        from evaluation_metrics import psnr
+        mask = np.asarray(torch.as_tensor(obj_mask_1d).cpu()).reshape(-1).astype(bool)
+        self.writer.add_image(img_name, rendered_img.transpose(2, 0, 1), global_step=epoch)
+        self.writer.add_scalar(f"{img_name}_psnr", psnr(rendered_img, gt_img, mask), epoch)
+        mean_distance_2d = 1. - np.mean(np.abs(rendered_img - gt_img), -1)
+        self.writer.add_image(f"{img_name}_2d_mean_distance", np.repeat(mean_distance_2d[None, ...], 3, axis=0),
+                              global_step=epoch)
+        total_dist = np.abs(gt_img.reshape(-1, 3)[mask] - rendered_img.reshape(-1, 3)[mask]).sum()
+        self.writer.add_scalar(f"{img_name}_dist", total_dist, epoch)
+
+    @torch.no_grad()
+    def _render_view_for_tensorboard(self, input_path, img_name, epoch):
+        """Reference trainer.py:106-128: one validation view rendered on the device (rays
+        cast against the mesh, csrc/raycast.hip; shading by the plan's render path)."""
+        from utils import imread, load_cameras, load_obj_mask_as_tensor
+        obj_mask_1d = torch.as_tensor(load_obj_mask_as_tensor(input_path)).reshape(-1)
+        camCv2world, K = load_cameras(input_path)
+        rendered_img = self.renderer.render(camCv2world, K, obj_mask_1d=obj_mask_1d)
+        gt_img = imread(os.path.join(input_path, "image", "000.png"))[..., :3].astype(np.float32) / 255.
+        shape = gt_img.shape
+        gt_img = gt_img.reshape(-1, 3)
+        gt_img[obj_mask_1d.numpy() == False] = 1.  # noqa: E712
+        self.write_vis_metrics_to_tensorboard(img_name, rendered_img, gt_img.reshape(shape), obj_mask_1d, epoch)
+
+    @torch.no_grad()
+    def _render_views_for_tensorboard_meshroom_radial_k3(self, epoch):
+        """Reference trainer.py:130-156."""
+        from dataset import MeshroomRadialK3Dataset
+        ds = MeshroomRadialK3Dataset(self.config["data"]["vis_dataset_path"], self.config["data"]["vis_split"],
+                                     H=self.H, W=self.W)
+        for idx in range(len(ds)):
+            item = ds[idx]
+            rendered_img = self.renderer.render(item["camCv2world"], item["K"],
+                                                distortion_coeffs=item["distortion_params"],
+                                                distortion_type=item["distortion_type"])
+            self.write_vis_metrics_to_tensorboard(f"meshroom_radial_k3_view_{idx}", rendered_img, item["img"].numpy(),
+                                                  item["obj_mask_1d"], epoch)
+
+    def _visualize(self, epoch):
+        """trainer.py:285-300."""
+        if self.renderer is None or getattr(self.renderer, "mesh", None) is None:
+            if not self._render_note:
+                print("Visualizing... skipped: no mesh to cast the validation views against (data.mesh_path)")
+                self._render_note = True
+            return
+        self.model.eval()
+        print("Visualizing...")
+        t0 = time.time()
+        if self.dataset_type is None:
+            for i, (input_path, _name) in enumerate(self.val_render_infos):
+                self._render_view_for_tensorboard(input_path, f"img{i:03d}", epoch)
+        elif self.dataset_type == "meshroom_radial_k3":
+            self._render_views_for_tensorboard_meshroom_radial_k3(epoch)
+        else:
+            raise NotImplementedError(f"Unknown dataset type: {self.dataset_type}!")
+        print(f"Done with visualizations after {time.time() - t0} seconds.")
+
     def evaluate(self, epoch=None):
         """Reference trainer.py:164-187 (sums kept on the device, one sync)."""
         self.model.eval()
@@ -298,9 +359,8 @@ class Trainer:
                 print(f"Epoch: {epoch + 1} / {self.epochs}, Train Loss: {train_loss}, Train PSNR: {train_psnr}, "
                       f"Val Loss: {val_loss}, Val PSNR: {val_psnr}"
                       f"Epoch Time: {t1 - t0}s")
-            if (epoch == 0 or (epoch + 1) % self.render_every == 0) and not self._render_note:
-                print("Visualizing... skipped: view rendering needs ray casting (outside this build's hot path)")
-                self._render_note = True
+            if epoch == 0 or (epoch + 1) % self.render_every == 0:
+                self._visualize(epoch)
             if self.checkpoint_every is not None and epoch % self.checkpoint_every == 0:
                 print("Saving checkpoint...")
                 torch.save(self._checkpoint_dict(epoch), self.checkpoint_path)

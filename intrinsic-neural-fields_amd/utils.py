@@ -1,9 +1,13 @@
-"""Host mirror of the reference utils.py -- the helpers on the hot path.
+"""Host mirror of the reference utils.py.
 
-load_trained_model (utils.py:22-29), model_summary (:39-41), batchify_dict_data
-(:72-83) and to_device (:137-144).  Camera / mask / depth IO (:32-36, 44-69) and the
-tandem helpers are outside this build's scope.
+load_trained_model (utils.py:22-29), load_cameras (:32-36), model_summary (:39-41),
+load_obj_mask_as_tensor (:44-61), batchify_dict_data (:72-83) and to_device (:137-144).
+Images are read with PIL (imageio is not installed here); the reference's OpenEXR depth
+maps need imageio's freeimage plugin, so a view's object mask is read from
+depth/mask.png (the reference's own fallback, utils.py:55-58) or an .npy file, and an
+EXR-only view raises.  The tandem helpers are outside this build's scope.
 """
+import os
 import sys
 
 import numpy as np
@@ -25,6 +29,39 @@ def load_trained_model(model_config, weights_path, device, mesh=None):
     else:
         model.load_state_dict(data)
     return model.to(device)
+
+
+def load_cameras(view_path):
+    """Reference utils.py:32-36: camCv2world and K of a view (depth/cameras.npz)."""
+    cameras = np.load(os.path.join(view_path, "depth", "cameras.npz"))
+    camCv2world = torch.from_numpy(cameras["world_mat_0"]).to(dtype=torch.float32)
+    K = torch.from_numpy(cameras["camera_mat_0"]).to(dtype=torch.float32)
+    return camCv2world, K
+
+
+def imread(path):
+    """An image file as a numpy array (PIL; uint8 for PNG / JPEG)."""
+    from PIL import Image
+    with Image.open(path) as im:
+        return np.asarray(im)
+
+
+def load_obj_mask_as_tensor(view_path):
+    """Reference utils.py:44-61: the view's object mask (H x W bool).  A .npy path is
+    loaded as is; a view directory uses depth/depth_0000.exr (depth != 1e10) when present
+    -- which needs imageio's EXR plugin, absent here -- else depth/mask.png (!= 0)."""
+    if view_path.endswith(".npy"):
+        return np.load(view_path)
+    mask_path = os.path.join(view_path, "depth", "mask.png")
+    depth_path = os.path.join(view_path, "depth", "depth_0000.exr")
+    if os.path.exists(depth_path) and not os.path.exists(mask_path):
+        raise NotImplementedError(f"{depth_path}: OpenEXR depth maps need imageio's freeimage plugin, which is not "
+                                  "installed; provide depth/mask.png")
+    assert os.path.exists(mask_path), "Must have depth or mask"
+    mask = imread(mask_path)
+    if mask.ndim == 3:
+        mask = mask[..., 0]
+    return torch.from_numpy(mask != 0)
 
 
 def model_summary(model, data):
