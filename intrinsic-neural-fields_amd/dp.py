@@ -1,5 +1,9 @@
 """Data parallelism: one process per GPU, gradients all-reduced over RCCL.
 
+Shapes of the exchange: replicated parameters / Adam state, the same
+shuffle on every rank, a torch.chunk split of every global batch, one flat fp32 gradient
+all-reduce per step (3.68 MB at k=1024 8x256).
+
 Replaces `torch.nn.DataParallel(model, device_ids)` (reference train.py:46-48), which
 scatters each global batch over the GPUs of one process, gathers the predictions to
 GPU 0 and computes the loss there over the GLOBAL batch, so the gradient is the mean over
@@ -46,10 +50,10 @@ def allreduce_grads(flat_grads: torch.Tensor, group=None) -> torch.Tensor:
     return flat_grads
 
 
-def allreduce_scalars(values, device) -> list:
+def allreduce_scalars(values, device, group=None) -> list:
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, group=group)
     return [float(x) for x in t.cpu()]
 
 
@@ -78,73 +82,163 @@ def render_distributed(renderer, camCv2world, K, obj_mask_1d=None, group=None):
     return torch.cat([parts[r][:shard_span(H, r, world)[1] - shard_span(H, r, world)[0]] for r in range(world)])
 
 
-class DataParallelTrainer:
-    """Fused training epochs of one TextureField replica (see module docstring)."""
+class DataParallelEpoch:
+    """The training epoch of one rank under `train.py --data_parallel` (nn.DataParallel's
+    role, reference train.py:46-48), plugged into trainer.Trainer, which keeps its
+    evaluation, best-model tracking, checkpoints, visualisation and scalars (rank 0 writes).
 
-    def __init__(self, model, optim, loss_type: str, loader, seed: int = 0):
-        self.model, self.optim, self.loss_type, self.loader, self.seed = model, optim, loss_type, loader, seed
-        self.rank = dist.get_rank() if dist.is_initialized() else 0
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
+    Per epoch: the loader's own shuffle (randperm, trainer.py:248 via
+    ray_dataloader.py:105) is drawn on rank 0 and broadcast, so every rank walks the same
+    batches; rank r takes its torch.chunk shard of each global batch; its shard rows of the
+    full batches are laid out contiguously so a captured graph replays the epoch with the
+    batch index advancing on the device.  One step = the fused gather -> forward -> loss
+    (normalised by the GLOBAL 3 x B) -> backward -> slab reduction into the flat gradient,
+    the flat-gradient all-reduce over RCCL, then Adam and the batch advance -- GRAPH_STEPS
+    steps per graph replay, the collective captured inside (no host round trip per step).
+    Replicas stay bitwise equal without parameter broadcasts.  A partial last batch
+    (drop_last=False) runs eagerly."""
 
-    def train_epoch(self, epoch: int):
-        ld = self.loader
-        B, N = ld.B, ld.N
-        nb = len(ld)
-        perm = epoch_permutation(N, self.seed, epoch, ld.device)
-        model, optim = self.model, self.optim
+    GRAPH_STEPS = 8
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.graph = None
+        self.key = None
+        self.idx = None
+        self.steps_done = 0
+
+    def _tail_all_reduce(self, rt, plan):
+        allreduce_grads(rt.grads, self.group)
+        plan.adam(0, 0.0)
+        plan.ctrl_advance()
+
+    def _capture(self, plan, rt, batch):
+        saved = [x.clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl)]
+        plan.set_batch_index(0)
+        plan.train_step(batch, None, apply_adam=False)  # settles the plan's tables before capture
+        self._tail_all_reduce(rt, plan)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                plan.train_step(batch, None, apply_adam=False)
+                self._tail_all_reduce(rt, plan)
+            with torch.cuda.graph(gm, stream=s):
+                for _ in range(self.GRAPH_STEPS):
+                    plan.train_step(batch, None, apply_adam=False)
+                    self._tail_all_reduce(rt, plan)
+        torch.cuda.current_stream().wait_stream(s)
+        for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
+            dst.copy_(src)
+        plan.sync_shadow()
+        self.graph = (g1, gm)
+
+    def run(self, trainer, loader):
+        """One epoch; returns (train loss, summed squared error / rays) over ALL ranks' rays,
+        as the reference's single-process loop reports them (trainer.py:248-263)."""
+        model, optim = trainer.model, trainer.optim
+        loss_type = trainer.loss_fn.loss_type
+        B, N = loader.B, loader.N
+        iter(loader)  # the reference's per-epoch reshuffle (ray_dataloader.py:103-106)
+        perm = loader.idxs
+        if self.world > 1:
+            perm = perm.contiguous()
+            dist.broadcast(perm, 0, group=self.group)
+        nb = len(loader)
+        full = N // B
+        lo, hi = shard_span(B, self.rank, self.world)
+        bs = hi - lo
+        if bs < 1:
+            raise ValueError(f"global batch {B} too small for {self.world} ranks")
         rt = model.hip_runtime()
         group = optim.fused_group_for(model)
         rt.ensure_optimizer_arenas()
-        lo, hi = shard_span(B, self.rank, self.world)
-        plan = model.hip_plan(max(hi - lo, 1), self.loss_type)
+        plan = model.hip_plan(bs, loss_type)
+        rows = perm[:full * B].view(full, B)[:, lo:hi].reshape(-1)
+        if self.idx is None or self.idx.numel() != rows.numel() or self.idx.device != rows.device:
+            self.idx = torch.empty_like(rows)
+        self.idx.copy_(rows)
         optim.sync_runtime_state(model, rt, plan, group)
         plan.reset_epoch_sums()
-        total = 0
-        for i in range(nb):
-            b0 = i * B
-            gb = min(B, N - b0)
+        steps = 0
+        use_graph = os.environ.get("INF_GRAPH", "1") != "0" and full >= 2
+        if full:
+            batch = plan.make_batch(source=loader.source, ray_idx=self.idx, offset=0, batch=bs,
+                                    offset_from_ctrl=True, loss_count=3 * B, loss=loss_type)
+            if use_graph:
+                key = (plan, bs, full, loss_type, loader.source, self.idx.data_ptr())
+                stale = self.key is None or self.key[0] is not plan or self.key[4] is not loader.source or \
+                    self.key[1:4] != key[1:4] or self.key[5] != key[5]
+                if self.graph is None or stale:
+                    self._capture(plan, rt, batch)
+                    self.key = key
+                optim.sync_runtime_state(model, rt, plan, group)
+                plan.reset_epoch_sums()
+                plan.set_batch_index(0)
+                g1, gm = self.graph
+                for _ in range(full // self.GRAPH_STEPS):
+                    gm.replay()
+                for _ in range(full % self.GRAPH_STEPS):
+                    g1.replay()
+            else:
+                plan.set_batch_index(0)
+                for _ in range(full):
+                    plan.train_step(batch, None, apply_adam=False)
+                    self._tail_all_reduce(rt, plan)
+            steps = full
+        if nb > full:  # partial last batch (drop_last=False), eager
+            gb = N - full * B
             slo, shi = shard_span(gb, self.rank, self.world)
             if shi > slo:
-                b = plan.make_batch(source=ld.source, ray_idx=perm, offset=b0 + slo, batch=shi - slo,
-                                    loss_count=3 * gb, loss=self.loss_type)
+                b = plan.make_batch(source=loader.source, ray_idx=perm, offset=full * B + slo, batch=shi - slo,
+                                    loss_count=3 * gb, loss=loss_type)
                 plan.train_step(b, None, apply_adam=False)
             else:  # an empty shard still joins the all-reduce with a zero gradient
                 rt.grads.zero_()
-                plan.set_step(rt.dev_step + 1)
-            allreduce_grads(rt.grads)
+                plan.set_step(rt.dev_step + full + 1)
+            allreduce_grads(rt.grads, self.group)
             plan.adam(0, 0.0)
-            optim.after_fused_step(model, rt, group)
-            total += gb
+            steps += 1
+        optim.after_fused_steps(model, rt, group, steps)
+        self.steps_done += steps
         c = plan.read_ctrl()
-        loss_sum, sse = allreduce_scalars([c["epoch_loss"], c["epoch_sse"]], rt.device)
-        return loss_sum / (3 * total), sse / total
+        loss_sum, sse = allreduce_scalars([c["epoch_loss"], c["epoch_sse"]], rt.device, self.group)
+        return loss_sum / (3 * N if nb > full else 3 * full * B), sse / (N if nb > full else full * B)
 
 
-def main_distributed(config, seed):
-    """`train.py --data_parallel` under torchrun: one process per GPU."""
+def main_distributed(config, seed, allow_checkpoint_loading=False):
+    """`train.py --data_parallel` under torchrun: one process per GPU running the
+    reference's Trainer (trainer.py:232-337) with DataParallelEpoch for its epochs."""
     import random
 
     import numpy as np
 
-    from config import get_data, get_loss_fn, get_model_and_optim
-    from evaluation_metrics import epoch_psnr
+    from config import get_data, get_loss_fn, get_model_and_optim, get_renderer
+    from trainer import Trainer
+    from utils import model_summary
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = f"cuda:{local}"
-    data = get_data(config, device)
-    model, optim = get_model_and_optim(config, None, device)
-    loss_fn = get_loss_fn(config)
-    random.seed(seed)
-    np.random.seed(seed)
-    torch.manual_seed(seed)
-    dpt = DataParallelTrainer(model, optim, loss_fn.loss_type, data["train"], seed)
-    out_dir = config["training"]["out_dir"]
-    for epoch in range(config["training"]["epochs"]):
-        train_loss, mse = dpt.train_epoch(epoch)
-        if dpt.rank == 0:
-            print(f"Epoch: {epoch + 1} / {config['training']['epochs']}, Train Loss: {train_loss}, "
-                  f"Train PSNR: {epoch_psnr(mse)}")
-    if dpt.rank == 0:
-        torch.save(model.state_dict(), os.path.join(out_dir, "model_last_epoch.pt"))
-    dist.destroy_process_group()
+    try:
+        mesh_path = config["data"].get("mesh_path")
+        mesh = None
+        if mesh_path is not None and os.path.exists(mesh_path):
+            from mesh import load_mesh
+            mesh = load_mesh(mesh_path)
+        data = get_data(config, device)
+        model, optim = get_model_and_optim(config, mesh, device)
+        if dist.get_rank() == 0:
+            model_summary(model, data)
+        loss_fn = get_loss_fn(config)
+        renderer = get_renderer(config, model, mesh, device)
+        random.seed(seed)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        trainer = Trainer(model, optim, loss_fn, renderer, data, mesh, config, device, dp=DataParallelEpoch())
+        trainer.train()
+    finally:
+        dist.destroy_process_group()

@@ -2,9 +2,11 @@
 
 `LinearWithConcatAndActivation` (reference layers.py:50-62) keeps the reference's
 module structure (Lx, Ly, actn, batchnorm) so TextureField's parameter names, order
-and seeded initialisation are identical.  Its arithmetic, relu(Lx(h) + Ly(x)), runs
-fused inside TextureField's HIP forward as ONE GEMM over the concatenated K = H + k
-(csrc/plan.hip run_forward_layer); it has no standalone CPU implementation.
+and seeded initialisation are identical.  Inside TextureField its arithmetic,
+relu(Lx(h) + Ly(x)), runs fused in the plan's kernels (one accumulator over the two K
+segments, csrc/chain3.hip / plan.hip run_forward_layer); called on its own it runs as one
+HIP dense-layer launch over both segments (csrc/dense.hip via dense.linear, with
+autograd).
 
 The position encoders FourierFeatEnc / RandomFourierFeatEnc (reference layers.py:6-39)
 keep the reference's constructor, buffers (`freq_bands` non-persistent, `B` persistent,
@@ -78,5 +80,14 @@ class LinearWithConcatAndActivation(nn.Module):
             self.batchnorm = nn.BatchNorm1d(out_dim)
 
     def forward(self, x, y):
-        raise RuntimeError("LinearWithConcatAndActivation runs fused inside TextureField's HIP forward "
-                           "(one GEMM over [h | x]); it is not callable on its own in this build")
+        """actn(Lx(x) + Ly(y)) (layers.py:60-62): both products into one output with the
+        ReLU in the epilogue.  BatchNorm (unused by every config) is not implemented."""
+        import dense
+        if self.batchnorm is not None:
+            raise NotImplementedError("batchnorm=True is not used by any intrinsic config and is not implemented")
+        if not isinstance(self.actn, nn.ReLU):
+            raise NotImplementedError("only the ReLU activation is implemented")
+        lead = x.shape[:-1]
+        out = dense.linear([(x.reshape(-1, x.shape[-1]), 0, 0), (y.reshape(-1, y.shape[-1]), 1, 0)],
+                           [self.Lx.weight, self.Ly.weight], [self.Lx.bias, self.Ly.bias], "relu")
+        return out.view(*lead, out.shape[-1])

@@ -5,7 +5,8 @@
 --data_parallel: the reference wraps the model in torch.nn.DataParallel (train.py:46-48).
 Here data parallelism is one process per GPU (launch with torchrun); the global batch
 of the YAML is split evenly over the ranks and the gradients are all-reduced over RCCL
-before the Adam step (see dp.py).  Without torchrun the flag is a no-op on one GPU.
+before the Adam step, inside the same Trainer (evaluation, checkpoints, scalars and
+models from rank 0; see dp.py).  Without torchrun the flag is a no-op on one GPU.
 """
 import argparse
 import os
@@ -37,7 +38,7 @@ def main():
     if not torch.cuda.is_available():
         raise RuntimeError("this build trains on MI355X (HIP) devices; no GPU is visible")
     device = "cuda"
-    if args.data_parallel and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if args.data_parallel and "WORLD_SIZE" in os.environ:  # launched by torchrun
         import dp
         return dp.main_distributed(config, seed)
     # train.py:38 loads the mesh: the renderer casts against it and the extrinsic

@@ -44,6 +44,17 @@ class _JsonlWriter:
         pass
 
 
+class _NullWriter:
+    """Ranks other than 0 of a data-parallel run log nothing (rank 0 logs the all-reduced
+    epoch metrics)."""
+
+    def add_scalar(self, *args, **kwargs):
+        pass
+
+    def add_image(self, *args, **kwargs):
+        pass
+
+
 def _summary_writer(log_dir):
     try:
         from tensorboardX import SummaryWriter
@@ -105,7 +116,10 @@ class _FusedEpoch:
             optim.after_fused_steps(model, rt, group, full)
             done = full
             total = full * B
-        for i, batch in enumerate(it):
+        # next() on the loader itself: a second iter() (as `for batch in it` would call)
+        # reshuffles, and the reference draws ONE permutation per epoch (trainer.py:248)
+        for i in range(nb):
+            batch = next(it)
             if i < done:
                 continue
             model.fused_train_step(batch, optim, loss_type, want_pred=False)
@@ -139,7 +153,11 @@ class _FusedEpoch:
 
 
 class Trainer:
-    def __init__(self, model, optim, loss_fn, renderer, data, mesh, config, device):
+    def __init__(self, model, optim, loss_fn, renderer, data, mesh, config, device, dp=None):
+        # dp: dp.DataParallelEpoch under `train.py --data_parallel` (one process per GPU):
+        # it runs the training epochs; rank 0 writes logs, checkpoints and models
+        self.dp = dp
+        self.rank0 = dp is None or dp.rank == 0
         self.model = model
         self.optim = optim
         self.loss_fn = loss_fn
@@ -159,8 +177,11 @@ class Trainer:
         self.test_data_loader = data.get("test", None)
         self.out_dir = self.config["training"]["out_dir"]
         log_dir = os.path.join(self.out_dir, "logs")
-        os.makedirs(log_dir, exist_ok=True)
-        self.writer = _summary_writer(log_dir)
+        if self.rank0:
+            os.makedirs(log_dir, exist_ok=True)
+            self.writer = _summary_writer(log_dir)
+        else:
+            self.writer = _NullWriter()
         self.render_every = self.config["training"]["render_every"]
         self.print_every = self.config["training"]["print_every"]
         self.epochs = self.config["training"]["epochs"]
@@ -323,6 +344,11 @@ class Trainer:
         return checkpoint["epoch"] + 1
 
     def _train_epoch(self):
+        if self.dp is not None:
+            if not (self._can_fuse() and hasattr(self.train_data_loader, "source")):
+                raise NotImplementedError("--data_parallel runs the fused TextureField step (HIP Adam, L1/L2/cauchy "
+                                          "loss, a RayDataLoader)")
+            return self.dp.run(self, self.train_data_loader)
         if self._can_fuse() and hasattr(self.train_data_loader, "source"):
             return self._fused_epoch.run(self.train_data_loader)
         acc_loss, acc_l2, total = 0.0, 0.0, 0
@@ -337,7 +363,8 @@ class Trainer:
 
     def train(self):
         """Reference trainer.py:232-337."""
-        print("Starting training...")
+        if self.rank0:
+            print("Starting training...")
         epoch_start = self._init_or_load_checkpoint()
         min_val_loss = 1.
         for epoch in range(epoch_start, self.epochs):
@@ -351,10 +378,13 @@ class Trainer:
             val_loss, val_psnr = self.evaluate(epoch)
             if val_loss < min_val_loss:
                 min_val_loss = val_loss
-                torch.save(self.model.state_dict(), self.best_model_weights_path)
+                if self.rank0:
+                    torch.save(self.model.state_dict(), self.best_model_weights_path)
                 self.best_model = copy.deepcopy(self.model)
             if self.use_lr_scheduler:
                 self.lr_scheduler.step(val_loss)
+            if not self.rank0:
+                continue
             if epoch == 0 or (epoch + 1) % self.print_every == 0:
                 print(f"Epoch: {epoch + 1} / {self.epochs}, Train Loss: {train_loss}, Train PSNR: {train_psnr}, "
                       f"Val Loss: {val_loss}, Val PSNR: {val_psnr}"
@@ -372,5 +402,6 @@ class Trainer:
                 torch.save(best.state_dict(), os.path.join(self.out_dir, f"best_model_checkpoint_{epoch}.pt"))
                 print("Done.")
         self.test()
-        print("Done.")
-        torch.save(self.model.state_dict(), self.model_last_epoch_path)
+        if self.rank0:
+            print("Done.")
+            torch.save(self.model.state_dict(), self.model_last_epoch_path)

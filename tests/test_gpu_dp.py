@@ -1,0 +1,115 @@
+"""Data-parallel training on the GPU (dp.py): the Trainer's data-parallel epochs at world
+size 1 are bitwise its single-GPU fused epochs, and `train.py --data_parallel` under
+torchrun (an RCCL communicator, the collective captured in the step graphs) writes the
+same models and scalars as the single-process run.  World sizes above one are covered by
+tests/test_dp_gloo.py on the CPU (no multi-GPU box is available to this suite)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "intrinsic-neural-fields_amd")
+
+
+def _loaders(B, N, drop_last, k=64, V=500, seed=8):
+    from ray_dataloader import RayDataLoader
+    rng = np.random.default_rng(seed)
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32))
+    vids = torch.from_numpy(rng.integers(0, V, (N, 3)))
+    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32))
+    rgb = torch.from_numpy(rng.random((N, 3)).astype(np.float32))
+    tr = RayDataLoader(E, "efuncs", vids, bary, rgb, None, None, B, True, drop_last, device="cuda")
+    va = RayDataLoader(E, "efuncs", vids[:1000], bary[:1000], rgb[:1000], None, None, B, False, False, device="cuda")
+    return tr, va
+
+
+@pytest.mark.parametrize("mode,drop_last", [("bf16", True), ("fp32", False)])
+def test_dp_epochs_world1_bitwise_single_gpu(tmp_path, mode, drop_last):
+    """Trainer(dp=DataParallelEpoch()) without a process group (world 1): the reduce ->
+    (identity) all-reduce -> Adam step shape, graph-replayed, leaves exactly the
+    parameters, Adam state and epoch metrics of the plain fused epochs."""
+    import config
+    import dp
+    from trainer import Trainer
+    B, N = 1024, 9 * 1024 + (0 if drop_last else 300)
+    outs = {}
+    for tag in ("single", "dp"):
+        cfg = {"data": {"img_height": 8, "img_width": 8},
+               "model": {"k": 64, "num_layers": 4, "mlp_hidden_dim": 128, "skip_layer_idx": 2,
+                         "kernels": {"mode": mode}},
+               "training": {"out_dir": str(tmp_path / tag), "batch_size": B, "lr": 1e-3, "loss_type": "L1",
+                            "render_every": 100, "print_every": 100, "epochs": 3}}
+        torch.manual_seed(0)
+        model, optim = config.get_model_and_optim(cfg, None, "cuda")
+        model.kernel_mode = mode
+        tr_ld, va_ld = _loaders(B, N, drop_last)
+        t = Trainer(model, optim, config.get_loss_fn(cfg), None, {"train": tr_ld, "val": va_ld}, None, cfg, "cuda",
+                    dp=dp.DataParallelEpoch() if tag == "dp" else None)
+        torch.manual_seed(1)  # the loaders' shuffles
+        t.train()
+        rows = [json.loads(x) for x in open(tmp_path / tag / "logs" / "scalars.jsonl")]
+        st = optim.state_dict()["state"]
+        outs[tag] = ([(r["tag"], r["value"]) for r in rows],
+                     torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy(),
+                     torch.cat([st[i]["exp_avg_sq"].reshape(-1).cpu() for i in sorted(st)]).numpy(),
+                     float(st[0]["step"]))
+    s, d = outs["single"], outs["dp"]
+    assert s[3] == d[3] == 3 * (N // B + (0 if drop_last else 1))
+    np.testing.assert_array_equal(s[1], d[1])
+    np.testing.assert_array_equal(s[2], d[2])
+    assert [t for t, _ in s[0]] == [t for t, _ in d[0]]
+    np.testing.assert_allclose([v for _, v in s[0]], [v for _, v in d[0]], rtol=1e-12)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_train_data_parallel_torchrun_world1(tmp_path):
+    """`torchrun --nproc-per-node 1 train.py <cfg> --data_parallel` (RCCL process group,
+    all-reduce captured in the step graphs) vs `train.py <cfg>`: the same files, the same
+    final weights bit for bit, the same logged scalars."""
+    import synthetic_views as S
+    S.build(str(tmp_path), views=(4, 1, 1))
+    cfg = S.intrinsic_config(epochs=3, batch=512)
+    cfg["model"]["kernels"] = {"mode": "bf16"}
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    results = {}
+    for tag in ("single", "dp"):
+        cfg["training"]["out_dir"] = f"out/{tag}"
+        path = tmp_path / f"{tag}.yaml"
+        with open(path, "w") as fh:
+            yaml.safe_dump(cfg, fh)
+        if tag == "single":
+            cmd = [sys.executable, os.path.join(PKG, "train.py"), str(path)]
+        else:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(PKG, "train.py"),
+                   str(path), "--data_parallel"]
+        r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+        print(tag, r.stdout[-2000:], r.stderr[-2000:])
+        assert r.returncode == 0, tag
+        out = tmp_path / "out" / tag
+        files = sorted(os.listdir(out))
+        sd = torch.load(out / "model_last_epoch.pt", map_location="cpu", weights_only=True)
+        rows = [json.loads(x) for x in open(out / "logs" / "scalars.jsonl")]
+        results[tag] = (files, sd, rows)
+    (fs, ws, rs), (fd, wd, rd) = results["single"], results["dp"]
+    assert fs == fd and {"model.pt", "model_last_epoch.pt", "checkpoint.pt", "logs"} <= set(fs)
+    for k in ws:
+        assert torch.equal(ws[k], wd[k]), k
+    assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
+    np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=1e-9)

@@ -262,41 +262,3 @@ def test_fused_step_equals_autograd_step():
         outs.append((losses, torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy()))
     np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-5)
     np.testing.assert_allclose(outs[0][1], outs[1][1], atol=2e-6)
-
-
-def test_dp_trainer_single_rank_matches_fused_epoch():
-    """dp.DataParallelTrainer at world size 1 (RCCL path without peers) follows the same
-    arithmetic as the fused epoch: global-mean loss normalisation, reduce, Adam."""
-    import config
-    import dp
-    from ray_dataloader import RayDataLoader
-    rng = np.random.default_rng(8)
-    V, N, B = 500, 4096, 1024
-    E = torch.from_numpy(rng.standard_normal((V, 64)).astype(np.float32))
-    vids = torch.from_numpy(rng.integers(0, V, (N, 3)))
-    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32))
-    rgb = torch.from_numpy(rng.random((N, 3)).astype(np.float32))
-    cfg = {"model": {"k": 64, "num_layers": 4, "mlp_hidden_dim": 128, "skip_layer_idx": 2},
-           "training": {"batch_size": B, "lr": 1e-3, "loss_type": "L2"}}
-    torch.manual_seed(0)
-    model, optim = config.get_model_and_optim(cfg, None, "cuda")
-    model.kernel_mode = "fp32"
-    ld = RayDataLoader(E, "efuncs", vids, bary, rgb, None, None, B, True, True, device="cuda")
-    t = dp.DataParallelTrainer(model, optim, "L2", ld, seed=3)
-    loss, mse = t.train_epoch(0)
-    # oracle: same permutation, same batches
-    perm = dp.epoch_permutation(N, 3, 0, "cuda").cpu().numpy()
-    torch.manual_seed(0)
-    m2, _ = config.get_model_and_optim(cfg, None, "cpu")
-    w = {n: p.detach().numpy().copy() for n, p in m2.named_parameters()}
-    tr = O.OracleTrainer(w, 4, 2, 1e-3, "L2")
-    losses = []
-    for i in range(N // B):
-        idx = perm[i * B:(i + 1) * B]
-        lv, _, _ = tr.step(O.gather(E.numpy(), vids.numpy()[idx], bary.numpy()[idx]), rgb.numpy()[idx])
-        losses.append(lv)
-    assert abs(loss - np.mean(losses)) < 1e-5
-    for n, p in model.named_parameters():
-        d = np.abs(p.detach().cpu().numpy() - tr.w[n])
-        assert int((d > 5e-6).sum()) <= max(1e-3 * d.size, 4) and d.max() < 1e-2, n
-    assert float(optim.state_dict()["state"][0]["step"]) == N // B

@@ -89,3 +89,35 @@ def test_host_adam_step_with_zero_lr():
     for p, b, g, mb in zip(model.parameters(), before, grads, m_before):
         assert torch.equal(p.detach(), b)
         torch.testing.assert_close(optim.state[p]["exp_avg"], 0.9 * mb + 0.1 * g, rtol=1e-5, atol=1e-9)
+
+
+def test_one_shuffle_per_epoch(monkeypatch):
+    """The fused epoch draws exactly one permutation per epoch, as the reference's
+    `for batch in self.train_data_loader` (trainer.py:248, ray_dataloader.py:103-106):
+    eager (INF_GRAPH=0) and graph-replayed epochs use the same batches and leave the same
+    global RNG state."""
+    import config
+    from ray_dataloader import RayDataLoader
+    from trainer import Trainer
+    E, vids, bary, rgb = _data()
+    B = CFG["training"]["batch_size"]
+    outs = {}
+    for graph in ("1", "0"):
+        monkeypatch.setenv("INF_GRAPH", graph)
+        torch.manual_seed(0)
+        model, optim = config.get_model_and_optim(CFG, None, "cuda")
+        model.kernel_mode = "fp32"
+        ld = RayDataLoader(E, "efuncs", vids, bary, rgb, None, None, B, True, True, device="cuda")
+        tr = Trainer(model, optim, config.get_loss_fn(CFG), None, {"train": ld, "val": ld}, None, CFG, "cuda")
+        torch.manual_seed(1)
+        calls = []
+        orig = RayDataLoader.__iter__
+        monkeypatch.setattr(RayDataLoader, "__iter__", lambda self: calls.append(1) or orig(self))
+        losses = [tr._train_epoch()[0] for _ in range(3)]
+        monkeypatch.setattr(RayDataLoader, "__iter__", orig)
+        assert len(calls) == 3
+        outs[graph] = (losses, torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy(),
+                       torch.cuda.get_rng_state().clone())
+    np.testing.assert_allclose(outs["1"][0], outs["0"][0], rtol=1e-6)
+    np.testing.assert_allclose(outs["1"][1], outs["0"][1], atol=1e-6)
+    assert torch.equal(outs["1"][2], outs["0"][2])

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 from conftest import golden
+from oracle import inf_oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -105,3 +106,35 @@ def test_viewdep_render_matches_model_on_hits():
     miss = np.ones(H * W, bool)
     miss[hit.cpu().numpy()] = False
     assert hit.numel() > 100 and (flat[miss] == 1.0).all()
+
+
+@pytest.mark.parametrize("name,L,s", [("A", 4, 2), ("R", 6, 3), ("B", 8, 4)])
+def test_concat_layer_standalone(name, L, s):
+    """LinearWithConcatAndActivation called on its own (layers.py:60-62) with the G2
+    weights: its output on the G2 features' skip-layer input matches the oracle's skip
+    layer (fp32 dense kernels, <= 1e-5), and autograd's gradients match the oracle's
+    (relu' masked) products."""
+    from layers import LinearWithConcatAndActivation
+    d = golden(f"g2_forward_{name}.npz")
+    w = {k[2:]: d[k] for k in d.files if k.startswith("w:")}
+    x = d["features"]
+    _, cache = O.mlp_forward(w, x, L, s)
+    h_in, ref = cache["in"][s], cache["out"][s]
+    H, k = w[f"layers.{s}.Lx.weight"].shape[0], x.shape[1]
+    layer = LinearWithConcatAndActivation(H, k, H).cuda()
+    with torch.no_grad():
+        for sub in ("Lx", "Ly"):
+            getattr(layer, sub).weight.copy_(torch.from_numpy(w[f"layers.{s}.{sub}.weight"]))
+            getattr(layer, sub).bias.copy_(torch.from_numpy(w[f"layers.{s}.{sub}.bias"]))
+    hx = torch.from_numpy(h_in).cuda().requires_grad_(True)
+    xx = torch.from_numpy(x).cuda().requires_grad_(True)
+    out = layer(hx, xx)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref, atol=1e-5)
+    g = np.random.default_rng(1).standard_normal(ref.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).cuda())
+    dz = g * (cache["z"][s] > 0)
+    np.testing.assert_allclose(layer.Lx.weight.grad.cpu().numpy(), dz.T @ h_in, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(layer.Ly.weight.grad.cpu().numpy(), dz.T @ x, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(layer.Lx.bias.grad.cpu().numpy(), dz.sum(0), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(hx.grad.cpu().numpy(), dz @ w[f"layers.{s}.Lx.weight"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(xx.grad.cpu().numpy(), dz @ w[f"layers.{s}.Ly.weight"], rtol=1e-4, atol=1e-5)
