@@ -20,6 +20,7 @@
 #include "gemm.hpp"
 #include "head.hpp"
 #include "lgemm.hpp"
+#include "rchain.hpp"
 
 namespace inf {
 
@@ -812,12 +813,91 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
+bool use_rchain(const inf_plan* p, const inf_batch* b) {
+  const ParamSeg* w0 = p->weight_seg(0, 0);
+  const ParamSeg* wy = p->weight_seg(p->s, 1);
+  if (!use_chain(p) || !rchain_supported(p->H, p->L, p->k_pad) || w0->f_off < 0 || wy->f_off < 0) return false;
+  for (int l = 1; l <= p->L - 2; ++l)
+    if (p->weight_seg(l, 0)->f_off < 0) return false;
+  return b->table != nullptr && b->encoding == INF_ENC_NONE && b->table_dtype == INF_DTYPE_BF16 &&
+         b->vids != nullptr && !b->offset_from_ctrl && std::getenv("INF_NO_RCHAIN") == nullptr;
+}
+
+// Forward-only register-streamed chain (csrc/rchain.hip): gather + every layer + head +
+// placement in one launch.  Weight stream: per RC_KC-column feature chunk the W_y then
+// the W_0 k-blocks (W_y x in the second accumulator set), then one block per hidden layer.
+int run_rchain(inf_plan* p, const inf_batch* b, float* pred, const int64_t* hit, const int64_t* pixel_map,
+               float* img, hipStream_t st) {
+  const int H = p->H, L = p->L, s = p->s;
+  const int upl = H / 32;
+  RchainArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.L = L;
+  a.s = s;
+  a.H = H;
+  a.k_pad = p->k_pad;
+  a.batch = b->batch;
+  a.table = reinterpret_cast<const bf16*>(b->table);
+  a.num_vertices = b->num_vertices;
+  a.vids = b->vids;
+  a.vid_dtype = b->vid_dtype;
+  a.bary = b->bary;
+  a.ray_idx = b->ray_idx;
+  a.idx_dtype = b->idx_dtype;
+  a.idx_offset = b->idx_offset;
+  a.num_rays = b->num_rays;
+  a.nchunk = (int)ceil_div(p->k_pad, RC_KC);
+  auto add = [&](const ParamSeg* w, int kb0, int a_x, int ak0, int phase, int last, int flags) -> int {
+    INF_CHECK_ARG(w != nullptr && w->f_off >= 0, "rchain: fragment image missing");
+    INF_CHECK_ARG(a.nblk < RC_MAX_BLOCKS, "rchain: too many weight-stream blocks");
+    C3Block& blk = a.blk[a.nblk++];
+    blk.img = reinterpret_cast<const bf16*>(p->shadow + w->f_off);
+    blk.kb0 = kb0;
+    blk.a_x = a_x;
+    blk.ak0 = ak0;
+    blk.phase = phase;
+    blk.last = last;
+    blk.flags = flags;
+    return INF_OK;
+  };
+  int rc;
+  for (int c = 0; c < a.nchunk; ++c) {
+    const int nb = std::min(RC_KC, p->k_pad - c * RC_KC) / (32 * upl);
+    const int kb = c * (RC_KC / 32);
+    for (int i = 0; i < nb; ++i)
+      if ((rc = add(p->weight_seg(s, 1), kb + i * upl, 1, i * upl, 0, 0,
+                    i == 0 ? C3F_SWAP | (c > 0 ? C3F_GATHER | (c << C3F_CHUNK_SHIFT) : 0) : 0)))
+        return rc;
+    for (int i = 0; i < nb; ++i)
+      if ((rc = add(p->weight_seg(0, 0), kb + i * upl, 1, i * upl, 0, c == a.nchunk - 1 && i == nb - 1,
+                    i == 0 ? C3F_SWAP : 0)))
+        return rc;
+  }
+  for (int l = 1; l <= L - 2; ++l)
+    if ((rc = add(p->weight_seg(l, 0), 0, 0, 0, l, 1, 0))) return rc;
+  a.nphase = L - 1;
+  for (int l = 0; l <= L - 2; ++l) a.bias[l] = p->params + p->bias_seg(l, 0)->off;
+  a.bias_y = p->params + p->bias_seg(s, 1)->off;
+  a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
+  a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
+  a.pred = pred;
+  a.hit = hit;
+  a.pixel_map = pixel_map;
+  a.img = img;
+  return launch_rchain(a, st);
+}
+
 int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool loss, const int64_t* hit,
                  const int64_t* pixel_map, float* img, hipStream_t st) {
   INF_CHECK_ARG(b != nullptr, "null batch");
   int Bp = 0;
   int rc = pad_batch(p, b->batch, save, &Bp);
   if (rc) return rc;
+  if (!save && !loss && use_rchain(p, b)) {
+    if ((rc = run_rchain(p, b, pred, hit, pixel_map, img, st))) return rc;
+    p->saved = false;
+    return INF_OK;
+  }
   if ((rc = run_input(p, b, Bp, save, st))) return rc;
   if (!save && use_chain(p)) {
     if ((rc = run_chain(p, b, Bp, false, pred, hit, pixel_map, img, st))) return rc;

@@ -288,11 +288,18 @@ def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
 
 
 def test_bf16_chain_render_matches_layered(monkeypatch):
+    """bf16 render of the G7 frame: the forward-only register chain (rchain.hip, default),
+    the LDS-ring chain (INF_NO_RCHAIN) and the layered kernels (INF_NO_CHAIN).  The register
+    chain adds W_y x to the skip layer as a separate fp32 sum, so a bf16 activation can
+    round the other way: 5e-4 against the layered path, which the LDS-ring chain matches
+    to 1e-5."""
     d = golden("g7_render.npz")
     H, W = int(d["H"]), int(d["W"])
     E = torch.from_numpy(d["E"]).cuda()
     imgs = {}
-    for tag in ("chain", "layered"):
+    for tag in ("rchain", "chain", "layered"):
+        if tag == "chain":
+            monkeypatch.setenv("INF_NO_RCHAIN", "1")
         if tag == "layered":
             monkeypatch.setenv("INF_NO_CHAIN", "1")
         plan, _, _ = make_plan("A", mode="bf16", max_batch=1024)
@@ -302,7 +309,9 @@ def test_bf16_chain_render_matches_layered(monkeypatch):
         plan.render(plan.make_batch(source=src, batch=hit.shape[0]), hit, None, img)
         imgs[tag] = img.cpu().numpy()
     np.testing.assert_allclose(imgs["chain"], imgs["layered"], atol=1e-5)
-    np.testing.assert_allclose(imgs["chain"].reshape(H, W, 3), d["img_full"], atol=2e-2)
+    np.testing.assert_allclose(imgs["rchain"], imgs["layered"], atol=5e-4)
+    for tag in imgs:
+        np.testing.assert_allclose(imgs[tag].reshape(H, W, 3), d["img_full"], atol=2e-2)
 
 
 @pytest.mark.parametrize("apply_adam", [True, False])
