@@ -338,6 +338,11 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, 0, n0);
       else gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, 0, n0);
     }
+    // every load issued so far has landed (the gather's data is in LDS and the fragment
+    // prologue was issued before it; vmcnt is in order): an explicit wait here costs
+    // nothing and clears the compiler's scoreboard of the gather registers, which it
+    // otherwise drains the whole fragment ring for (vmcnt(0)) at every stream block
+    __builtin_amdgcn_s_waitcnt(0);
     stamp(3 * nphase + 4);
     lbar();  // barrier 0: feature tile in LDS
     stamp(3 * nphase + 5);
@@ -427,11 +432,19 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const bool from_x = B.a_x != 0;
       const char* act_in = act + (B.phase & 1) * C::ACT_BYTES;
       const int ak0 = B.ak0, ckb = B.kb0, nkb = Bn.kb0;
+      // B operand: the feature tile (natural k order) or the activation tile.  One base per
+      // block and a branch-free per-k-block offset (a select on the uniform source flag):
+      // a pointer ternary inside the unrolled loop had compiled to scalar branches between
+      // the MFMAs.  X: chunk (m 4 + g4) ^ r16 of row r16 with m = ak0 + kb, and ak0 a
+      // multiple of UPL keeps the xor inside the k-block's 32-chunk (UPL = 8) / 16-chunk
+      // (UPL = 4) span: xlane + 64 ak0 + ((kb 4 + g4) ^ r16) 16
+      const int fx = from_x ? 1 : 0;
+      const char* bbase = from_x ? xlane + ak0 * 64 : act_in;
 #pragma unroll
       for (int kb = 0; kb < UPL; ++kb) {
-        // B operand: the feature tile (natural k order) or the activation tile
-        const char* bp = from_x ? xlane + ((((ak0 + kb) * 4 + g4) ^ r16) << 4) : act_in + kb * 1024 + aoffs[kb & 3];
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bp);
+        const int xo = ((kb * 4 + g4) ^ r16) << 4;
+        const int ao = kb * 1024 + aoffs[kb & 3];
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bbase + ao + fx * (xo - ao));
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[j], 0, 0, 0);
 #pragma unroll

@@ -884,6 +884,7 @@ int run_rchain(inf_plan* p, const inf_batch* b, float* pred, const int64_t* hit,
   a.hit = hit;
   a.pixel_map = pixel_map;
   a.img = img;
+  a.stamps = p->stamps;
   return launch_rchain(a, st);
 }
 

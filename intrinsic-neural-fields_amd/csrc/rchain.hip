@@ -29,8 +29,11 @@ using namespace c3;
 
 constexpr int RC_CW = 8;              // waves
 constexpr int RC_THREADS = RC_CW * 64;
+// fragment ring depth: the block time does not move between 4 and 8 (tools/rchain_timing.py:
+// the loop is bound by its MFMA + LDS issue, not by loads in flight), and 4 leaves the
+// registers for the next k-block's B operands
 #ifndef RC_DEPTH
-#define RC_DEPTH 8
+#define RC_DEPTH 4
 #endif
 
 template <int H>
@@ -77,6 +80,16 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
   const int xq = nb / 8, xr = nb % 8, xcd = bid % 8;
   const int tile = xcd * xq + min(xcd, xr) + bid / 8;
   const int b0 = tile * BM;
+  unsigned long long* stl = nullptr;
+  if (a.stamps != nullptr && tid == 0 && (bid == 0 || bid == nb / 2)) stl = a.stamps + (bid == 0 ? 0 : RC_STAMPS);
+  auto stamp = [&](int i) {
+    if (stl != nullptr) {
+      __builtin_amdgcn_sched_barrier(0);
+      stl[i] = wall_clock64();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp(0);
 
   // ---- ray records and the per-launch vectors --------------------------------------------
   if (tid < BM * 3) {
@@ -121,6 +134,7 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
     }
   }
   lbar();  // ray records, vectors in LDS
+  stamp(1);
 
   // ---- gather of columns [col0, col0 + ncols) of the BM rays into the feature chunk ----
   // (fp32 FMA in the reference order, one bf16 rounding: chain3.hip / gather.hip numerics)
@@ -177,6 +191,7 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
   };
   gather_chunk(0);
   lbar();  // chunk 0 in LDS
+  stamp(2);
 
   int aoffs[4];
 #pragma unroll
@@ -216,6 +231,7 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
   for (int i = 0; i < a.nblk; ++i) {
     const C3Block& B = a.blk[i];
     const C3Block& Bn = a.blk[i + 1 < a.nblk ? i + 1 : i];
+    stamp(3 + i);
     if (B.flags & C3F_GATHER) {
       lbar();  // every wave is done with the previous chunk
       gather_chunk(B.flags >> C3F_CHUNK_SHIFT);
@@ -236,24 +252,39 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
     const bool from_x = B.a_x != 0;
     const char* act_in = act + (B.phase & 1) * C::ACT_BYTES;
     const int ak0 = B.ak0, ckb = B.kb0, nkb = Bn.kb0;
+    // the k-blocks of this stream block, B operands from the feature chunk (X) or the
+    // activation tile: two straight-line copies of the unrolled loop (a uniform branch
+    // outside it), the B operands of k-block kb + 1 read before the MFMAs of kb so their
+    // LDS latency hides under them
+    auto run_block = [&](auto FROMXc) {
+      constexpr bool FROMX = decltype(FROMXc)::value;
+      auto read_b = [&](int kb, bf16x8 (&bv)[RT]) {
 #pragma unroll
-    for (int kb = 0; kb < UPL; ++kb) {
-      bf16x8 bv[RT];
+        for (int t = 0; t < RT; ++t) {
+          const char* bp;
+          if constexpr (FROMX) bp = xs + (t * 16 + r16) * xrow + ((((ak0 + kb) * 4 + g4) ^ r16) << 4);
+          else bp = act_in + t * C::ACT_T + kb * 1024 + aoffs[kb & 3];
+          bv[t] = *reinterpret_cast<const bf16x8*>(bp);
+        }
+      };
+      bf16x8 bq[2][RT];
+      read_b(0, bq[0]);
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        const char* bp = from_x ? xs + (t * 16 + r16) * xrow + ((((ak0 + kb) * 4 + g4) ^ r16) << 4)
-                                : act_in + t * C::ACT_T + kb * 1024 + aoffs[kb & 3];
-        bv[t] = *reinterpret_cast<const bf16x8*>(bp);
+      for (int kb = 0; kb < UPL; ++kb) {
+        if (kb + 1 < UPL) read_b(kb + 1, bq[(kb + 1) & 1]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bq[kb & 1][t], acc[t][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int t = 0; t < RT; ++t) acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv[t], acc[t][j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    };
+    if (from_x) run_block(std::true_type{});
+    else run_block(std::false_type{});
     if (!B.last) continue;
 
     // ---- epilogue of layer l = phase: bias (+ W_y x and Ly.bias at the skip layer) + ReLU
@@ -310,6 +341,7 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
     lbar();  // the next layer's tile (or the head partials) complete
   }
 
+  stamp(3 + a.nblk);
   // ---- sigmoid head and placement (renderer.py:132-141) -----------------------------------
   if (tid < BM * 3) {
     const int ray = tid / 3, o = tid % 3;

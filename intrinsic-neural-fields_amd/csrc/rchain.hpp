@@ -36,7 +36,12 @@ struct RchainArgs {
   const int64_t* hit;
   const int64_t* pixel_map;
   float* img;
+  // diagnostics (inf_debug_timing): wall-clock stamps of wave 0 of workgroups 0 and
+  // gridDim / 2: [2][RC_STAMPS] = entry, records in LDS, chunk 0 in LDS, each block's
+  // start, end
+  unsigned long long* stamps;
 };
+constexpr int RC_STAMPS = 4 + RC_MAX_BLOCKS;
 
 inline int rchain_blocks(int H, int L, int k_pad) { return 2 * (k_pad / H) + (L - 2); }
 inline bool rchain_supported(int H, int L, int k_pad) {
