@@ -107,16 +107,35 @@ class Trainer:
         # INF_BENCH_DP=1 runs it at world 1 too (rehearses RCCL capture on a one-GPU box)
         self.dp = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
         self.ar_in_graph = False
+        # INF_PREFETCH=1: the next batch's gather on a side stream beside the gradient
+        # all-reduce (runtime.StepPipeline lead 0).  Off by default: on one MI355X the
+        # data-parallel step takes 94.2 us with it vs 77.4 us without (the gather and two
+        # cross-queue signals land on the critical path when the all-reduce is empty); it is
+        # meant for N > 1, where the all-reduce is long, and is unmeasured there
+        self.pipe = runtime.StepPipeline(self.plan, self.batch, lead=int(os.environ.get("INF_PREFETCH_LEAD", "0")))
+        want = os.environ.get("INF_PREFETCH", "0") != "0"
+        self.prefetch = want and self.pipe.start()
 
     # steps per replayed graph (divides nb)
     GRAPH_STEPS = int(os.environ.get("INF_GRAPH_STEPS", "8"))
 
-    def _launch(self):
+    def _launch(self, xslot=None):
         if not self.dp:
             # Adam + the batch-index advance ride in the step's update launch
-            self.plan.train_step(self.batch, None, apply_adam=True, advance=True)
+            self.plan.train_step(self.batch, None, apply_adam=True, advance=True, xslot=xslot)
         else:
-            self.plan.train_step(self.batch, None, apply_adam=False)
+            self.plan.train_step(self.batch, None, apply_adam=False, xslot=xslot)
+
+    def _steps(self, n):
+        """n steps: pipelined (side-stream prefetch of the next batch) or plain."""
+        tail = self._dp_tail if self.dp else None
+        if self.prefetch:
+            self.pipe.run(n, self._launch, first_slot=self.i % 2, tail_fn=tail)
+        else:
+            for _ in range(n):
+                self._launch()
+                if tail is not None:
+                    tail()
 
     def _dp_tail(self):
         """all-reduce of the flat gradient bucket, then the replicated Adam + batch advance"""
@@ -133,9 +152,7 @@ class Trainer:
         try:
             gm = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, stream=s):
-                for _ in range(self.GRAPH_STEPS):
-                    self._launch()
-                    self._dp_tail()
+                self._steps(self.GRAPH_STEPS)
             self.ar_in_graph = True
             return gm
         except Exception as exc:  # capture refused: per-step replays around an eager all-reduce
@@ -145,6 +162,7 @@ class Trainer:
 
     def capture(self):
         # one eager step: settles the plan's tables before capture
+        self.step_eager()
         self.step_eager()
         if self.args.no_graph:
             return
@@ -162,30 +180,33 @@ class Trainer:
                     self.plan.adam(0, 0.0)
                     self.plan.ctrl_advance()
             else:
-                # several steps per graph: one replay launch per GRAPH_STEPS steps
+                # several steps per graph: one replay launch per GRAPH_STEPS steps (an even
+                # number: the pre-gather slots alternate)
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm, stream=s):
-                    for _ in range(self.GRAPH_STEPS):
-                        self._launch()
+                    self.i = 0
+                    self._steps(self.GRAPH_STEPS)
         torch.cuda.current_stream().wait_stream(s)
         self.graphs = (g1, g2, gm)
         self.plan.set_batch_index(0)
         self.i = 0
+        if self.prefetch:
+            self.pipe.start()
 
     def _wrap(self):
         if self.i == self.nb:
             self.plan.set_batch_index(0)
             self.i = 0
+            if self.prefetch:
+                self.pipe.start()
 
     def step_eager(self):
         self._wrap()
-        self._launch()
-        if self.dp:
-            self._dp_tail()
+        self._steps(1)
         self.i += 1
 
     def step(self):
-        if self.graphs is None:
+        if self.graphs is None or self.prefetch:
             return self.step_eager()
         self._wrap()
         g1, g2, _ = self.graphs
@@ -201,7 +222,7 @@ class Trainer:
         gm = self.graphs[2] if self.graphs is not None else None
         while n > 0:
             self._wrap()
-            if gm is not None and n >= self.GRAPH_STEPS and self.i + self.GRAPH_STEPS <= self.nb:
+            if gm is not None and n >= self.GRAPH_STEPS and self.i + self.GRAPH_STEPS <= self.nb and self.i % 2 == 0:
                 gm.replay()
                 self.i += self.GRAPH_STEPS
                 n -= self.GRAPH_STEPS

@@ -106,7 +106,7 @@ typedef struct inf_ctrl {
   int32_t step;        /* Adam step count t (post-increment semantics of torch Adam) */
   int32_t batch_index; /* batch number inside the current epoch                     */
   float lr;            /* learning rate (ReduceLROnPlateau may change it)            */
-  int32_t pad;
+  int32_t prefetch_index; /* batch number the next inf_prefetch_batch gathers        */
   double loss_sum;     /* sum of element losses of the last step                     */
   double sse_sum;      /* sum of squared errors of the last step                     */
   double epoch_loss;   /* accumulated over the epoch (host resets)                   */
@@ -218,9 +218,20 @@ int inf_backward(inf_plan* plan, const float* dpred, float* grads, inf_stream_t 
  * at the end of the step (a graph-replayed epoch; same as a following
  * inf_ctrl_advance).  pred may be NULL.  The step's loss / SSE sums are stored in
  * ctrl->loss_sum / sse_sum and added to the epoch sums. */
-enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2 };
+enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2, INF_STEP_XSLOT0 = 4, INF_STEP_XSLOT1 = 8 };
 int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int flags,
                    inf_stream_t stream);
+
+/* Gather of a training batch's features (mesh.py:313-324 with the loader's index select,
+ * ray_dataloader.py:122-129) into pre-gather slot `slot` (0 / 1) of the plan's workspace,
+ * for a later inf_train_step with INF_STEP_XSLOT0 / XSLOT1: the fused chain then reads
+ * each ray's feature row instead of three table rows, so the gather can run on a side
+ * stream while the previous step's dW GEMM, update and all-reduce run.  With
+ * batch->offset_from_ctrl the batch offset is idx_offset + ctrl->prefetch_index * batch and
+ * ctrl->prefetch_index is advanced after the gather (graph-replayed epochs).  Returns
+ * INF_ERR_STATE when the batch's training step would not use the fused chain (bf16 mode,
+ * a bf16 eigenfunction table, the fused shapes): the caller then steps without slots. */
+int inf_prefetch_batch(inf_plan* plan, const inf_batch* batch, int slot, inf_stream_t stream);
 
 /* Adam update from the bound `grads` arena (optim.step(), trainer.py:82).  step > 0:
  * step and lr are used as given (torch state["step"] after its increment, param_group

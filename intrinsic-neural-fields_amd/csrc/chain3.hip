@@ -166,7 +166,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     };
     // ---- gather: ray records of the 16 rays (index, vertex ids, barycentrics), one
     // thread per (ray, corner) ------------------------------------------------------------
-    if (tid < BM * 3) {
+    if (tid < BM * 3 && a.xpre == nullptr) {
       int64_t offset = a.idx_offset;
       if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
       const int rl = tid / 3, i = tid % 3;
@@ -218,9 +218,40 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // are live)
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.table), (short)0, (int)0xFFFFFFFFu, 0x00020000);
+    // pre-gathered rows (inf_prefetch_batch): the workgroup's 16 feature rows are one
+    // contiguous block of xpre, copied 16 bytes per thread, all loads of a round first
+    const __amdgpu_buffer_rsrc_t rxp = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(a.xpre != nullptr ? a.xpre + (int64_t)b0 * k_pad : a.table), (short)0, 0x7FFFFFFF, 0x00020000);
+    auto copy_cols = [&](int col0, int ncols) {
+      const int cpr = ncols >> 3;
+      const int nch = BM * cpr;
+      constexpr int GR = 4;
+#pragma unroll 1
+      for (int q0 = tid; q0 < nch; q0 += C3_CT * GR) {
+        u32x4 v[GR];
+#pragma unroll
+        for (int g = 0; g < GR; ++g) {
+          const int q = q0 + C3_CT * g;
+          const int r = (q < nch ? q : 0) / cpr, ch = (q < nch ? q : 0) % cpr;
+          v[g] = __builtin_amdgcn_raw_buffer_load_b128(rxp, (unsigned)(r * k_pad + col0 + ch * 8) * 2u, 0, C3_GATHER_CPOL);
+        }
+#pragma unroll
+        for (int g = 0; g < GR; ++g) {
+          const int q = q0 + C3_CT * g;
+          if (q < nch) {
+            const int r = q / cpr, ch = q % cpr;
+            *reinterpret_cast<u32x4*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = v[g];
+          }
+        }
+      }
+    };
     auto gather_cols = [&](auto GRc, auto BIGc, int col0, int ncols) {
       constexpr int GR = decltype(GRc)::value;
       constexpr bool BIG = decltype(BIGc)::value;
+      if (a.xpre != nullptr) {
+        copy_cols(col0, ncols);
+        return;
+      }
       const int cpr = ncols >> 3;          // chunks per row
       const int nch = BM * cpr;            // chunks of the tile
 #pragma unroll 1

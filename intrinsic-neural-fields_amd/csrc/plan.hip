@@ -30,6 +30,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 namespace {
 
 __global__ void ctrl_advance_kernel(inf_ctrl* c) { c->batch_index += 1; }
+__global__ void prefetch_advance_kernel(inf_ctrl* c) { c->prefetch_index += 1; }
 
 struct ParamSeg {
   int64_t off = 0;
@@ -66,6 +67,7 @@ struct inf_plan {
 
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_ws_end = 0;
+  int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
   int n_aux_items = 0;
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
@@ -220,6 +222,8 @@ int build_layout(inf_plan* p) {
   };
   p->o_x0 = take(Bp * p->k_pad * p->esz);
   p->o_x0t = take((int64_t)p->k_pad * Bp * p->esz);
+  if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS)
+    for (int i = 0; i < 2; ++i) p->o_xp[i] = take(Bp * p->k_pad * 2);
   const int64_t max_parts =
       std::max<int64_t>({chain_max_partials(Bp), std::min<int64_t>(Bp, CHAIN3_MAX_ROWS) / 16, (int64_t)p->grid_hb});
   for (int l = 0; l < L - 1; ++l) {
@@ -703,7 +707,7 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
 // layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
 // k_pad > C3_KC (config D): X is streamed in C3_KC-column chunks and phase 0 runs W_y then
 // W_0 over each chunk (W_y x kept in the second accumulator set until the skip layer).
-int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
+int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st, const bf16* xpre = nullptr) {
   const int H = p->H, L = p->L, s = p->s;
   const int upl = H / 32;
   const int nx = p->k_pad / (32 * upl);  // stream blocks of X
@@ -810,6 +814,7 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.ctrl = p->ctrl;
   a.count_step = 1;
   a.stamps = p->stamps;
+  a.xpre = b->encoding == INF_ENC_NONE ? xpre : nullptr;
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
@@ -1125,7 +1130,9 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     return INF_ERR_STATE;
   }
   const bool apply_adam = (flags & INF_STEP_ADAM) != 0;
-  INF_CHECK_ARG((flags & ~(INF_STEP_ADAM | INF_STEP_ADVANCE)) == 0, "train_step: unknown flags");
+  INF_CHECK_ARG((flags & ~(INF_STEP_ADAM | INF_STEP_ADVANCE | INF_STEP_XSLOT0 | INF_STEP_XSLOT1)) == 0,
+                "train_step: unknown flags");
+  const int xslot = (flags & INF_STEP_XSLOT0) ? 0 : (flags & INF_STEP_XSLOT1) ? 1 : -1;
   INF_CHECK_ARG(batch != nullptr && batch->rgb != nullptr, "train_step: batch with target colours required");
   INF_CHECK_ARG(p->grads != nullptr || apply_adam, "train_step: grads not bound");
   INF_CHECK_ARG(!apply_adam || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr), "train_step: Adam state");
@@ -1157,7 +1164,12 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     // it, the first blocks do the biases and the end-of-step sums; bitwise the same) --
     // slower today: the last arriver's four items run back to back
     const int Bp = Bp3;
-    if ((rc = run_chain3(p, batch, Bp, pred, st))) return rc;
+    const bf16* xpre = nullptr;
+    if (xslot >= 0) {
+      INF_CHECK_ARG(p->o_xp[xslot] >= 0 && batch->encoding == INF_ENC_NONE, "train_step: no pre-gather slot");
+      xpre = p->W<bf16>(p->o_xp[xslot]);
+    }
+    if ((rc = run_chain3(p, batch, Bp, pred, st, xpre))) return rc;
     p->saved = false;
     p->saved_batch = batch->batch;
     p->saved_bp = Bp;
@@ -1324,6 +1336,32 @@ int inf_debug_timing(inf_plan* p, unsigned long long* stamps, int max_steps) {
   INF_CHECK_ARG(p != nullptr && max_steps >= 0, "debug timing");
   p->stamps = stamps;
   p->stamp_steps = max_steps;
+  return INF_OK;
+}
+
+int inf_prefetch_batch(inf_plan* p, const inf_batch* b, int slot, inf_stream_t stream) {
+  if (p == nullptr || !p->bound) {
+    set_error("plan not bound");
+    return INF_ERR_STATE;
+  }
+  INF_CHECK_ARG(b != nullptr && (slot == 0 || slot == 1), "prefetch: batch and slot 0 / 1 required");
+  int Bp = 0;
+  int rc = pad_batch(p, b->batch, true, &Bp);
+  if (rc) return rc;
+  if (p->o_xp[slot] < 0 || b->encoding != INF_ENC_NONE || !use_chain3(p, b, Bp)) {
+    set_error("prefetch: this batch's step does not run the fused chain");
+    return INF_ERR_STATE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = launch_gather(b->table, b->table_dtype, b->num_vertices, p->k_pad, p->k_pad, b->vids, b->vid_dtype,
+                          b->bary, b->ray_idx, b->idx_dtype, b->idx_offset,
+                          b->offset_from_ctrl ? &p->ctrl->prefetch_index : nullptr, b->num_rays, b->batch,
+                          p->W(p->o_xp[slot]), INF_DTYPE_BF16, p->k_pad, Bp, nullptr, 0, st)))
+    return rc;
+  if (b->offset_from_ctrl) {
+    prefetch_advance_kernel<<<1, 1, 0, st>>>(p->ctrl);
+    INF_LAUNCH_CHECK();
+  }
   return INF_OK;
 }
 

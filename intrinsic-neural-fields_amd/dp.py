@@ -98,7 +98,7 @@ class DataParallelEpoch:
     Replicas stay bitwise equal without parameter broadcasts.  A partial last batch
     (drop_last=False) runs eagerly."""
 
-    GRAPH_STEPS = 8
+    GRAPH_STEPS = 8  # even: the pre-gather slots alternate
 
     def __init__(self, group=None):
         self.group = group
@@ -108,17 +108,33 @@ class DataParallelEpoch:
         self.key = None
         self.idx = None
         self.steps_done = 0
+        self.pipe = None
 
     def _tail_all_reduce(self, rt, plan):
         allreduce_grads(rt.grads, self.group)
         plan.adam(0, 0.0)
         plan.ctrl_advance()
 
+    def _step(self, rt, plan, batch, xslot=None):
+        plan.train_step(batch, None, apply_adam=False, xslot=xslot)
+        self._tail_all_reduce(rt, plan)
+
+    def _pipelined(self, count, rt, plan, batch):
+        self.pipe.run(count, lambda xs: plan.train_step(batch, None, apply_adam=False, xslot=xs),
+                      tail_fn=lambda: self._tail_all_reduce(rt, plan))
+
     def _capture(self, plan, rt, batch):
+        from inf_hip import runtime
         saved = [x.clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl)]
         plan.set_batch_index(0)
         plan.train_step(batch, None, apply_adam=False)  # settles the plan's tables before capture
         self._tail_all_reduce(rt, plan)
+        # the next batch's gather on a side stream, beside the all-reduce (StepPipeline)
+        # INF_PREFETCH=1: the next batch's gather beside the all-reduce (off by default, see
+        # runtime.StepPipeline and bench.py for the world-1 measurement)
+        self.pipe = runtime.StepPipeline(plan, batch, lead=0) if os.environ.get("INF_PREFETCH", "0") != "0" else None
+        if self.pipe is not None and not self.pipe.start():
+            self.pipe = None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -127,9 +143,11 @@ class DataParallelEpoch:
                 plan.train_step(batch, None, apply_adam=False)
                 self._tail_all_reduce(rt, plan)
             with torch.cuda.graph(gm, stream=s):
-                for _ in range(self.GRAPH_STEPS):
-                    plan.train_step(batch, None, apply_adam=False)
-                    self._tail_all_reduce(rt, plan)
+                if self.pipe is not None:
+                    self._pipelined(self.GRAPH_STEPS, rt, plan, batch)
+                else:
+                    for _ in range(self.GRAPH_STEPS):
+                        self._step(rt, plan, batch)
         torch.cuda.current_stream().wait_stream(s)
         for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
             dst.copy_(src)
@@ -179,10 +197,15 @@ class DataParallelEpoch:
                 plan.reset_epoch_sums()
                 plan.set_batch_index(0)
                 g1, gm = self.graph
-                for _ in range(full // self.GRAPH_STEPS):
-                    gm.replay()
-                for _ in range(full % self.GRAPH_STEPS):
-                    g1.replay()
+                if self.pipe is not None and self.pipe.start():
+                    for _ in range(full // self.GRAPH_STEPS):
+                        gm.replay()
+                    self._pipelined(full % self.GRAPH_STEPS, rt, plan, batch)
+                else:
+                    for _ in range(full // self.GRAPH_STEPS):
+                        gm.replay()
+                    for _ in range(full % self.GRAPH_STEPS):
+                        g1.replay()
             else:
                 plan.set_batch_index(0)
                 for _ in range(full):

@@ -21,7 +21,7 @@ LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
 LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
-STEP_ADAM, STEP_ADVANCE = 1, 2  # inf_train_step flags
+STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1 = 1, 2, 4, 8  # inf_train_step flags
 ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF = 0, 1, 2, 3
 ENC_CODES = {"xyz": ENC_XYZ, "rff": ENC_RFF, "ff": ENC_FF}
 
@@ -50,7 +50,7 @@ class Batch(ctypes.Structure):
 
 
 class Ctrl(ctypes.Structure):
-    _fields_ = [("step", c_int32), ("batch_index", c_int32), ("lr", c_float), ("pad", c_int32),
+    _fields_ = [("step", c_int32), ("batch_index", c_int32), ("lr", c_float), ("prefetch_index", c_int32),
                 ("loss_sum", c_double), ("sse_sum", c_double), ("epoch_loss", c_double),
                 ("epoch_sse", c_double)]
 
@@ -97,6 +97,7 @@ _SIGNATURES = {
     "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_plan_last_step_path": (c_int, [c_void_p]),
+    "inf_prefetch_batch": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "inf_debug_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "inf_debug_block_times": (c_int, [c_void_p, c_void_p]),

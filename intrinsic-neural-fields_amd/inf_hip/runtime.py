@@ -10,8 +10,9 @@ import ctypes
 
 import torch
 
-from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, LOSS_CODES, MODE_BF16, MODE_CODES, Batch,
-               STEP_ADAM, STEP_ADVANCE, MlpDesc, PlanInfo, c_int64, c_void_p, check, lib)
+from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
+               MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo, c_int64, c_void_p,
+               check, lib)
 
 _TORCH_DTYPE = {DTYPE_F32: torch.float32, DTYPE_BF16: torch.bfloat16}
 _CODE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.int32: DTYPE_I32, torch.int64: DTYPE_I64}
@@ -294,6 +295,9 @@ class Plan:
     def set_batch_index(self, i: int):
         self.ctrl_i32[1].fill_(int(i))
 
+    def set_prefetch_index(self, i: int):
+        self.ctrl_i32[3].fill_(int(i))
+
     def reset_epoch_sums(self):
         self.ctrl_f64[4:6].zero_()
 
@@ -379,10 +383,24 @@ class Plan:
     def backward(self, dpred: torch.Tensor, grads: torch.Tensor):
         check(lib.inf_backward(self.handle, ptr(dpred), ptr(grads), stream_handle()), "backward")
 
-    def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool, advance: bool = False):
-        """inf_train_step; advance=True also moves ctrl.batch_index on (graph-replayed epochs)."""
+    def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool, advance: bool = False,
+                   xslot: int | None = None):
+        """inf_train_step; advance=True also moves ctrl.batch_index on (graph-replayed epochs);
+        xslot: the batch's features were gathered into that pre-gather slot (prefetch)."""
         flags = (STEP_ADAM if apply_adam else 0) | (STEP_ADVANCE if advance else 0)
+        if xslot is not None:
+            flags |= STEP_XSLOT0 if xslot == 0 else STEP_XSLOT1
         check(lib.inf_train_step(self.handle, ctypes.byref(b), ptr(pred), flags, stream_handle()), "train_step")
+
+    def prefetch(self, b: Batch, slot: int) -> bool:
+        """inf_prefetch_batch: gather the batch's features into pre-gather slot 0 / 1 on the
+        current stream.  False (nothing launched) when its step does not run the fused chain."""
+        rc = lib.inf_prefetch_batch(self.handle, ctypes.byref(b), int(slot), stream_handle())
+        if rc == INF_OK:
+            return True
+        if rc == -4:  # INF_ERR_STATE: not a fused-chain batch
+            return False
+        check(rc, "prefetch_batch")
 
     def adam(self, step: int = 0, lr: float = 0.0):
         check(lib.inf_adam(self.handle, int(step), float(lr), stream_handle()), "adam")
@@ -520,3 +538,68 @@ class Bvh:
                                    ptr(ray), ptr(fc), stream_handle()), "compact_hits")
         m = int(count.item())
         return vids[:m], ob[:m], ray[:m], fc[:m]
+
+
+class StepPipeline:
+    """Training steps with the NEXT batch's gather on a side HIP stream.
+
+    Step n reads its features from pre-gather slot n % 2 (inf_train_step XSLOT flags); the
+    side stream gathers batch n + 1 into the other slot (inf_prefetch_batch, batch offset
+    from ctrl.prefetch_index) and the main stream's step n + 1 waits for it.  `lead`:
+      0 -- the gather starts when step n's fused chain / dW / update launches are done, so it
+           runs beside what follows them on the main stream: the data-parallel step's
+           gradient all-reduce and Adam (SURVEY.md §8(e));
+      1 -- it starts when step n - 1 is done (the last reader of its slot), beside step n's
+           own kernels.
+    Measured on one MI355X at 4096 rays, config B: lead 1 beside the single-GPU fused step
+    costs +14 us per step (the gather's workgroups contend with the fused chain's, which
+    hold every CU); lead 0 in the world-1 data-parallel step +17 us (94.2 vs 77.4 us: with
+    an empty all-reduce the gather and two cross-queue signals sit on the critical path).
+    So the in-kernel gather stays the default; the pipeline is opt-in (INF_PREFETCH=1) for
+    multi-GPU runs, where it would run beside the all-reduce.  Events order the two
+    streams, so the pattern is captured into a HIP graph as it is (a fork / join per step).
+    `start()` gathers batch 0 into slot 0; a graph of an even number of steps leaves the
+    slot parity as it found it."""
+
+    def __init__(self, plan: Plan, batch: Batch, lead: int = 0):
+        self.plan, self.batch, self.lead = plan, batch, lead
+        self.side = torch.cuda.Stream(device=plan.device)
+        self.enabled = True
+
+    def start(self) -> bool:
+        """Epoch start: prefetch index 0, batch 0 into slot 0 (current stream).  False when
+        the plan cannot pre-gather this batch (then step without slots)."""
+        self.plan.set_prefetch_index(0)
+        self.enabled = self.plan.prefetch(self.batch, 0)
+        return self.enabled
+
+    def run(self, count: int, step_fn, first_slot: int = 0, tail_fn=None):
+        """Issues `count` steps: step_fn(xslot) enqueues one step's fused launches, then
+        tail_fn() what follows them (the data-parallel all-reduce / Adam / advance)."""
+        if not self.enabled:
+            for _ in range(count):
+                step_fn(None)
+                if tail_fn is not None:
+                    tail_fn()
+            return
+        main = torch.cuda.current_stream()
+        self.side.wait_stream(main)
+        prev_done, ready = None, None
+        for j in range(count):
+            slot = (first_slot + j) % 2
+            if ready is not None:
+                main.wait_event(ready)
+            step_fn(slot)
+            done = torch.cuda.Event()
+            done.record(main)
+            after = done if self.lead == 0 else prev_done
+            with torch.cuda.stream(self.side):
+                if after is not None:
+                    self.side.wait_event(after)
+                self.plan.prefetch(self.batch, 1 - slot)
+                ready = torch.cuda.Event()
+                ready.record(self.side)
+            if tail_fn is not None:
+                tail_fn()
+            prev_done = done
+        main.wait_stream(self.side)

@@ -65,15 +65,19 @@ def _summary_writer(log_dir):
 
 class _FusedEpoch:
     """Replays captured fused steps (GRAPH_STEPS per graph launch, then single steps) over
-    the full batches of an epoch; the batch index advances on the device."""
+    the full batches of an epoch; the batch index advances on the device.  Where the step
+    runs the fused chain, the next batch's gather runs on a side stream
+    (runtime.StepPipeline: each step reads pre-gathered feature rows); INF_PREFETCH=0 turns
+    that off."""
 
     def __init__(self, trainer):
         self.t = trainer
         self.graph = None
         self.key = None
         self.perm = None
+        self.pipe = None
 
-    GRAPH_STEPS = 8
+    GRAPH_STEPS = 8  # even: the pre-gather slots alternate
 
     def run(self, loader):
         t = self.t
@@ -109,10 +113,17 @@ class _FusedEpoch:
             plan.reset_epoch_sums()
             plan.set_batch_index(0)
             g1, gm = self.graph
-            for _ in range(full // self.GRAPH_STEPS):
-                gm.replay()
-            for _ in range(full % self.GRAPH_STEPS):
-                g1.replay()
+            if self.pipe is not None and self.pipe.start():
+                for _ in range(full // self.GRAPH_STEPS):
+                    gm.replay()
+                b = self._batch
+                self.pipe.run(full % self.GRAPH_STEPS,
+                              lambda xs: plan.train_step(b, None, apply_adam=True, advance=True, xslot=xs))
+            else:
+                for _ in range(full // self.GRAPH_STEPS):
+                    gm.replay()
+                for _ in range(full % self.GRAPH_STEPS):
+                    g1.replay()
             optim.after_fused_steps(model, rt, group, full)
             done = full
             total = full * B
@@ -135,6 +146,12 @@ class _FusedEpoch:
         saved = [x.clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl)]
         plan.set_batch_index(0)
         plan.train_step(b, None, apply_adam=True)
+        from inf_hip import runtime
+        # single-GPU epochs keep the in-kernel gather (StepPipeline's measurement); INF_PREFETCH=1
+        # moves it to a side stream
+        self.pipe = runtime.StepPipeline(plan, b, lead=1) if os.environ.get("INF_PREFETCH", "0") != "0" else None
+        if self.pipe is not None and not self.pipe.start():  # this batch's step has no fused chain
+            self.pipe = None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -143,8 +160,12 @@ class _FusedEpoch:
             with torch.cuda.graph(g1, stream=s):
                 plan.train_step(b, None, apply_adam=True, advance=True)
             with torch.cuda.graph(gm, stream=s):  # GRAPH_STEPS steps per replay launch
-                for _ in range(self.GRAPH_STEPS):
-                    plan.train_step(b, None, apply_adam=True, advance=True)
+                if self.pipe is not None:
+                    self.pipe.run(self.GRAPH_STEPS,
+                                  lambda xs: plan.train_step(b, None, apply_adam=True, advance=True, xslot=xs))
+                else:
+                    for _ in range(self.GRAPH_STEPS):
+                        plan.train_step(b, None, apply_adam=True, advance=True)
         torch.cuda.current_stream().wait_stream(s)
         for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
             dst.copy_(src)
