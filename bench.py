@@ -265,6 +265,15 @@ def time_stage(plan, stage, reps=20, batch=None, layer=0):
     return e0.elapsed_time(e1) / reps, flops, byts
 
 
+def _pmc_traffic(key):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/traffic.json,
+    tools/profile_r02.sh: 2 x FETCH_SIZE + WRITE_SIZE), or None."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(key)
+    except Exception:
+        return None
+
+
 def flops_per_ray(k, H, L):
     """Training FLOPs per ray: forward, dX chain and dW."""
     return 2 * (2 * (2 * k * H + (L - 2) * H * H + 3 * H) + (L - 2) * H * H + 3 * H)
@@ -310,6 +319,7 @@ def config_d_bench(args, device, B=4096, steps=40):
     out = {"config": "human_dense D: k=4096 8x256 skip 4, L2, Adam lr 1e-4, V=500000, bf16 table 4.1 GB",
            "rays_per_step": B, "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s", "path": path,
            "roofline": step_roofline(4096, a.hidden, a.layers, B, P, ms),
+           "chain3_traffic_per_launch": _pmc_traffic("chain3_chunked_bf16_D4096"),
            "stages": {kk: {"ms": v[0], "tflops": v[1] / (v[0] * 1e-3) / 1e12} for kk, v in st.items()},
            "gather_kernel": {"ms": gms, "table_row_bytes": row_bytes,
                              "table_gbs": row_bytes / (gms * 1e-3) / 1e9,
@@ -425,6 +435,10 @@ def render_bench(args, device):
             "bound": "mfma" if t_mfma >= t_hbm else "hbm", "mfma_frac": t_mfma / ms, "hbm_frac": t_hbm / ms,
             "frac": max(t_mfma, t_hbm) / ms, "achieved_tflops": flops / (ms * 1e-3) / 1e12,
             "achieved_gbs": byts / (ms * 1e-3) / 1e9}
+    tr = _pmc_traffic(f"rchain_{args.mode}_render_{chunk}")
+    if tr is not None:  # measured HBM bytes of one launch (PMC), over the frame's launches
+        roof["traffic_per_launch"] = tr
+        roof["traffic"] = tr * len(offs)
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
             "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams, "roofline": roof}
 

@@ -14,7 +14,9 @@ from collections import defaultdict
 
 
 def short(name):
-    for key in ("chain3_kernel", "lgemm_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
+    if "chain3_kernel" in name and ("Lb0ELb1E" in name or "false, true>" in name):
+        return "chain3_kernel<chunked>"
+    for key in ("rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
                 "head_bwd_kernel", "pack_kernel", "ctrl_advance_kernel"):
         if key in name:
             tail = ""
@@ -60,7 +62,8 @@ def counters(d, counter):
 
 
 # bench.py stage -> kernel, for the per-launch traffic table bench.py reads
-STAGE_KERNEL = {"chain3": "chain3_kernel", "dw_gemm": "lgemm_kernel", "update": "update_kernel"}
+STAGE_KERNEL = {"chain3": "chain3_kernel", "dw_gemm": "lgemm_kernel", "update": "update_kernel",
+                "rchain": "rchain_kernel", "chain3_chunked": "chain3_kernel<chunked>"}
 
 
 def main(root, tag=None):
