@@ -19,6 +19,8 @@
 // a second register set (accy) and joins the skip layer's epilogue (chain3.hip's chunked
 // schedule).  Consecutive ray tiles go to one XCD (render hits are in pixel order, so
 // their table rows repeat across neighbouring tiles and stay in that XCD's L2).
+#include <cstdlib>
+
 #include "c3common.hpp"
 #include "rchain.hpp"
 
@@ -27,8 +29,6 @@ namespace {
 
 using namespace c3;
 
-constexpr int RC_CW = 8;              // waves
-constexpr int RC_THREADS = RC_CW * 64;
 // fragment ring depth: the block time does not move between 4 and 8 (tools/rchain_timing.py:
 // the loop is bound by its MFMA + LDS issue, not by loads in flight), and 4 leaves the
 // registers for the next k-block's B operands
@@ -36,10 +36,12 @@ constexpr int RC_THREADS = RC_CW * 64;
 #define RC_DEPTH 4
 #endif
 
-template <int H>
+// CW waves per workgroup, RT 16-ray tiles: <8, 4> one 147 KB workgroup per CU (4 MFMAs
+// per fragment); <4, 2> two 72 KB workgroups per CU, so one gathers while the other streams
+template <int H, int CW, int RT_>
 struct LR {
-  static constexpr int RT = RC_RT, BM = RC_BM;
-  static constexpr int TN = H / (16 * RC_CW);  // 16-feature tiles per wave
+  static constexpr int RT = RT_, BM = 16 * RT_, THREADS = CW * 64;
+  static constexpr int TN = H / (16 * CW);  // 16-feature tiles per wave
   static constexpr int UPL = H / 32;           // 32-deep k blocks per stream block
   static constexpr int NT = H / 16;            // 16-row tiles per k block of a weight image
   static constexpr int ACT_T = 16 * H * 2;     // one ray tile of activations
@@ -49,15 +51,16 @@ struct LR {
   static constexpr int OFF_RAY = OFF_X + BM * RC_KC * 2;       // [BM][4] vertex ids, [BM][3] ok
   static constexpr int OFF_RB = OFF_RAY + BM * 16 + BM * 12;   // [BM][3] barycentrics
   static constexpr int OFF_ZP = OFF_RB + BM * 12;              // [waves][BM][3] head partial sums
-  static constexpr int OFF_W7 = OFF_ZP + RC_CW * BM * 12;      // [3][H], b7[3]
+  static constexpr int OFF_W7 = OFF_ZP + CW * BM * 12;         // [3][H], b7[3]
   static constexpr int OFF_VEC = OFF_W7 + 3 * H * 4 + 16;      // biases [L-1][H], Ly.bias [H]
   static int lds_bytes(int L) { return OFF_VEC + L * H * 4; }
   static_assert(OFF_RAY % 16 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
 
-template <int H>
-__global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) {
-  using C = LR<H>;
+template <int H, int CW, int RT_>
+__global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
+  using C = LR<H, CW, RT_>;
+  constexpr int RC_THREADS = C::THREADS;
   constexpr int RT = C::RT, BM = C::BM, TN = C::TN, UPL = C::UPL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = a.L, k_pad = a.k_pad;
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
     if (b < a.batch) {
       float z = w7s[3 * H + o];
 #pragma unroll
-      for (int w = 0; w < RC_CW; ++w) z += zps[(w * BM + ray) * 3 + o];
+      for (int w = 0; w < CW; ++w) z += zps[(w * BM + ray) * 3 + o];
       const float pv = 1.f / (1.f + expf(-z));
       if (a.pred != nullptr) a.pred[(int64_t)b * 3 + o] = pv;
       if (a.img != nullptr) {
@@ -361,20 +364,20 @@ __global__ __launch_bounds__(RC_THREADS) void rchain_kernel(const RchainArgs a) 
   }
 }
 
-template <int H>
+template <int H, int CW, int RT_>
 int launch_typed(const RchainArgs& a_in, hipStream_t stream) {
-  using C = LR<H>;
+  using C = LR<H, CW, RT_>;
   RchainArgs a = a_in;
   a.table_big = a.num_vertices * (int64_t)a.k_pad * 2 >= ((int64_t)1 << 32);
   const int lds = C::lds_bytes(a.L);
   INF_CHECK_ARG(lds <= 160 * 1024, "rchain: LDS budget exceeded");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)rchain_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)rchain_kernel<H, CW, RT_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
-  const int64_t grid = ceil_div(a.batch, RC_BM);
-  rchain_kernel<H><<<dim3((unsigned)grid), dim3(RC_THREADS), lds, stream>>>(a);
+  const int64_t grid = ceil_div(a.batch, C::BM);
+  rchain_kernel<H, CW, RT_><<<dim3((unsigned)grid), dim3(C::THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -390,8 +393,13 @@ int launch_rchain(const RchainArgs& a, hipStream_t stream) {
   INF_CHECK_ARG(a.nchunk == ceil_div(a.k_pad, RC_KC), "rchain: feature chunking");
   INF_CHECK_ARG(a.pred != nullptr || (a.img != nullptr && a.hit != nullptr), "rchain: no output");
   for (int i = 0; i < a.nblk; ++i) INF_CHECK_ARG(a.blk[i].img != nullptr, "rchain: weight image missing");
-  if (a.H == 256) return launch_typed<256>(a, stream);
-  return launch_typed<128>(a, stream);
+  // INF_RCHAIN_CFG=84 / 42: <8 waves, 4 ray tiles> / <4 waves, 2 ray tiles>
+  static const int cfg = [] {
+    const char* e = std::getenv("INF_RCHAIN_CFG");
+    return e != nullptr ? std::atoi(e) : 84;
+  }();
+  if (a.H == 256) return cfg == 42 ? launch_typed<256, 4, 2>(a, stream) : launch_typed<256, 8, 4>(a, stream);
+  return cfg == 42 ? launch_typed<128, 4, 2>(a, stream) : launch_typed<128, 8, 4>(a, stream);
 }
 
 }  // namespace inf
