@@ -395,52 +395,74 @@ def render_bench(args, device):
     hit = torch.randperm(H * W, device=device)[:nhit]
     img = torch.empty((H * W, 3), device=device)
     offs = list(range(0, nhit, chunk))
-    batches = [plans[j % nstreams].make_batch(source=src, offset=o, batch=min(chunk, nhit - o))
-               for j, o in enumerate(offs)]
+    T = src.table_for(plan)
+    project = args.mode == "bf16" and plan.can_project() and os.environ.get("INF_RENDER_PROJECT", "1") != "0"
+    P = plan.project_table(T) if project else None
+    batches = {False: [plans[j % nstreams].make_batch(source=src, offset=o, batch=min(chunk, nhit - o))
+                       for j, o in enumerate(offs)]}
+    if project:  # no workspace behind a projected batch: the frame's hits in one persistent launch
+        batches[True] = [plan.make_batch(source=src, offset=0, batch=nhit, projected=P)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
 
-    def frame():
+    def frame(pj):
         img.fill_(1.0)
+        if pj:  # the vertices' first-layer projections under the current weights, every frame
+            plan.project_table(T, out=P)
         cur = torch.cuda.current_stream()
         for st in streams[1:]:
             st.wait_stream(cur)
         # chunks round-robin over the plans/streams: one chunk's gather overlaps another's chain
-        for j, (o, b) in enumerate(zip(offs, batches)):
+        for j, (o, b) in enumerate(zip([0] if pj else offs, batches[pj])):
             with torch.cuda.stream(streams[j % nstreams]):
                 plans[j % nstreams].render(b, hit[o:o + b.batch], None, img)
         for st in streams[1:]:
             cur.wait_stream(st)
 
-    frame()
-    torch.cuda.synchronize()
-    reps = 5
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        frame()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    def timed(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ms_gather = timed(lambda: frame(False))
+    ms = timed(lambda: frame(True)) if project else ms_gather
+    ms_proj = timed(lambda: plan.project_table(T, out=P)) if project else None
     # both t_min terms of the frame: forward FLOPs of the hits vs the
     # dense MFMA peak; table rows + ids / bary / hit index per hit, the image (fill + pixel
-    # writes) and one pass of the bf16 weights vs HBM
+    # writes) and one pass of the bf16 weights vs HBM.  Projected frames: the projection
+    # GEMM (V x k_pad x 2H) reads the table once and writes the V x 2H projections; each
+    # hit then reads three 2H-wide rows and runs the hidden layers and the head only.
     L, Hd, k = args.layers, args.hidden, args.k
     k_pad = -(-k // 128) * 128
-    fwd = 2 * (2 * k * Hd + (L - 2) * Hd * Hd + 3 * Hd)
-    flops = nhit * fwd
-    byts = nhit * (3 * k_pad * 2 + 12 + 12 + 8 + 12) + H * W * 12 + 2 * (2 * k_pad * Hd + (L - 2) * Hd * Hd)
+    wbytes = 2 * (2 * k_pad * Hd + (L - 2) * Hd * Hd)
+    per_hit_io = 12 + 12 + 8 + 12
+    if project:
+        Vp = -(-V // 128) * 128
+        flops = Vp * 2 * k_pad * 2 * Hd + nhit * 2 * ((L - 2) * Hd * Hd + 3 * 2 * Hd + 3 * Hd)
+        byts = (V * k_pad * 2 + Vp * 2 * Hd * 2 + nhit * (3 * 2 * Hd * 2 + per_hit_io) + H * W * 12 + wbytes)
+    else:
+        flops = nhit * 2 * (2 * k * Hd + (L - 2) * Hd * Hd + 3 * Hd)
+        byts = nhit * (3 * k_pad * 2 + per_hit_io) + H * W * 12 + wbytes
     t_mfma = flops / (PEAK[args.mode] * 1e12) * 1e3
     t_hbm = byts / (HBM_PEAK * 1e9) * 1e3
     roof = {"flops": flops, "bytes": byts, "t_mfma_ms": t_mfma, "t_hbm_ms": t_hbm,
             "bound": "mfma" if t_mfma >= t_hbm else "hbm", "mfma_frac": t_mfma / ms, "hbm_frac": t_hbm / ms,
             "frac": max(t_mfma, t_hbm) / ms, "achieved_tflops": flops / (ms * 1e-3) / 1e12,
             "achieved_gbs": byts / (ms * 1e-3) / 1e9}
-    tr = _pmc_traffic(f"rchain_{args.mode}_render_{chunk}")
+    tr = _pmc_traffic(f"rchain_{args.mode}_render_{chunk}" + ("_proj" if project else ""))
     if tr is not None:  # measured HBM bytes of one launch (PMC), over the frame's launches
         roof["traffic_per_launch"] = tr
         roof["traffic"] = tr * len(offs)
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
-            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams, "roofline": roof}
+            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams,
+            "path": "projected table (inf_project_table per frame + rchain)" if project else "feature gather rchain",
+            "projection_ms": ms_proj, "ms_per_frame_feature_gather": ms_gather,
+            "feature_gather_pixels_per_s": H * W / (ms_gather * 1e-3), "roofline": roof}
 
 
 def torus_mesh(nu=640, nv=320, R=1.0, r=0.4):

@@ -44,7 +44,10 @@ enum { INF_LOSS_L2 = 0, INF_LOSS_L1 = 1, INF_LOSS_CAUCHY = 2 }; /* config.py:113
  * barycentric hit position x (ray_dataloader.py:134-136), as is (XYZ) or encoded:
  *   RFF  [cos e | sin e | x?], e_j = sum_c (2 pi x_c) B[c][j]   (layers.py:28-39)
  *   FF   [cos e | sin e | x?], e_{c k + f} = x_c band_f        (layers.py:6-25)     */
-enum { INF_ENC_NONE = 0, INF_ENC_XYZ = 1, INF_ENC_RFF = 2, INF_ENC_FF = 3 };
+enum { INF_ENC_NONE = 0, INF_ENC_XYZ = 1, INF_ENC_RFF = 2, INF_ENC_FF = 3,
+       /* table = inf_project_table output [V][2H] bf16 (forward-only: inf_render /
+        * inf_forward with save = 0 of bf16 plans) */
+       INF_ENC_PROJECTED = 4 };
 
 /* TextureField architecture (model.py:12-96, make_model model.py:199-258). */
 typedef struct inf_mlp_desc {
@@ -246,6 +249,19 @@ int inf_adam(inf_plan* plan, int step, float lr, inf_stream_t stream);
  * and must already hold the background. */
 int inf_render(inf_plan* plan, const inf_batch* batch, const int64_t* hit, const int64_t* pixel_map,
                float* img, inf_stream_t stream);
+
+/* Projected table for repeated forward passes over one eigenfunction table (rendering):
+ * out[v][0:H] = W_0 E[v] and out[v][H:2H] = W_y E[v] (the first layer's and the skip
+ * layer's input weights, no biases; model.py:43-47, layers.py:60-62), bf16, from the
+ * packed bf16 table [num_vertices][k_pad] and the plan's current bf16 weight shadow.
+ * Both layers are linear in the features, so a hit's pre-activations are the
+ * barycentric interpolation of its vertices' rows: a batch with encoding
+ * INF_ENC_PROJECTED and table = out gathers 2H instead of k_pad values per vertex and
+ * skips the two k_pad-deep layers.  out has inf_projected_rows(num_vertices) rows
+ * (128-row multiple); valid until the weights change.  Replaces nothing in the
+ * reference: a reassociation of renderer.py:104-110's model(batch). */
+int64_t inf_projected_rows(int64_t num_vertices);
+int inf_project_table(inf_plan* plan, const void* table, int64_t num_vertices, void* out, inf_stream_t stream);
 
 /* Diagnostics: re-launch one stage of the last saved training step on its saved
  * inputs (used by bench.py to time a single kernel with HIP events).  Stages:

@@ -75,6 +75,7 @@ struct inf_plan {
   int64_t o_hw = 0, o_hb = 0;                             // head partials
   int64_t o_loss = 0;                                     // chain per-tile loss partials
   int64_t table_bytes = 0;
+  int64_t o_pcat = -1;  // shadow offset of [W_0; W_y] (inf_project_table)
 
   // bound buffers
   float* params = nullptr;
@@ -188,6 +189,12 @@ int build_layout(inf_plan* p) {
         sh = align_up(sh + (int64_t)H * H * 2);
       }
     }
+  }
+  // [W_0; W_y] row-major, the B operand of inf_project_table's single N = 2H GEMM (each
+  // table tile read once; refreshed from the two shadows per call)
+  if (p->mode == INF_MODE_BF16 && s >= 0 && s < L - 1) {
+    p->o_pcat = sh;
+    sh = align_up(sh + 2 * (int64_t)H * p->k_pad * 2);
   }
   p->shadow_bytes = sh;
 
@@ -824,6 +831,7 @@ bool use_rchain(const inf_plan* p, const inf_batch* b) {
   if (!use_chain(p) || !rchain_supported(p->H, p->L, p->k_pad) || w0->f_off < 0 || wy->f_off < 0) return false;
   for (int l = 1; l <= p->L - 2; ++l)
     if (p->weight_seg(l, 0)->f_off < 0) return false;
+  if (b->encoding == INF_ENC_PROJECTED) return b->table != nullptr && b->table_dtype == INF_DTYPE_BF16 && b->vids != nullptr;
   return b->table != nullptr && b->encoding == INF_ENC_NONE && b->table_dtype == INF_DTYPE_BF16 &&
          b->vids != nullptr && !b->offset_from_ctrl && std::getenv("INF_NO_RCHAIN") == nullptr;
 }
@@ -866,6 +874,11 @@ int run_rchain(inf_plan* p, const inf_batch* b, float* pred, const int64_t* hit,
     return INF_OK;
   };
   int rc;
+  if (b->encoding == INF_ENC_PROJECTED) {
+    // projected table (inf_project_table, rproj.hip): no feature chunks, the hidden layers
+    a.projected = 1;
+    a.nchunk = 0;
+  }
   for (int c = 0; c < a.nchunk; ++c) {
     const int nb = std::min(RC_KC, p->k_pad - c * RC_KC) / (32 * upl);
     const int kb = c * (RC_KC / 32);
@@ -896,9 +909,21 @@ int run_rchain(inf_plan* p, const inf_batch* b, float* pred, const int64_t* hit,
 int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool loss, const int64_t* hit,
                  const int64_t* pixel_map, float* img, hipStream_t st) {
   INF_CHECK_ARG(b != nullptr, "null batch");
+  int rc;
+  if (b->encoding == INF_ENC_PROJECTED) {
+    // no workspace: any number of rays per call (a whole frame in one persistent launch)
+    INF_CHECK_ARG(b->batch >= 1, "empty batch");
+    INF_CHECK_ARG(b->offset_from_ctrl == 0, "projected batches take an explicit offset");
+    if (save || loss || !use_rchain(p, b)) {
+      set_error("projected tables feed the forward-only register chain (bf16 plan, inference) only");
+      return INF_ERR_UNSUPPORTED;
+    }
+    if ((rc = run_rchain(p, b, pred, hit, pixel_map, img, st))) return rc;
+    p->saved = false;
+    return INF_OK;
+  }
   int Bp = 0;
-  int rc = pad_batch(p, b->batch, save, &Bp);
-  if (rc) return rc;
+  if ((rc = pad_batch(p, b->batch, save, &Bp))) return rc;
   if (!save && !loss && use_rchain(p, b)) {
     if ((rc = run_rchain(p, b, pred, hit, pixel_map, img, st))) return rc;
     p->saved = false;
@@ -1134,6 +1159,10 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
                 "train_step: unknown flags");
   const int xslot = (flags & INF_STEP_XSLOT0) ? 0 : (flags & INF_STEP_XSLOT1) ? 1 : -1;
   INF_CHECK_ARG(batch != nullptr && batch->rgb != nullptr, "train_step: batch with target colours required");
+  if (batch->encoding == INF_ENC_PROJECTED) {
+    set_error("train_step: projected tables are forward-only");
+    return INF_ERR_UNSUPPORTED;
+  }
   INF_CHECK_ARG(p->grads != nullptr || apply_adam, "train_step: grads not bound");
   INF_CHECK_ARG(!apply_adam || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr), "train_step: Adam state");
   hipStream_t st = (hipStream_t)stream;
@@ -1232,6 +1261,74 @@ int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const in
   }
   INF_CHECK_ARG(hit != nullptr && img != nullptr, "render: hit indices and image required");
   return forward_impl(p, batch, nullptr, false, false, hit, pixel_map, img, (hipStream_t)stream);
+}
+
+int64_t inf_projected_rows(int64_t num_vertices) { return num_vertices <= 0 ? 0 : round_up(num_vertices, 128); }
+
+// out[v] = (W_0 E[v], W_y E[v]) in bf16: one NT GEMM per row range over the packed table
+// (A = E [V][k_pad], B = [W_0; W_y] [2H][k_pad] bf16, C = out [.][2H]).  The
+// last partial 128-row tile is staged through X0 (the GEMM reads whole tiles; out has
+// inf_projected_rows(V) rows, so its stores stay in bounds).
+int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void* out, inf_stream_t stream) {
+  if (p == nullptr || !p->bound) {
+    set_error("plan not bound");
+    return INF_ERR_STATE;
+  }
+  INF_CHECK_ARG(table != nullptr && out != nullptr && num_vertices >= 1, "project_table: table and output required");
+  if (p->mode != INF_MODE_BF16 || p->weight_seg(p->s, 1) == nullptr) {
+    set_error("project_table: bf16 plans with the input skip layer only");
+    return INF_ERR_UNSUPPORTED;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int H = p->H, k_pad = p->k_pad;
+  const int64_t full = num_vertices / 128 * 128, tail = num_vertices - full;
+  const size_t row_bytes = (size_t)k_pad * 2;
+  if (tail > 0) {
+    INF_CHECK_ARG(p->bp_max >= 128, "project_table: staging tile");
+    char* x0 = p->W(p->o_x0);
+    INF_HIP_TRY(hipMemsetAsync(x0 + tail * row_bytes, 0, (size_t)(128 - tail) * row_bytes, st));
+    INF_HIP_TRY(hipMemcpyAsync(x0, (const char*)table + full * row_bytes, (size_t)tail * row_bytes,
+                               hipMemcpyDeviceToDevice, st));
+  }
+  const ParamSeg* w[2] = {p->weight_seg(0, 0), p->weight_seg(p->s, 1)};
+  INF_CHECK_ARG(p->o_pcat >= 0 && w[0]->c_pad == k_pad && w[1]->c_pad == k_pad, "project_table: weight layout");
+  char* pcat = p->shadow + p->o_pcat;
+  const size_t wbytes = (size_t)H * k_pad * 2;
+  for (int h = 0; h < 2; ++h)
+    INF_HIP_TRY(hipMemcpyAsync(pcat + h * wbytes, p->shadow + w[h]->w_off, wbytes, hipMemcpyDeviceToDevice, st));
+  // the GEMM's M is a 32-bit row count: the full tiles in slices of 2^24 rows
+  constexpr int64_t SLICE = (int64_t)1 << 24;
+  GemmBatch gb;
+  std::memset(&gb, 0, sizeof(gb));
+  auto flush = [&]() -> int {
+    if (gb.nprob == 0) return INF_OK;
+    const int rc = launch_gemm(gb, p->mode, TILE_128x128, st);
+    std::memset(&gb, 0, sizeof(gb));
+    return rc;
+  };
+  auto add = [&](const void* A, int64_t rows, int64_t r0) -> int {
+    if (gb.nprob + 1 > GEMM_MAX_PROBLEMS)
+      if (int rc = flush()) return rc;
+    GemmProblem& q = gb.p[gb.nprob++];
+    q = blank_problem();
+    q.A[0] = A;
+    q.lda[0] = k_pad;
+    q.B[0] = pcat;
+    q.ldb[0] = k_pad;
+    q.K[0] = k_pad;
+    q.M = (int32_t)rows;
+    q.N = 2 * H;
+    q.C = reinterpret_cast<char*>(out) + r0 * 2 * H * 2;
+    q.ldc = 2 * H;
+    return INF_OK;
+  };
+  int rc;
+  for (int64_t m0 = 0; m0 < full; m0 += SLICE)
+    if ((rc = add((const char*)table + m0 * row_bytes, std::min(SLICE, full - m0), m0))) return rc;
+  if (tail > 0 && (rc = add(p->W(p->o_x0), 128, full))) return rc;
+  if ((rc = flush())) return rc;
+  p->saved = false;  // X0 held the staged tail
+  return INF_OK;
 }
 
 int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double* flops, double* bytes,

@@ -230,6 +230,7 @@ __global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[t][j] = accy[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+
 #pragma unroll 1
   for (int i = 0; i < a.nblk; ++i) {
     const C3Block& B = a.blk[i];
@@ -385,6 +386,7 @@ int launch_typed(const RchainArgs& a_in, hipStream_t stream) {
 }  // namespace
 
 int launch_rchain(const RchainArgs& a, hipStream_t stream) {
+  if (a.projected) return launch_rproj(a, stream);
   INF_CHECK_ARG(rchain_supported(a.H, a.L, a.k_pad), "rchain: unsupported shape");
   INF_CHECK_ARG(a.batch >= 1, "rchain: empty batch");
   INF_CHECK_ARG(a.table != nullptr && a.vids != nullptr && a.bary != nullptr, "rchain: inputs");

@@ -14,7 +14,8 @@ struct RchainArgs {
   int32_t L, s, H, k_pad;
   int32_t batch;  // rays of this launch
   // rays: ray b reads row r = ray_idx ? ray_idx[idx_offset + b] : idx_offset + b of vids / bary
-  const bf16* table;  // [V][k_pad] bf16
+  const bf16* table;  // [V][k_pad] bf16, or the projected table [V][2H] (projected = 1)
+  int32_t projected;  // table rows are (W_0 E[v], W_y E[v]) (inf_project_table)
   int64_t num_vertices;
   int32_t table_big;  // 4 GiB or more: 64-bit row addresses
   const void* vids;
@@ -49,6 +50,9 @@ inline bool rchain_supported(int H, int L, int k_pad) {
          RC_KC % H == 0 && rchain_blocks(H, L, k_pad) <= RC_MAX_BLOCKS;
 }
 
+// projected = 0: rchain.hip; 1: the persistent projected-table chain (rproj.hip; blk =
+// the hidden layers 1 .. L - 2, nchunk = 0)
 int launch_rchain(const RchainArgs& a, hipStream_t stream);
+int launch_rproj(const RchainArgs& a, hipStream_t stream);
 
 }  // namespace inf

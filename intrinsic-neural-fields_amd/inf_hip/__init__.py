@@ -22,7 +22,7 @@ LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
 STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1 = 1, 2, 4, 8  # inf_train_step flags
-ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF = 0, 1, 2, 3
+ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF, ENC_PROJECTED = 0, 1, 2, 3, 4
 ENC_CODES = {"xyz": ENC_XYZ, "rff": ENC_RFF, "ff": ENC_FF}
 
 c_void_p, c_int, c_int32, c_int64, c_float, c_double = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int32,
@@ -95,6 +95,8 @@ _SIGNATURES = {
     "inf_train_step": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_int, c_void_p]),
     "inf_adam": (c_int, [c_void_p, c_int, c_float, c_void_p]),
     "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
+    "inf_projected_rows": (c_int64, [c_int64]),
+    "inf_project_table": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_plan_last_step_path": (c_int, [c_void_p]),
     "inf_prefetch_batch": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_void_p]),

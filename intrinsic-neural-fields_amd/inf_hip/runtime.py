@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
+from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, ENC_PROJECTED, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
                MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo, c_int64, c_void_p,
                check, lib)
 
@@ -315,9 +315,10 @@ class Plan:
         check(lib.inf_plan_set_adam(self.handle, beta1, beta2, eps), "set_adam")
 
     def make_batch(self, *, features=None, rgb=None, source=None, ray_idx=None, offset=0, batch=None, loss_count=0,
-                   offset_from_ctrl=False, loss=None, xyz=None) -> Batch:
+                   offset_from_ctrl=False, loss=None, xyz=None, projected=None) -> Batch:
         """Rays of a RaySource (gathered, or interpolated + encoded under self.encoding),
-        given positions `xyz` [B, 3] (encoded), or given features [B, in_dim]."""
+        given positions `xyz` [B, 3] (encoded), or given features [B, in_dim].
+        projected: the source table's project_table() output (forward-only batches)."""
         b = Batch()
         b.encoding = ENC_NONE
         enc = self.encoding
@@ -368,12 +369,18 @@ class Plan:
                 b.num_rays = ray_idx.numel()  # the kernels never read past the permutation
             else:
                 b.num_rays = src.vids32.shape[0]
+            if projected is not None:
+                if projected.dtype != torch.bfloat16 or projected.shape[1] != 2 * self.desc.hidden or \
+                        projected.shape[0] < T.shape[0]:
+                    raise ValueError("projected table does not match this plan / source")
+                b.table = projected.data_ptr()
+                b.encoding = ENC_PROJECTED
             b.idx_offset = int(offset)
             b.offset_from_ctrl = 1 if offset_from_ctrl else 0
             b.batch = int(batch)
         b.loss_count = int(loss_count)
         b.loss = -1 if loss is None else LOSS_CODES[loss]
-        if b.batch < 1 or b.batch > self.max_batch:
+        if b.batch < 1 or (b.batch > self.max_batch and b.encoding != ENC_PROJECTED):
             raise ValueError(f"batch of {b.batch} rays outside this plan's range 1..{self.max_batch}")
         return b
 
@@ -408,6 +415,23 @@ class Plan:
     def render(self, b: Batch, hit: torch.Tensor, pixel_map: torch.Tensor | None, img: torch.Tensor):
         check(lib.inf_render(self.handle, ctypes.byref(b), ptr(hit), ptr(pixel_map), ptr(img), stream_handle()),
               "render")
+
+    def can_project(self) -> bool:
+        """project_table() applies: bf16 eigenfunction plans with the input skip layer."""
+        d = self.desc
+        return self.encoding is None and self.gemm_dtype == torch.bfloat16 and 0 <= d.skip < d.num_layers - 1
+
+    def project_table(self, T: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """inf_project_table: rows (W_0 E[v], W_y E[v]) of a packed bf16 table T [V, in_pad]
+        under the current weights, bf16 [inf_projected_rows(V), 2H]."""
+        require_hip(T)
+        if T.dtype != torch.bfloat16 or T.dim() != 2 or T.shape[1] != self.in_pad or not T.is_contiguous():
+            raise ValueError("project_table reads the packed bf16 [V, in_pad] table")
+        rows = int(lib.inf_projected_rows(T.shape[0]))
+        if out is None:
+            out = torch.empty((rows, 2 * self.desc.hidden), dtype=torch.bfloat16, device=T.device)
+        check(lib.inf_project_table(self.handle, ptr(T), T.shape[0], ptr(out), stream_handle()), "project_table")
+        return out
 
     def run_stage(self, stage: int, layer: int = 0, b: Batch | None = None):
         """Re-launch one stage of the last saved step; returns (flops, bytes) per launch."""

@@ -22,6 +22,7 @@ from mesh import load_first_k_eigenfunctions
 from utils import load_trained_model
 
 RENDER_CHUNK = 1 << 18
+PROJECTED_CHUNK = 1 << 30
 
 
 def make_renderer_with_trained_model(config, device="cuda"):
@@ -36,6 +37,16 @@ def make_renderer_with_trained_model(config, device="cuda"):
     model = load_trained_model(config["model"], weights_path, device, mesh=None)
     return Renderer(model, mesh, eigenfunctions=efuncs, device=device, H=config["data"]["img_height"],
                     W=config["data"]["img_width"])
+
+
+def _project_enabled(num_hits, num_vertices):
+    """INF_RENDER_PROJECT=1 / 0 forces the projected-table render on / off; by default it
+    runs when the frame has at least half as many hits as the table has vertices (the
+    projection GEMM costs about what the per-hit input layers save at one hit per vertex)."""
+    env = os.environ.get("INF_RENDER_PROJECT")
+    if env is not None:
+        return env != "0"
+    return 2 * num_hits >= num_vertices
 
 
 def _to_host(img):
@@ -145,9 +156,15 @@ class Renderer:
         src._tables = self._table_cache["tables"]
         chunk = min(RENDER_CHUNK, num_rays)
         plan = self.model.hip_plan(chunk)
+        # enough hits per vertex: interpolate the vertices' first-layer projections instead
+        # of their features (inf_project_table; recomputed per call, the weights may move)
+        proj = None
+        if plan.can_project() and _project_enabled(num_rays, E.shape[0]):
+            proj = plan.project_table(src.table_for(plan))
+            chunk = min(num_rays, PROJECTED_CHUNK)  # no workspace: the frame in one persistent launch
         for low in range(0, num_rays, chunk):
             n = min(chunk, num_rays - low)
-            b = plan.make_batch(source=src, offset=low, batch=n)
+            b = plan.make_batch(source=src, offset=low, batch=n, projected=proj)
             plan.render(b, hit[low:low + n], pixel_map, img)
         self.model._rt.saved_gen = None
         img = img.reshape(self.H, self.W, 3)

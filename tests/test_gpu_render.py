@@ -4,7 +4,10 @@ register chain (csrc/rchain.hip) against the oracle on a sample of hits (predict
 within 2e-2, the bf16 bar of test_gpu_kernels.py) and against the LDS-ring chain on the
 whole frame (5e-4), plus whole-frame properties: background pixels untouched, every hit
 pixel written, values in (0, 1), no NaN; and the no-grad forward of loader batches
-(shuffled ray indices) through the same kernel."""
+(shuffled ray indices) through the same kernel.  The projected-table render
+(inf_project_table + INF_ENC_PROJECTED batches: the vertices' W_0 / W_y rows interpolated
+per hit) against the oracle, the feature-gather chain and a torch fp32 projection, with
+tail tiles, out-of-range ids, the 128-wide MLP and the forward-only guard."""
 import numpy as np
 import pytest
 import torch
@@ -36,13 +39,16 @@ def _setup(k=1024, H=256, L=8, s=4, V=400_000, HW=2048 * 2048, seed=0):
     return m, w, E, src, vids, bary, hit.cuda(), HW
 
 
-def _render(m, src, hit, HW, chunk=1 << 18):
+def _render(m, src, hit, HW, chunk=1 << 18, project=False):
     rt = m.hip_runtime()
     plan = m.hip_plan(chunk)
     img = torch.ones((HW, 3), device="cuda")
     n = hit.shape[0]
+    proj = plan.project_table(src.table_for(plan)) if project else None
+    if project:
+        chunk = n  # projected batches are not bounded by the plan's max batch: one launch
     for lo in range(0, n, chunk):
-        b = plan.make_batch(source=src, offset=lo, batch=min(chunk, n - lo))
+        b = plan.make_batch(source=src, offset=lo, batch=min(chunk, n - lo), projected=proj)
         plan.render(b, hit[lo:lo + b.batch], None, img)
     torch.cuda.synchronize()
     del rt
@@ -103,3 +109,129 @@ def test_forward_loader_batches_rchain(monkeypatch):
     rows = np.concatenate(idx)
     p_ref, _ = O.mlp_forward(w, O.gather(E.numpy(), vids.numpy()[rows], bary.numpy()[rows]), 8, 4)
     assert np.abs(pred - p_ref).max() < 2e-2
+
+
+def _oracle_sample(w, E, vids, bary, hit_np, L, s, n=1000, seed=3):
+    rng = np.random.default_rng(seed)
+    sample = np.concatenate([rng.choice(hit_np.shape[0], min(n, hit_np.shape[0]), replace=False),
+                             [0, hit_np.shape[0] - 1]])
+    sv = vids.numpy()[sample]
+    rows, inv = np.unique(sv.reshape(-1), return_inverse=True)
+    E_sub = E[torch.from_numpy(rows).cuda()].cpu().numpy()
+    X = O.gather(E_sub, inv.reshape(sv.shape), bary.numpy()[sample])
+    p_ref, _ = O.mlp_forward(w, X, L, s)
+    return sample, p_ref
+
+
+def test_render_projected_config_e():
+    """The projected render at config E's size: the oracle bar (2e-2) on a sample, and
+    the feature-gather register chain on the whole frame.  The two differ by where bf16
+    rounds (the interpolated features vs the vertices' projections): 5e-3 in RGB."""
+    m, w, E, src, vids, bary, hit, HW = _setup()
+    img = _render(m, src, hit, HW, project=True).cpu().numpy()
+    img_g = _render(m, src, hit, HW).cpu().numpy()
+    hit_np = hit.cpu().numpy()
+    mask = np.zeros(HW, bool)
+    mask[hit_np] = True
+    assert np.isfinite(img).all() and (img[~mask] == 1.0).all()
+    assert ((img[mask] > 0) & (img[mask] < 1)).all()
+    np.testing.assert_allclose(img, img_g, atol=5e-3)
+    sample, p_ref = _oracle_sample(w, E, vids, bary, hit_np, 8, 4)
+    assert np.abs(img[hit_np[sample]] - p_ref).max() < 2e-2
+
+
+@pytest.mark.parametrize("V", [100, 256, 1000])
+def test_project_table_vs_torch(V):
+    """inf_project_table against torch fp32 on the bf16 operands: whole tiles, a staged
+    tail tile (V % 128 != 0) and a table smaller than one tile."""
+    import model as M
+    torch.manual_seed(1)
+    k, H = 512, 256
+    m = M.make_model({"k": k, "num_layers": 8, "mlp_hidden_dim": H, "skip_layer_idx": 4}).cuda()
+    m.kernel_mode = "bf16"
+    plan = m.hip_plan(1024)
+    E = torch.randn((V, k), device="cuda") * 0.3
+    from inf_hip import runtime
+    T = runtime.pack_table(E, plan.in_pad, torch.bfloat16)
+    P = plan.project_table(T)
+    torch.cuda.synchronize()
+    assert P.shape == (((V + 127) // 128) * 128, 2 * H)
+    sd = {n: p.detach() for n, p in m.named_parameters()}
+    W0 = [v for n, v in sd.items() if n.endswith("weight") and v.shape == (H, k)]
+    assert len(W0) == 2  # layer 0 and the skip layer's Ly (parameter order)
+    Eb = T[:, :k].float()
+    ref = torch.cat([Eb @ W.bfloat16().float().t() for W in W0], 1)
+    got = P[:V].float()
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+
+
+def test_render_projected_small_models(monkeypatch):
+    """The 128-wide MLP (TN = 1 per wave), ragged batches and out-of-range vertex ids
+    (rows read as zero, as the gather does) against the oracle and the gather chain."""
+    import model as M
+    from inf_hip import runtime
+    rng = np.random.default_rng(5)
+    for (k, H, L, s) in [(256, 128, 6, 3), (1024, 256, 8, 4)]:
+        V, N, HW = 777, 3001, 4096
+        E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32) * 0.3).cuda()
+        vids = torch.from_numpy(rng.integers(0, V, (N, 3)))
+        vids[7, 1] = V + 5  # out of range: the whole feature row reads as zero
+        bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32))
+        hit = torch.from_numpy(np.sort(rng.choice(HW, N, replace=False))).cuda()
+        torch.manual_seed(0)
+        m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()
+        m.kernel_mode = "bf16"
+        w = {n: p.detach().cpu().numpy() for n, p in m.named_parameters()}
+        src = runtime.RaySource(E, vids.cuda(), bary.cuda(), None, validate=False)
+        img = _render(m, src, hit, HW, chunk=1024, project=True).cpu().numpy()
+        img_g = _render(m, src, hit, HW, chunk=1024).cpu().numpy()
+        np.testing.assert_allclose(img, img_g, atol=5e-3)
+        hit_np = hit.cpu().numpy()
+        X = O.gather(E.cpu().numpy(), np.minimum(vids.numpy(), V - 1), bary.numpy())
+        X[7] = 0.0
+        p_ref, _ = O.mlp_forward(w, X, L, s)
+        assert np.abs(img[hit_np] - p_ref).max() < 2e-2
+
+
+def test_projected_batches_are_forward_only():
+    import model as M
+    from inf_hip import runtime
+    torch.manual_seed(0)
+    m = M.make_model({"k": 256, "num_layers": 6, "mlp_hidden_dim": 128, "skip_layer_idx": 3}).cuda()
+    m.kernel_mode = "bf16"
+    plan = m.hip_plan(1024)
+    E = torch.randn((300, 256), device="cuda")
+    vids = torch.randint(0, 300, (1024, 3), device="cuda")
+    bary = torch.full((1024, 3), 1 / 3, device="cuda")
+    rgb = torch.rand((1024, 3), device="cuda")
+    src = runtime.RaySource(E, vids, bary, rgb)
+    P = plan.project_table(src.table_for(plan))
+    b = plan.make_batch(source=src, offset=0, batch=1024, projected=P)
+    pred = torch.empty((1024, 3), device="cuda")
+    plan.forward(b, pred, save=False)  # the no-grad forward runs
+    with pytest.raises(RuntimeError):
+        plan.train_step(b, pred, apply_adam=True)
+    with pytest.raises(RuntimeError):
+        plan.forward(b, pred, save=True)
+
+
+def test_renderer_projected_matches_gather(monkeypatch):
+    """Renderer.render_hits with the projection forced on and off."""
+    import model as M
+    from renderer import Renderer
+    rng = np.random.default_rng(6)
+    V, N, Hh, Ww, k = 500, 2000, 64, 64, 256
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32) * 0.3)
+    torch.manual_seed(0)
+    m = M.make_model({"k": k, "num_layers": 6, "mlp_hidden_dim": 128, "skip_layer_idx": 3}).cuda()
+    m.kernel_mode = "bf16"
+    r = Renderer(m, None, eigenfunctions=E, H=Hh, W=Ww, device="cuda")
+    vids = torch.from_numpy(rng.integers(0, V, (N, 3)))
+    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32))
+    hit = torch.from_numpy(np.sort(rng.choice(Hh * Ww, N, replace=False)))
+    monkeypatch.setenv("INF_RENDER_PROJECT", "1")
+    a = r.render_hits(vids, bary, hit)
+    monkeypatch.setenv("INF_RENDER_PROJECT", "0")
+    b = r.render_hits(vids, bary, hit)
+    np.testing.assert_allclose(a, b, atol=5e-3)

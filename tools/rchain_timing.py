@@ -2,7 +2,7 @@
 (rchain.hip) for wave 0 of workgroup 0 and of the middle workgroup, on the bench's
 render configuration (k=1024 8x256 bf16, V=400k random rows), plus the launch time.
 
-    python tools/rchain_timing.py [hits] [coherent(0/1)]
+    python tools/rchain_timing.py [hits] [coherent(0/1)]      (PROJ=1: projected table)
 """
 import ctypes
 import os
@@ -35,7 +35,22 @@ src = runtime.RaySource(E, vids, bary, None)
 plan = m.hip_plan(n)
 hit = torch.arange(n, device="cuda")
 img = torch.ones((n, 3), device="cuda")
-b = plan.make_batch(source=src, offset=0, batch=n)
+proj = None
+if os.environ.get("PROJ") == "1":
+    T = src.table_for(plan)
+    proj = plan.project_table(T)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        plan.project_table(T, out=proj)
+    e1.record()
+    torch.cuda.synchronize()
+    pm = e0.elapsed_time(e1) / 10
+    fl = proj.shape[0] * 2 * 1024 * 512
+    print(f"project_table: {pm * 1e3:.1f} us for V={V} -> {fl / pm / 1e9:.0f} TFLOP/s, "
+          f"{(V * 2048 + proj.numel() * 2) / pm / 1e6:.0f} GB/s")
+b = plan.make_batch(source=src, offset=0, batch=n, projected=proj)  # (n may exceed max_batch when projected)
 for _ in range(3):
     plan.render(b, hit, None, img)
 torch.cuda.synchronize()
