@@ -21,6 +21,7 @@
 #include "head.hpp"
 #include "lgemm.hpp"
 #include "rchain.hpp"
+#include "blaslt.hpp"
 
 namespace inf {
 
@@ -1265,8 +1266,9 @@ int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const in
 
 int64_t inf_projected_rows(int64_t num_vertices) { return num_vertices <= 0 ? 0 : round_up(num_vertices, 128); }
 
-// out[v] = (W_0 E[v], W_y E[v]) in bf16: one NT GEMM per row range over the packed table
-// (A = E [V][k_pad], B = [W_0; W_y] [2H][k_pad] bf16, C = out [.][2H]).  The
+// out[v] = (W_0 E[v], W_y E[v]) in bf16: one plain NT GEMM over the packed table (A = E
+// [V][k_pad], B = [W_0; W_y] [2H][k_pad] bf16, C = out [.][2H]) through hipBLASLt; with
+// INF_PROJECT_GEMM=own the plan's grouped GEMM in 2^24-row slices.  The
 // last partial 128-row tile is staged through X0 (the GEMM reads whole tiles; out has
 // inf_projected_rows(V) rows, so its stores stay in bounds).
 int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void* out, inf_stream_t stream) {
@@ -1281,6 +1283,16 @@ int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void
   }
   hipStream_t st = (hipStream_t)stream;
   const int H = p->H, k_pad = p->k_pad;
+  const ParamSeg* w[2] = {p->weight_seg(0, 0), p->weight_seg(p->s, 1)};
+  INF_CHECK_ARG(p->o_pcat >= 0 && w[0]->c_pad == k_pad && w[1]->c_pad == k_pad, "project_table: weight layout");
+  char* pcat = p->shadow + p->o_pcat;
+  const size_t wbytes = (size_t)H * k_pad * 2;
+  for (int h = 0; h < 2; ++h)
+    INF_HIP_TRY(hipMemcpyAsync(pcat + h * wbytes, p->shadow + w[h]->w_off, wbytes, hipMemcpyDeviceToDevice, st));
+  const char* gsel = std::getenv("INF_PROJECT_GEMM");
+  const bool own = gsel != nullptr && std::string(gsel) == "own";
+  if (!own)  // hipBLASLt: any row count, rows past V untouched
+    return blaslt_gemm_nt_bf16(table, k_pad, pcat, k_pad, out, 2 * H, num_vertices, 2 * H, k_pad, st);
   const int64_t full = num_vertices / 128 * 128, tail = num_vertices - full;
   const size_t row_bytes = (size_t)k_pad * 2;
   if (tail > 0) {
@@ -1290,12 +1302,6 @@ int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void
     INF_HIP_TRY(hipMemcpyAsync(x0, (const char*)table + full * row_bytes, (size_t)tail * row_bytes,
                                hipMemcpyDeviceToDevice, st));
   }
-  const ParamSeg* w[2] = {p->weight_seg(0, 0), p->weight_seg(p->s, 1)};
-  INF_CHECK_ARG(p->o_pcat >= 0 && w[0]->c_pad == k_pad && w[1]->c_pad == k_pad, "project_table: weight layout");
-  char* pcat = p->shadow + p->o_pcat;
-  const size_t wbytes = (size_t)H * k_pad * 2;
-  for (int h = 0; h < 2; ++h)
-    INF_HIP_TRY(hipMemcpyAsync(pcat + h * wbytes, p->shadow + w[h]->w_off, wbytes, hipMemcpyDeviceToDevice, st));
   // the GEMM's M is a 32-bit row count: the full tiles in slices of 2^24 rows
   constexpr int64_t SLICE = (int64_t)1 << 24;
   GemmBatch gb;

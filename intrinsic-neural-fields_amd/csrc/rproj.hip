@@ -40,6 +40,9 @@ using namespace c3;
 #ifndef RP_DEPTH
 #define RP_DEPTH 4
 #endif
+#ifndef RP_BQ
+#define RP_BQ 2
+#endif
 // diagnostics (tools/rchain_timing.py): 1 = loader waves only take part in the barriers
 #ifndef RP_LOADER_IDLE
 #define RP_LOADER_IDLE 0
@@ -355,16 +358,18 @@ __global__ __launch_bounds__(LP<H>::THREADS) void rproj_kernel(const RchainArgs 
       for (int t = 0; t < RT; ++t)
         bv[t] = *reinterpret_cast<const bf16x8*>(act_in + t * C::ACT_T + kb * 1024 + aoffs[kb & 3]);
     };
-    bf16x8 bq[2][RT];
+    constexpr int NB = RP_BQ;  // B-operand buffers: 2 = next k-block's read ahead of the MFMAs
+    bf16x8 bq[NB][RT];
     read_b(0, bq[0]);
 #pragma unroll
     for (int kb = 0; kb < UPL; ++kb) {
-      if (kb + 1 < UPL) read_b(kb + 1, bq[(kb + 1) & 1]);
+      if (NB == 2 && kb + 1 < UPL) read_b(kb + 1, bq[(kb + 1) % NB]);
+      if (NB == 1 && kb > 0) read_b(kb, bq[0]);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bq[kb & 1][t], acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bq[kb % NB][t], acc[t][j], 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         fr[kb % D][j] = kb + D < UPL ? frag(crs, kb + D, j) : frag(nrs, kb + D - UPL, j);

@@ -140,10 +140,14 @@ def test_render_projected_config_e():
     assert np.abs(img[hit_np[sample]] - p_ref).max() < 2e-2
 
 
+@pytest.mark.parametrize("gemm", ["hipblaslt", "own"])
 @pytest.mark.parametrize("V", [100, 256, 1000])
-def test_project_table_vs_torch(V):
+def test_project_table_vs_torch(V, gemm, monkeypatch):
     """inf_project_table against torch fp32 on the bf16 operands: whole tiles, a staged
-    tail tile (V % 128 != 0) and a table smaller than one tile."""
+    tail tile (V % 128 != 0) and a table smaller than one tile; through hipBLASLt and
+    through the plan's own grouped GEMM (INF_PROJECT_GEMM=own)."""
+    if gemm == "own":
+        monkeypatch.setenv("INF_PROJECT_GEMM", "own")
     import model as M
     torch.manual_seed(1)
     k, H = 512, 256
