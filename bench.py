@@ -454,10 +454,17 @@ def render_bench(args, device):
             "bound": "mfma" if t_mfma >= t_hbm else "hbm", "mfma_frac": t_mfma / ms, "hbm_frac": t_hbm / ms,
             "frac": max(t_mfma, t_hbm) / ms, "achieved_tflops": flops / (ms * 1e-3) / 1e12,
             "achieved_gbs": byts / (ms * 1e-3) / 1e9}
-    tr = _pmc_traffic(f"rchain_{args.mode}_render_{chunk}" + ("_proj" if project else ""))
-    if tr is not None:  # measured HBM bytes of one launch (PMC), over the frame's launches
-        roof["traffic_per_launch"] = tr
-        roof["traffic"] = tr * len(offs)
+    if project:  # measured HBM bytes (PMC) of the frame's two launches: projection GEMM + rproj
+        tr_g, tr_p = _pmc_traffic(f"project_gemm_{args.mode}_render"), _pmc_traffic(f"rproj_{args.mode}_render")
+        if tr_g is not None and tr_p is not None:
+            roof["traffic_projection"] = tr_g
+            roof["traffic_rproj"] = tr_p
+            roof["traffic"] = tr_g + tr_p
+    else:
+        tr = _pmc_traffic(f"rchain_{args.mode}_render_{chunk}")
+        if tr is not None:  # measured HBM bytes of one launch (PMC), over the frame's launches
+            roof["traffic_per_launch"] = tr
+            roof["traffic"] = tr * len(offs)
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
             "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams,
             "path": "projected table (inf_project_table per frame + rchain)" if project else "feature gather rchain",

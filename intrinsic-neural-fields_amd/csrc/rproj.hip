@@ -29,6 +29,8 @@
 // at those barriers: I0 record loads of tile + 1, I1 record stores, then the rows in
 // four groups -- loads in one interval, interpolation into Z in the next: W_0 half
 // I2 -> I3, I3 -> I4, W_y half I4 -> I_jy, I_jy -> I_jy+1 (jy >= s + 2: after B_s).
+#include <cstdlib>
+
 #include "c3common.hpp"
 #include "rchain.hpp"
 
@@ -48,9 +50,9 @@ using namespace c3;
 #define RP_LOADER_IDLE 0
 #endif
 
-template <int H>
+template <int H, int CW_>
 struct LP {
-  static constexpr int CW = 8, LW = 4, RT = 4, BM = 64;  // compute waves, loader waves
+  static constexpr int CW = CW_, LW = 4, RT = 4, BM = 64;  // compute waves, loader waves
   static constexpr int THREADS = (CW + LW) * 64, LT = LW * 64;
   static constexpr int TN = H / (16 * CW);
   static constexpr int UPL = H / 32, NT = H / 16;
@@ -71,9 +73,9 @@ struct LP {
   static_assert(OFF_RAY % 16 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
 
-template <int H>
-__global__ __launch_bounds__(LP<H>::THREADS) void rproj_kernel(const RchainArgs a) {
-  using C = LP<H>;
+template <int H, int CW_>
+__global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const RchainArgs a) {
+  using C = LP<H, CW_>;
   constexpr int RT = C::RT, BM = C::BM, TN = C::TN, UPL = C::UPL, CW = C::CW, NH = C::NH, HC = C::HC,
                 THREADS = C::THREADS, LT = C::LT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -426,14 +428,14 @@ __global__ __launch_bounds__(LP<H>::THREADS) void rproj_kernel(const RchainArgs 
   }
 }
 
-template <int H>
+template <int H, int CW_>
 int launch_typed(const RchainArgs& a, hipStream_t stream) {
-  using C = LP<H>;
+  using C = LP<H, CW_>;
   const int lds = C::lds_bytes(a.L);
   INF_CHECK_ARG(lds <= 160 * 1024, "rproj: LDS budget exceeded");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)rproj_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)rproj_kernel<H, CW_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
   static int ncu = 0;
@@ -444,7 +446,7 @@ int launch_typed(const RchainArgs& a, hipStream_t stream) {
   }
   const int64_t ntile = ceil_div(a.batch, C::BM);
   const int grid = (int)std::min<int64_t>(ntile, ncu);
-  rproj_kernel<H><<<dim3((unsigned)grid), dim3(C::THREADS), lds, stream>>>(a);
+  rproj_kernel<H, CW_><<<dim3((unsigned)grid), dim3(C::THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -460,7 +462,14 @@ int launch_rproj(const RchainArgs& a, hipStream_t stream) {
   INF_CHECK_ARG(a.pred != nullptr || (a.img != nullptr && a.hit != nullptr), "rproj: no output");
   for (int i = 0; i < a.nblk; ++i)
     INF_CHECK_ARG(a.blk[i].img != nullptr && a.blk[i].phase == i + 1 && a.blk[i].kb0 == 0, "rproj: weight stream");
-  return a.H == 256 ? launch_typed<256>(a, stream) : launch_typed<128>(a, stream);
+  // compute waves: 8 (32 output features each; default) or INF_RPROJ_WAVES=4 (64 each: half
+  // the LDS operand reads, one compute wave per SIMD)
+  static const int waves = [] {
+    const char* e = std::getenv("INF_RPROJ_WAVES");
+    return e != nullptr && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  if (a.H == 256) return waves == 4 ? launch_typed<256, 4>(a, stream) : launch_typed<256, 8>(a, stream);
+  return waves == 4 ? launch_typed<128, 4>(a, stream) : launch_typed<128, 8>(a, stream);
 }
 
 }  // namespace inf
