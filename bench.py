@@ -467,7 +467,7 @@ def render_bench(args, device):
             roof["traffic"] = tr * len(offs)
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
             "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams,
-            "path": "projected table (inf_project_table per frame + rchain)" if project else "feature gather rchain",
+            "path": "projected table (inf_project_table per frame + rproj)" if project else "feature gather rchain",
             "projection_ms": ms_proj, "ms_per_frame_feature_gather": ms_gather,
             "feature_gather_pixels_per_s": H * W / (ms_gather * 1e-3), "roofline": roof}
 
