@@ -239,3 +239,31 @@ def test_renderer_projected_matches_gather(monkeypatch):
     monkeypatch.setenv("INF_RENDER_PROJECT", "0")
     b = r.render_hits(vids, bary, hit)
     np.testing.assert_allclose(a, b, atol=5e-3)
+
+
+@pytest.mark.parametrize("L,s", [(3, 1), (4, 1), (4, 2), (5, 3), (6, 4), (8, 4)])
+def test_render_projected_layer_schedules(L, s):
+    """rproj's loader/compute barrier schedule for every depth / skip position class: one
+    hidden layer (all row groups in extra intervals), the skip layer last (W_y half after
+    the final hidden layer), the defaults; 40k hits so every workgroup pipelines several
+    tiles (the loader's next-tile work runs)."""
+    import model as M
+    from inf_hip import runtime
+    rng = np.random.default_rng(10 + L)
+    k, H, V, N, HW = 256, 128, 3000, 40_000, 65536
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32) * 0.3).cuda()
+    vids = torch.from_numpy(rng.integers(0, V, (N, 3)))
+    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32))
+    hit = torch.from_numpy(np.sort(rng.choice(HW, N, replace=False))).cuda()
+    torch.manual_seed(0)
+    m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()
+    m.kernel_mode = "bf16"
+    w = {n: p.detach().cpu().numpy() for n, p in m.named_parameters()}
+    src = runtime.RaySource(E, vids.cuda(), bary.cuda(), None)
+    img = _render(m, src, hit, HW, chunk=4096, project=True).cpu().numpy()
+    img_g = _render(m, src, hit, HW, chunk=4096).cpu().numpy()
+    np.testing.assert_allclose(img, img_g, atol=5e-3)
+    hit_np = hit.cpu().numpy()
+    X = O.gather(E.cpu().numpy(), vids.numpy(), bary.numpy())
+    p_ref, _ = O.mlp_forward(w, X, L, s)
+    assert np.abs(img[hit_np] - p_ref).max() < 2e-2
