@@ -454,6 +454,12 @@ def render_bench(args, device):
             "bound": "mfma" if t_mfma >= t_hbm else "hbm", "mfma_frac": t_mfma / ms, "hbm_frac": t_hbm / ms,
             "frac": max(t_mfma, t_hbm) / ms, "achieved_tflops": flops / (ms * 1e-3) / 1e12,
             "achieved_gbs": byts / (ms * 1e-3) / 1e9}
+    # the same frame against the roofline of the reference's algorithm (gather k-wide rows,
+    # every layer per hit: SURVEY.md §8(d)'s 1.837 MFLOP and 6.2 KB per hit)
+    f_ref = nhit * 2 * (2 * k * Hd + (L - 2) * Hd * Hd + 3 * Hd)
+    b_ref = nhit * (3 * k_pad * 2 + per_hit_io) + H * W * 12 + wbytes
+    t_ref = max(f_ref / (PEAK[args.mode] * 1e12), b_ref / (HBM_PEAK * 1e9)) * 1e3
+    roof["reference_algorithm"] = {"flops": f_ref, "bytes": b_ref, "t_min_ms": t_ref, "frac": t_ref / ms}
     if project:  # measured HBM bytes (PMC) of the frame's two launches: projection GEMM + rproj
         tr_g, tr_p = _pmc_traffic(f"project_gemm_{args.mode}_render"), _pmc_traffic(f"rproj_{args.mode}_render")
         if tr_g is not None and tr_p is not None:
@@ -465,8 +471,34 @@ def render_bench(args, device):
         if tr is not None:  # measured HBM bytes of one launch (PMC), over the frame's launches
             roof["traffic_per_launch"] = tr
             roof["traffic"] = tr * len(offs)
+    variants = {}
+    if project:  # SURVEY.md §8(d)'s second distributions: pixel-coherent ids, a 100 % hit rate
+        def variant(n, coherent):
+            gv = torch.Generator(device="cpu").manual_seed(11)
+            if coherent:  # neighbouring pixels on nearby vertices, hits in pixel order
+                base = torch.randint(0, V - 64, (n // 64 + 1,), generator=gv).repeat_interleave(64)[:n]
+                vv = (base[:, None] + torch.randint(0, 64, (n, 3), generator=gv)).clamp_max(V - 1)
+                hv = torch.randperm(H * W, generator=gv)[:n].sort().values
+            else:
+                vv = torch.randint(0, V, (n, 3), generator=gv)
+                hv = torch.randperm(H * W, generator=gv)[:n]
+            uv = -torch.log(torch.rand((n, 3), generator=gv).clamp_min(1e-12))
+            sv = runtime.RaySource(src.E, vv.to(device), (uv / uv.sum(1, keepdim=True)).to(device), None,
+                                   validate=False)
+            sv._tables = src._tables  # the packed table is shared
+            bv = plan.make_batch(source=sv, offset=0, batch=n, projected=P)
+            hv = hv.to(device)
+
+            def fr():
+                img.fill_(1.0)
+                plan.project_table(T, out=P)
+                plan.render(bv, hv, None, img)
+            t = timed(fr)
+            return {"hits": n, "ms_per_frame": t, "pixels_per_s": H * W / (t * 1e-3)}
+        variants["coherent_ids_50pct"] = variant(nhit, True)
+        variants["random_ids_100pct"] = variant(H * W, False)
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
-            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams,
+            "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams, "variants": variants,
             "path": "projected table (inf_project_table per frame + rproj)" if project else "feature gather rchain",
             "projection_ms": ms_proj, "ms_per_frame_feature_gather": ms_gather,
             "feature_gather_pixels_per_s": H * W / (ms_gather * 1e-3), "roofline": roof}
