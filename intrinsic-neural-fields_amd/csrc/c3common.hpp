@@ -95,6 +95,20 @@ __device__ __forceinline__ float col_sum4(float v) {
   return x + y;
 }
 
+// ReLU as one v_max_f32 (fmaxf adds a canonicalising max per element; NaN -> 0 either way)
+__device__ __forceinline__ float relu1(float x) {
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// two floats -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32), a in the low half
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+
 // LDS hand-off barrier that does not drain the vector-memory queue (__syncthreads()
 // would add `s_waitcnt vmcnt(0)` and stall on the weight fragments in flight)
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }

@@ -471,11 +471,25 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       // (UPL = 4) span: xlane + 64 ak0 + ((kb 4 + g4) ^ r16) 16
       const int fx = from_x ? 1 : 0;
       const char* bbase = from_x ? xlane + ak0 * 64 : act_in;
-#pragma unroll
-      for (int kb = 0; kb < UPL; ++kb) {
+      auto bread = [&](int kb) -> bf16x8 {
         const int xo = ((kb * 4 + g4) ^ r16) << 4;
         const int ao = kb * 1024 + aoffs[kb & 3];
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bbase + ao + fx * (xo - ao));
+        return *reinterpret_cast<const bf16x8*>(bbase + ao + fx * (xo - ao));
+      };
+      // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
+      // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
+      // latency is exposed at every k-block, behind only TN MFMAs)
+      // (not in the chunked variant: its second accumulator set leaves no room -- it spills)
+      constexpr bool BPF = !XC;
+      bf16x8 bq[2];
+      if constexpr (BPF) bq[0] = bread(0);
+#pragma unroll
+      for (int kb = 0; kb < UPL; ++kb) {
+        if constexpr (BPF) {
+          if (kb + 1 < UPL) bq[(kb + 1) & 1] = bread(kb + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const bf16x8 bv = BPF ? bq[kb & 1] : bread(kb);
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[j], 0, 0, 0);
 #pragma unroll

@@ -276,6 +276,9 @@ __global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
 #pragma unroll
       for (int kb = 0; kb < UPL; ++kb) {
         if (kb + 1 < UPL) read_b(kb + 1, bq[(kb + 1) & 1]);
+        // issue them ahead of this k-block's MFMAs (the scheduler otherwise sinks the reads to
+        // just before their first use, one MFMA ahead, exposing the LDS latency every k-block)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll

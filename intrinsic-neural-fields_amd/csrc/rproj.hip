@@ -45,6 +45,11 @@ using namespace c3;
 #ifndef RP_BQ
 #define RP_BQ 2
 #endif
+// diagnostics (tools/rchain_timing.py; results wrong): RP_DIAG bit 0 = no fragment refills,
+// bit 1 = no LDS B-operand reads, bit 2 = no epilogue work
+#ifndef RP_DIAG
+#define RP_DIAG 0
+#endif
 // diagnostics (tools/rchain_timing.py): 1 = loader waves only take part in the barriers
 #ifndef RP_LOADER_IDLE
 #define RP_LOADER_IDLE 0
@@ -265,87 +270,108 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
 #pragma unroll
   for (int q = 0; q < 4; ++q) aoffs[q] = act_off(q, r16, g4) - q * 1024;
   auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
-  auto put_act = [&](const float (&v)[TN][4], char* dst) {
-    if constexpr (TN % 2 == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; j += 2) {
-        u16x8 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          o[r] = bf_bits3(v[j][r]);
-          o[4 + r] = bf_bits3(v[j + 1][r]);
-        }
-        *reinterpret_cast<u16x8*>(dst + act_off((t0 + j) >> 1, r16, g4)) = o;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        u16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = bf_bits3(v[j][r]);
-        const int t = t0 + j;
-        *reinterpret_cast<u16x4*>(dst + act_off(t >> 1, r16, g4) + 8 * (t & 1)) = o;
-      }
-    }
-  };
-
   f32x4 acc[RT][TN];
 
   // epilogue of layer l: bias (+ W_y x and Ly.bias at the skip layer) + ReLU into the next
   // activation tile, or the head partials at l = L - 2 (rchain.hip's)
-  auto epilogue = [&](int l) {
+  // layer l's bias (+ Ly.bias and the tile's W_y x at the skip layer) as the start value of
+  // the accumulators, so the epilogue is ReLU + bf16 packing only
+  auto init_acc = [&](int l) {
     const bool skip = l == a.s;
-    const bool head = l == L - 2;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      f32x4 bb = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+      if (skip) bb += *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        acc[t][j] = bb;
+        if (skip) {
+          const u16x4 zy = *reinterpret_cast<const u16x4*>(zs + tile_off(C::ZROW, t * 16 + r16, H + feat(j)));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[t][j][r] += bf_val3(zy[r]);
+        }
+      }
+    }
+  };
+
+  // epilogue of layer l < L - 2: ReLU -> bf16 -> the next layer's activation tile
+  auto epilogue_act = [&](int l) {
     char* act_out = act + ((l + 1) & 1) * C::ACT_BYTES;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      char* dst = act_out + t * C::ACT_T;
+      if constexpr (TN % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; j += 2) {
+          u32x4 w;
+          w[0] = pack_bf16x2(relu1(acc[t][j][0]), relu1(acc[t][j][1]));
+          w[1] = pack_bf16x2(relu1(acc[t][j][2]), relu1(acc[t][j][3]));
+          w[2] = pack_bf16x2(relu1(acc[t][j + 1][0]), relu1(acc[t][j + 1][1]));
+          w[3] = pack_bf16x2(relu1(acc[t][j + 1][2]), relu1(acc[t][j + 1][3]));
+          *reinterpret_cast<u32x4*>(dst + act_off((t0 + j) >> 1, r16, g4)) = w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          u32x2 w;
+          w[0] = pack_bf16x2(relu1(acc[t][j][0]), relu1(acc[t][j][1]));
+          w[1] = pack_bf16x2(relu1(acc[t][j][2]), relu1(acc[t][j][3]));
+          const int tt = t0 + j;
+          *reinterpret_cast<u32x2*>(dst + act_off(tt >> 1, r16, g4) + 8 * (tt & 1)) = w;
+        }
+      }
+    }
+    lbar();  // the next layer's tile complete; after the skip layer, Z's W_y half is free
+  };
+
+  // epilogue of layer L - 2: ReLU, bf16 rounding and the head's partial dot products
+  // (model.py:89-94) over this lane's features, summed over the row groups
+  auto epilogue_head = [&]() {
     float zp[RT][3];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       float hq[TN][4];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
-        f32x4 yb = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (skip) yb = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
-        u16x4 zy = u16x4{0, 0, 0, 0};
-        if (skip) zy = *reinterpret_cast<const u16x4*>(zs + tile_off(C::ZROW, t * 16 + r16, H + feat(j)));
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[t][j][r];
-          if (skip) v += bf_val3(zy[r]);
-          v += bb[r];
-          if (skip) v += yb[r];
-          hq[j][r] = bf_val3(bf_bits3(fmaxf(v, 0.f)));
+        for (int r = 0; r < 4; r += 2) {
+          const unsigned w = pack_bf16x2(relu1(acc[t][j][r]), relu1(acc[t][j][r + 1]));
+          hq[j][r] = __builtin_bit_cast(float, w << 16);
+          hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
         }
-      }
-      if (!head) {
-        put_act(hq, act_out + t * C::ACT_T);
-      } else {
 #pragma unroll
-        for (int o = 0; o < 3; ++o) {
-          float z = 0.f;
+      for (int o = 0; o < 3; ++o) {
+        float z = 0.f;
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
+        for (int j = 0; j < TN; ++j) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
 #pragma unroll
-            for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
-          }
-          zp[t][o] = col_sum4(z);
+          for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
         }
+        zp[t][o] = col_sum4(z);
       }
     }
-    if (head) {
-      if (g4 == 0)
+    if (g4 == 0)
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-          for (int o = 0; o < 3; ++o) zps[(wc * BM + t * 16 + r16) * 3 + o] = zp[t][o];
+        for (int o = 0; o < 3; ++o) zps[(wc * BM + t * 16 + r16) * 3 + o] = zp[t][o];
+    lbar();  // the head partials complete (and Z's W_y half free when s = L - 2)
+  };
+  auto epilogue = [&](int l) {
+    if constexpr ((RP_DIAG & 4) != 0) {  // diagnostics (4): a minimal epilogue (keeps the MFMAs live)
+      float sm = 0.f;
+#pragma unroll
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sm += acc[t][j][0] + acc[t][j][1] + acc[t][j][2] + acc[t][j][3];
+      if (sm == 1234.5f) zps[tid] = sm;
+      lbar();
+      return;
     }
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    lbar();  // the next layer's tile (or the head partials) complete; after the skip
-             // layer, Z's W_y half is free
+    if (l == L - 2) epilogue_head();
+    else epilogue_act(l);
   };
 
   // one hidden layer: UPL k-blocks of the activation tile (rchain.hip's run_block)
@@ -357,8 +383,13 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
     const char* act_in = act + (B.phase & 1) * C::ACT_BYTES;
     auto read_b = [&](int kb, bf16x8 (&bv)[RT]) {
 #pragma unroll
-      for (int t = 0; t < RT; ++t)
-        bv[t] = *reinterpret_cast<const bf16x8*>(act_in + t * C::ACT_T + kb * 1024 + aoffs[kb & 3]);
+      for (int t = 0; t < RT; ++t) {
+        if constexpr ((RP_DIAG & 2) != 0) {  // diagnostics: no LDS operand reads
+          bv[t] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)kb, (unsigned)t, 0u, 0u});
+        } else {
+          bv[t] = *reinterpret_cast<const bf16x8*>(act_in + t * C::ACT_T + kb * 1024 + aoffs[kb & 3]);
+        }
+      }
     };
     constexpr int NB = RP_BQ;  // B-operand buffers: 2 = next k-block's read ahead of the MFMAs
     bf16x8 bq[NB][RT];
@@ -367,14 +398,19 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
     for (int kb = 0; kb < UPL; ++kb) {
       if (NB == 2 && kb + 1 < UPL) read_b(kb + 1, bq[(kb + 1) % NB]);
       if (NB == 1 && kb > 0) read_b(kb, bq[0]);
+      // issue them ahead of this k-block's MFMAs (the scheduler otherwise sinks the reads to
+      // just before their first use, one MFMA ahead, exposing the LDS latency every k-block)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int t = 0; t < RT; ++t)
           acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bq[kb % NB][t], acc[t][j], 0, 0, 0);
+      if constexpr ((RP_DIAG & 1) == 0) {  // diagnostics (1): no fragment refills
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        fr[kb % D][j] = kb + D < UPL ? frag(crs, kb + D, j) : frag(nrs, kb + D - UPL, j);
+        for (int j = 0; j < TN; ++j)
+          fr[kb % D][j] = kb + D < UPL ? frag(crs, kb + D, j) : frag(nrs, kb + D - UPL, j);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -386,13 +422,13 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
     // this tile's layer-0 pre-activations out of Z (tile_off's swizzle), then Z's W_0
     // half is free (the W_y half is read by the skip layer's epilogue)
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const int row = t * 16 + r16;
+    for (int j = 0; j < TN; ++j) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(vecs + feat(j));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const u16x4 p = *reinterpret_cast<const u16x4*>(zs + tile_off(C::ZROW, row, feat(j)));
+      for (int t = 0; t < RT; ++t) {
+        const u16x4 p = *reinterpret_cast<const u16x4*>(zs + tile_off(C::ZROW, t * 16 + r16, feat(j)));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[t][j][r] = bf_val3(p[r]);
+        for (int r = 0; r < 4; ++r) acc[t][j][r] = bf_val3(p[r]) + b0[r];
       }
     }
     lbar();  // every wave holds its pre-activations
@@ -401,6 +437,7 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
 #pragma unroll 1
     for (int hb = 0; hb < nh; ++hb) {
       if (tile - tb < 2) stamp(sbase + 1 + hb);
+      init_acc(hb + 1);
       run_block(hb);
       epilogue(hb + 1);
     }
