@@ -393,26 +393,27 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
     // activations / dZ -> the LDS tile: one 16-byte write per k block (tile pair), 8 bytes
     // for a lone tile (H = 128: a wave owns half a k block)
+    // (pairs of values through one v_cvt_pk_bf16_f32: the same RNE bits as one at a time)
     auto put_act = [&](const float (&v)[TN][4], char* act) {
       if constexpr (TN % 2 == 0) {
 #pragma unroll
         for (int j = 0; j < TN; j += 2) {
-          u16x8 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            o[r] = bf_bits3(v[j][r]);
-            o[4 + r] = bf_bits3(v[j + 1][r]);
-          }
-          *reinterpret_cast<u16x8*>(act + act_off((t0 + j) >> 1, r16, g4)) = o;
+          u32x4 w;
+          w[0] = pack_bf16x2(v[j][0], v[j][1]);
+          w[1] = pack_bf16x2(v[j][2], v[j][3]);
+          w[2] = pack_bf16x2(v[j + 1][0], v[j + 1][1]);
+          w[3] = pack_bf16x2(v[j + 1][2], v[j + 1][3]);
+          *reinterpret_cast<u32x4*>(act + act_off((t0 + j) >> 1, r16, g4)) = w;
         }
       } else {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          u16x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = bf_bits3(v[j][r]);
+          u32x2 w;
+          w[0] = pack_bf16x2(v[j][0], v[j][1]);
+          w[1] = pack_bf16x2(v[j][2], v[j][3]);
           const int t = t0 + j;
-          *reinterpret_cast<u16x4*>(act + act_off(t >> 1, r16, g4) + 8 * (t & 1)) = o;
+          *reinterpret_cast<u32x2*>(act + act_off(t >> 1, r16, g4) + 8 * (t & 1)) = w;
         }
       }
     };
@@ -431,7 +432,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 
     f32x4 acc[TN], accy[TN];  // accy: W_y x of the chunked schedule (XC)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = accy[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < TN; ++j) accy[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
     for (int i = 0; i < a.nblk; ++i) {
@@ -522,24 +525,37 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         const int l = p;
         const bool skip = l == a.s;
         const bool last = l == L - 2;
-        float hq[TN][4];  // bf16-rounded activations as f32
-        unsigned bits = 0;
+        // + bias (+ the chunked schedule's W_y x and Ly.bias at the skip layer), in the
+        // layered GEMM epilogue's order (the bias last: the fp32 sums match it)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
-          f32x4 yv = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (skip) yv = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
+          if (skip) {
+            const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[j][r];
-            if (XC && skip) v += accy[j][r];
-            v += bv[r];
-            if (skip) v += yv[r];
-            v = fmaxf(v, 0.f);
-            hq[j][r] = bf_val3(bf_bits3(v));
-            bits |= (hq[j][r] > 0.f ? 1u : 0u) << (j * 4 + r);
+            for (int r = 0; r < 4; ++r) {
+              float v = acc[j][r];
+              if constexpr (XC) v += accy[j][r];
+              acc[j][r] = (v + bv[r]) + yv[r];
+            }
+          } else {
+            acc[j] += bv;
           }
         }
+        float hq[TN][4];  // bf16-rounded activations as f32
+        unsigned bits = 0;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const unsigned w = pack_bf16x2(relu1(acc[j][r]), relu1(acc[j][r + 1]));
+            hq[j][r] = __builtin_bit_cast(float, w << 16);
+            hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
+            // h > 0 <=> the bf16 bits without the sign are nonzero (ReLU left no negatives
+            // but possibly a -0)
+            bits |= ((w & 0x7FFFu) != 0u ? 1u : 0u) << (j * 4 + r);
+            bits |= ((w & 0x7FFF0000u) != 0u ? 1u : 0u) << (j * 4 + r + 1);
+          }
         if (!last) {
           if (l < MPW) mbits[0] |= (unsigned long long)bits << (NV * l);
           else mbits[1] |= (unsigned long long)bits << (NV * (l - MPW));

@@ -200,35 +200,23 @@ __global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) aoffs[q] = act_off(q, r16, g4) - q * 1024;
   auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
-  auto put_act = [&](const float (&v)[TN][4], char* dst) {
-    if constexpr (TN % 2 == 0) {
+  f32x4 acc[RT][TN], accy[RT][TN];
+  // start value of layer l's accumulators: its bias (+ Ly.bias at the skip layer), so the
+  // epilogue is ReLU + packing (accy, W_y x of the input phase, starts at zero)
+  auto init_acc = [&](int l) {
 #pragma unroll
-      for (int j = 0; j < TN; j += 2) {
-        u16x8 o;
+    for (int j = 0; j < TN; ++j) {
+      f32x4 bb = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+      if (l == a.s) bb += *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          o[r] = bf_bits3(v[j][r]);
-          o[4 + r] = bf_bits3(v[j + 1][r]);
-        }
-        *reinterpret_cast<u16x8*>(dst + act_off((t0 + j) >> 1, r16, g4)) = o;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        u16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = bf_bits3(v[j][r]);
-        const int t = t0 + j;
-        *reinterpret_cast<u16x4*>(dst + act_off(t >> 1, r16, g4) + 8 * (t & 1)) = o;
-      }
+      for (int t = 0; t < RT; ++t) acc[t][j] = bb;
     }
   };
-
-  f32x4 acc[RT][TN], accy[RT][TN];
+  init_acc(0);
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[t][j] = accy[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) accy[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 
 #pragma unroll 1
@@ -294,33 +282,56 @@ __global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
     else run_block(std::false_type{});
     if (!B.last) continue;
 
-    // ---- epilogue of layer l = phase: bias (+ W_y x and Ly.bias at the skip layer) + ReLU
+    // ---- epilogue of layer l = phase (its accumulators started from the biases; W_y x
+    // joins at the skip layer): ReLU -> bf16 -> the next activation tile, or the head
     const int l = B.phase;
-    const bool skip = l == a.s;
-    const bool head = l == L - 2;
-    char* act_out = act + ((l + 1) & 1) * C::ACT_BYTES;
-    float zp[RT][3];
+    if (l == a.s)
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      float hq[TN][4];
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
-        f32x4 yb = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (skip) yb = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
+        for (int j = 0; j < TN; ++j) acc[t][j] += accy[t][j];
+    if (l < L - 2) {
+      char* act_out = act + ((l + 1) & 1) * C::ACT_BYTES;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[t][j][r];
-          if (skip) v += accy[t][j][r];
-          v += bb[r];
-          if (skip) v += yb[r];
-          hq[j][r] = bf_val3(bf_bits3(fmaxf(v, 0.f)));
+      for (int t = 0; t < RT; ++t) {
+        char* dst = act_out + t * C::ACT_T;
+        if constexpr (TN % 2 == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; j += 2) {
+            u32x4 w;
+            w[0] = pack_bf16x2(relu1(acc[t][j][0]), relu1(acc[t][j][1]));
+            w[1] = pack_bf16x2(relu1(acc[t][j][2]), relu1(acc[t][j][3]));
+            w[2] = pack_bf16x2(relu1(acc[t][j + 1][0]), relu1(acc[t][j + 1][1]));
+            w[3] = pack_bf16x2(relu1(acc[t][j + 1][2]), relu1(acc[t][j + 1][3]));
+            *reinterpret_cast<u32x4*>(dst + act_off((t0 + j) >> 1, r16, g4)) = w;
+          }
+        } else {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            u32x2 w;
+            w[0] = pack_bf16x2(relu1(acc[t][j][0]), relu1(acc[t][j][1]));
+            w[1] = pack_bf16x2(relu1(acc[t][j][2]), relu1(acc[t][j][3]));
+            const int tt = t0 + j;
+            *reinterpret_cast<u32x2*>(dst + act_off(tt >> 1, r16, g4) + 8 * (tt & 1)) = w;
+          }
         }
       }
-      if (!head) {
-        put_act(hq, act_out + t * C::ACT_T);
-      } else {
-        // head partials over this lane's features (model.py:89-94), then the row groups
+      init_acc(l + 1);
+    } else {
+      // head partials over this lane's features (model.py:89-94), then the row groups
+      float zp[RT][3];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        float hq[TN][4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const unsigned w = pack_bf16x2(relu1(acc[t][j][r]), relu1(acc[t][j][r + 1]));
+            hq[j][r] = __builtin_bit_cast(float, w << 16);
+            hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
+          }
 #pragma unroll
         for (int o = 0; o < 3; ++o) {
           float z = 0.f;
@@ -333,18 +344,12 @@ __global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
           zp[t][o] = col_sum4(z);
         }
       }
-    }
-    if (head) {
       if (g4 == 0)
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
           for (int o = 0; o < 3; ++o) zps[(wc * BM + t * 16 + r16) * 3 + o] = zp[t][o];
     }
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     lbar();  // the next layer's tile (or the head partials) complete
   }
 
