@@ -50,7 +50,9 @@ using namespace c3;
 #ifndef RP_DIAG
 #define RP_DIAG 0
 #endif
-// diagnostics (tools/rchain_timing.py): 1 = loader waves only take part in the barriers
+// diagnostics (tools/rchain_timing.py): 1 = loader waves only take part in the barriers,
+// 2 = they load the rows but neither interpolate nor store, 3 = interpolate and store
+// constants without loading
 #ifndef RP_LOADER_IDLE
 #define RP_LOADER_IDLE 0
 #endif
@@ -227,6 +229,13 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
     const int x = tid - CW * 64;
     const int lc = x % HC, lr = x / HC;
     auto load_group = [&](int h, int g, u16x8 (&ev)[G][3]) {
+      if constexpr (RP_LOADER_IDLE == 3) {  // diagnostics: interpolation + stores of constants, no loads
+#pragma unroll
+        for (int m = 0; m < G; ++m)
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ev[m][i] = u16x8{(unsigned short)(x + m), 1, 2, 3, 4, 5, 6, (unsigned short)i};
+        return;
+      }
 #pragma unroll
       for (int m = 0; m < G; ++m) rows_load(h, lr + RPI * (g * G + m), lc, ev[m]);
     };
@@ -237,6 +246,10 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
       for (int m = 0; m < G; ++m)
 #pragma unroll
         for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(ev[m][i]));
+      if constexpr (RP_LOADER_IDLE == 2) {  // diagnostics: the loads, no interpolation / stores
+        if (ev[0][0][0] == 0x1234 && ev[G - 1][2][7] == 0x4321) zs[x] = 1;
+        return;
+      }
 #pragma unroll
       for (int m = 0; m < G; ++m) rows_store(h, lr + RPI * (g * G + m), lc, ev[m]);
     };
@@ -247,7 +260,7 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
       u16x8 ev[G][3];
 #pragma unroll 1
       for (int j = 0; j < nbar; ++j) {
-        if (has_next && !RP_LOADER_IDLE) {
+        if (has_next && RP_LOADER_IDLE != 1) {
           if (j == 0) rec = rec_load(tile + 1, x);
           if (j == 1) rec_store(rec, x);
           // stores first: the group registers are reloaded in the same interval

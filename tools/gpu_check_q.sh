@@ -1,6 +1,6 @@
 set -o pipefail
-for l in "" g3 g4 g7; do
+for l in "" l1 l2 l3; do
   if [ -n "$l" ]; then export INF_LIB=$PWD/intrinsic-neural-fields_amd/inf_hip/libinf_hip_$l.so; else unset INF_LIB; fi
   echo "== lib ${l:-default}"
-  PROJ=1 timeout -k 10 100 python tools/rchain_timing.py 2>&1 | grep -v amdgpu.ids | tail -4 | head -3 || exit 1
+  PROJ=1 timeout -k 10 100 python tools/rchain_timing.py 2>&1 | grep -v amdgpu.ids | sed -n '2p;4p' || exit 1
 done
