@@ -1,0 +1,10 @@
+#!/bin/bash
+# Times diagnostic builds of the render chain side by side (run on the GPU box via gpurun):
+#   make -C intrinsic-neural-fields_amd/csrc BUILD=build_d_X OUT=../inf_hip/libinf_hip_X.so EXTRA="-D..."
+#   bash tools/gpu_variants.sh X Y ...      (the default library first)
+set -o pipefail
+for l in "" "$@"; do
+  if [ -n "$l" ]; then export INF_LIB=$PWD/intrinsic-neural-fields_amd/inf_hip/libinf_hip_$l.so; else unset INF_LIB; fi
+  echo "== lib ${l:-default}"
+  PROJ=1 timeout -k 10 100 python tools/rchain_timing.py 2>&1 | grep -v amdgpu.ids | sed -n '2p;4p' || exit 1
+done
