@@ -27,11 +27,15 @@ struct LtPlan {
 
 constexpr size_t WS_MAX = (size_t)256 << 20;  // workspace offered to the heuristic
 
+// per device (a process may drive more than one): handle, tuned plans, workspace
+struct DevState {
+  hipblasLtHandle_t handle = nullptr;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, LtPlan> plans;
+};
 std::mutex g_mu;
-hipblasLtHandle_t g_handle = nullptr;
-void* g_ws = nullptr;
-size_t g_ws_bytes = 0;
-std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, LtPlan> g_plans;
+std::map<int, DevState> g_dev;
 
 #define LT_TRY(x)                                                     \
   do {                                                                \
@@ -49,10 +53,24 @@ std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, LtPla
 int blaslt_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
                         int64_t N, int64_t K, hipStream_t stream) {
   std::lock_guard<std::mutex> lock(g_mu);
+  int dev = 0;
+  INF_HIP_TRY(hipGetDevice(&dev));
+  DevState& ds = g_dev[dev];
+  hipblasLtHandle_t& g_handle = ds.handle;
   if (g_handle == nullptr) LT_TRY(hipblasLtCreate(&g_handle));
+  // the workspace is kept for the process (plans may be replayed from graphs)
+  auto ensure_ws = [&](size_t need) -> int {
+    if (need <= ds.ws_bytes) return INF_OK;
+    if (ds.ws != nullptr) INF_HIP_TRY(hipFree(ds.ws));
+    ds.ws = nullptr;
+    ds.ws_bytes = 0;
+    INF_HIP_TRY(hipMalloc(&ds.ws, need));
+    ds.ws_bytes = need;
+    return INF_OK;
+  };
   const auto key = std::make_tuple(M, N, K, lda, ldb, ldc);
-  auto it = g_plans.find(key);
-  if (it == g_plans.end()) {
+  auto it = ds.plans.find(key);
+  if (it == ds.plans.end()) {
     LtPlan p;
     LT_TRY(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
     const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
@@ -85,13 +103,7 @@ int blaslt_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
       for (int i = 0; i < n; ++i)
         if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= WS_MAX)
           need = std::max(need, (size_t)res[i].workspaceSize);
-      if (need > g_ws_bytes) {
-        if (g_ws != nullptr) INF_HIP_TRY(hipFree(g_ws));
-        g_ws = nullptr;
-        g_ws_bytes = 0;
-        INF_HIP_TRY(hipMalloc(&g_ws, need));
-        g_ws_bytes = need;
-      }
+      if (int rc = ensure_ws(need)) return rc;
       hipEvent_t e0, e1;
       INF_HIP_TRY(hipEventCreate(&e0));
       INF_HIP_TRY(hipEventCreate(&e1));
@@ -104,7 +116,7 @@ int blaslt_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
         for (int rep = 0; rep < 2 && ok; ++rep) {  // rep 0 warms up
           INF_HIP_TRY(hipEventRecord(e0, stream));
           ok = hipblasLtMatmul(g_handle, p.desc, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &res[i].algo,
-                               g_ws, res[i].workspaceSize, stream) == HIPBLAS_STATUS_SUCCESS;
+                               ds.ws, res[i].workspaceSize, stream) == HIPBLAS_STATUS_SUCCESS;
           INF_HIP_TRY(hipEventRecord(e1, stream));
           INF_HIP_TRY(hipEventSynchronize(e1));
           INF_HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
@@ -128,20 +140,13 @@ int blaslt_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
       for (int i = 0; i < n; ++i)
         std::fprintf(stderr, "hipBLASLt candidate %d: workspace %zu bytes%s\n", i, (size_t)res[i].workspaceSize,
                      i == pick ? " (picked)" : "");
-    if (p.ws > g_ws_bytes) {
-      // the workspace is kept for the process (plans may be replayed from graphs)
-      if (g_ws != nullptr) INF_HIP_TRY(hipFree(g_ws));
-      g_ws = nullptr;
-      g_ws_bytes = 0;
-      INF_HIP_TRY(hipMalloc(&g_ws, p.ws));
-      g_ws_bytes = p.ws;
-    }
-    it = g_plans.emplace(key, p).first;
+    if (int rc = ensure_ws(p.ws)) return rc;
+    it = ds.plans.emplace(key, p).first;
   }
   const LtPlan& p = it->second;
   const float alpha = 1.f, beta = 0.f;
   LT_TRY(hipblasLtMatmul(g_handle, p.desc, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &p.algo,
-                         p.ws > 0 ? g_ws : nullptr, p.ws, stream));
+                         p.ws > 0 ? ds.ws : nullptr, p.ws, stream));
   return INF_OK;
 }
 
