@@ -25,6 +25,7 @@ Fixtures:
                                                                           model.py:33-40,98-104
   g10_rff_curve.npz                  12-epoch synthetic run, rff strategy  trainer.py:164-187,232-283 + the above
   g11_viewdep_{intrinsic,extrinsic}.npz  view-dependent field fwd + 1 step model.py:115-191,240-256
+  g12_train_curve_B.npz              G8's run on config B's MLP (k=1024, 8x256, skip 4)
 
 Run:  python tests/golden/make_golden.py
 """
@@ -492,9 +493,56 @@ def g11_viewdep():
              **state_dict_arrays(model, "w1:"))
 
 
+def g12_train_curve_B():
+    """G8's synthetic texture-reconstruction run on the bench's exact MLP (config B: k =
+    1024, 8 x 256, skip 4), L1, lr 2e-4: the reference's own fp32 val-PSNR curve that the
+    bf16 fused step (the benchmarked mode) is held to."""
+    rng = np.random.default_rng(13)
+    name = "B"
+    V, k = 1000, in_dim(name)
+    E = rescaled_table(rng, V, k)
+    proj = rng.standard_normal((16, 3)).astype(np.float32) * 2.0
+    vert_rgb = 1.0 / (1.0 + np.exp(-(E[:, :16] * 4.0) @ proj))
+    def rays(n):
+        vids, bary = synthetic_rays(rng, V, n, include_edges=False)
+        rgb = np.einsum("ni,nic->nc", bary, vert_rgb[vids]).astype(np.float32)
+        return vids, bary, rgb
+    tr_v, tr_b, tr_rgb = rays(16384)
+    va_v, va_b, va_rgb = rays(2048)
+    batch, lr = 1024, 2e-4  # a smooth curve: at 1e-3 this MLP's run is chaotic (non-monotonic)
+    cfg = {"model": model_cfg(name), "training": {"lr": lr, "loss_type": "L1"}}
+    torch.manual_seed(0)
+    model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+    loss_fn = ref_config.get_loss_fn(cfg)
+    tr = _bare_trainer(model, optim, loss_fn)
+    Et = torch.from_numpy(E)
+    train_ld = ref_loader.RayDataLoader(Et, "efuncs", torch.from_numpy(tr_v), torch.from_numpy(tr_b),
+                                        torch.from_numpy(tr_rgb), None, None, batch, False, True, device="cpu")
+    val_ld = ref_loader.RayDataLoader(Et, "efuncs", torch.from_numpy(va_v), torch.from_numpy(va_b),
+                                      torch.from_numpy(va_rgb), None, None, batch, False, False, device="cpu")
+    tr.val_data_loader = val_ld
+    val_psnr, train_psnr = [], []
+    for epoch in range(12):
+        acc_l2, total = 0.0, 0
+        for b in train_ld:  # shuffle=False: deterministic batch order
+            loss, pred = tr._train_step(b)
+            acc_l2 += torch.nn.functional.mse_loss(pred, b["expected_rgbs"], reduction="sum").item()
+            total += b["expected_rgbs"].shape[0]
+        train_psnr.append(ref_metrics.epoch_psnr(acc_l2 / total))
+        _, vp = tr.evaluate(epoch)
+        val_psnr.append(vp)
+    save("g12_train_curve_B.npz", E=E, tr_vids=tr_v, tr_bary=tr_b, tr_rgb=tr_rgb, va_vids=va_v, va_bary=va_b,
+         va_rgb=va_rgb, val_psnr=np.array(val_psnr), train_psnr=np.array(train_psnr), lr=np.float32(lr),
+         batch=np.int64(batch))
+
+
 if __name__ == "__main__":
     import tempfile
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:  # e.g. `make_golden.py g12_train_curve_B`: only those fixtures
+        for fn in sys.argv[1:]:
+            globals()[fn]()
+        sys.exit(0)
     with tempfile.TemporaryDirectory() as td:
         g1_gather()
         g1_load_efuncs(td)
@@ -508,3 +556,4 @@ if __name__ == "__main__":
         g9_frontends()
         g10_rff_curve()
         g11_viewdep()
+        g12_train_curve_B()

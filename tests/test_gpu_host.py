@@ -217,6 +217,48 @@ def test_trainer_g8_training_curve(tmp_path, mode, tol):
     assert os.path.exists(os.path.join(tmp_path, "model_last_epoch.pt"))
 
 
+def test_trainer_g12_curve_config_b(tmp_path):
+    """Statistical PSNR parity on the bench's exact MLP (config B: k = 1024, 8 x 256, skip
+    4): 12 epochs of the reference's synthetic run (G12, generated by importing the
+    reference) through trainer.Trainer in fp32 (parity mode) and bf16 (the benchmarked
+    fused step)."""
+    import config
+    from ray_dataloader import RayDataLoader
+    from trainer import Trainer
+    d = golden("g12_train_curve_B.npz")
+    curves = {}
+    for mode in ("fp32", "bf16"):
+        out = tmp_path / mode
+        cfg = {"seed": 0, "data": {"img_height": 8, "img_width": 8},
+               "model": {"k": 1024, "num_layers": 8, "mlp_hidden_dim": 256, "skip_layer_idx": 4,
+                         "kernels": {"mode": mode}},
+               "training": {"out_dir": str(out), "batch_size": int(d["batch"]), "lr": float(d["lr"]),
+                            "loss_type": "L1", "render_every": 1000, "print_every": 1000, "epochs": 12,
+                            "checkpoint_every": 1000}}
+        E = torch.from_numpy(d["E"])
+        train = RayDataLoader(E, "efuncs", torch.from_numpy(d["tr_vids"]), torch.from_numpy(d["tr_bary"]),
+                              torch.from_numpy(d["tr_rgb"]), None, None, int(d["batch"]), False, True, device="cuda")
+        val = RayDataLoader(E, "efuncs", torch.from_numpy(d["va_vids"]), torch.from_numpy(d["va_bary"]),
+                            torch.from_numpy(d["va_rgb"]), None, None, int(d["batch"]), False, False, device="cuda")
+        torch.manual_seed(0)
+        model, optim = config.get_model_and_optim(cfg, None, "cuda")
+        model.kernel_mode = mode
+        Trainer(model, optim, config.get_loss_fn(cfg), None, {"train": train, "val": val}, None, cfg, "cuda").train()
+        curves[mode] = np.array(_val_curve(out))
+    ref = d["val_psnr"]
+    print({m: np.round(c - ref, 3).tolist() for m, c in curves.items()})
+    # The first five epochs follow the reference's trajectory (fp32 0.005 dB, bf16 0.02 dB
+    # seen); later the two trajectories drift apart the same way in both modes (fp32 too:
+    # summation-order differences grow through training, ±0.33 dB seen at epochs 5-11),
+    # so the rest is held statistically: every epoch within 0.5 dB, the mean of the last
+    # four within 0.2 dB (0.08 seen in both modes).
+    for mode, early in (("fp32", 0.02), ("bf16", 0.2)):
+        c = curves[mode]
+        np.testing.assert_allclose(c[:5], ref[:5], atol=early, err_msg=mode)
+        np.testing.assert_allclose(c, ref, atol=0.5, err_msg=mode)
+        assert abs(float(np.mean(c[-4:] - ref[-4:]))) < 0.2, mode
+
+
 def test_trainer_checkpoint_resume(tmp_path):
     tr, d = _g8_trainer(tmp_path, "fp32", epochs=7)
     tr.train()
