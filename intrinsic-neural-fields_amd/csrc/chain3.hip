@@ -627,10 +627,14 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           float dzr[3];
 #pragma unroll
           for (int o = 0; o < 3; ++o) dzr[o] = dzs[wc * BM * 3 + r16 * 3 + o];
-          if (tid < 3) {
-            float db = 0.f;
-            for (int r = 0; r < BM; ++r) db += dzs[r * 3 + tid];
-            hbs[tid] = db;
+          // the output bias partials (sum over the 16 rays of dz_o): a DPP row sum in wave 0
+          // (lane r16 holds ray r16's dz) instead of a 16-deep dependent LDS loop
+          if (wc == 0) {
+#pragma unroll
+            for (int o = 0; o < 3; ++o) {
+              const float db = row_sum16(dzr[o]);
+              if (lane == 0) hbs[o] = db;
+            }
           }
           float gv[TN][4];
 #pragma unroll
