@@ -23,52 +23,64 @@ import numpy as np
 import torch
 
 
+def _first_k(values, k, axis):
+    """Columns (axis 1) or entries (axis 0) `k` of a stored spectrum: an explicit index list,
+    or the first k (which must be stored)."""
+    if isinstance(k, list):
+        return np.take(values, np.array(k), axis=axis)
+    assert k <= values.shape[axis]
+    return values[:, :k] if axis == 1 else values[:k]
+
+
+def _spectrum(eigenvalues_path, k):
+    """The eigenvalues matching the selected eigenfunctions, the first one's sign fixed (a
+    tiny negative lambda_0 is solver noise); all must then be positive."""
+    lam = np.load(eigenvalues_path)
+    lam = _first_k(lam, k, axis=1 if isinstance(k, list) and lam.ndim > 1 else 0)
+    if lam[0] < 0 and np.abs(lam[0]) < 1e-10:
+        lam[0] *= -1
+    assert np.all(lam > 0), f"Min value: {lam.min()}"
+    return lam
+
+
+def _heat_kernel_signature(phi, lam, ts):
+    # sum_i phi_i(v)^2 exp(-lambda_i t) at ts log-spaced t in [1e-2, 1]
+    t = np.logspace(-2, 0, num=ts)
+    return (phi * phi) @ np.exp(-lam[..., None] @ t[None, ...])
+
+
+def _column_range(phi):
+    return np.max(phi, axis=0, keepdims=True) - np.min(phi, axis=0, keepdims=True)
+
+
+_RESCALE = {
+    "standard": lambda phi: phi / _column_range(phi),  # each column into a unit-width range
+    "one-norm": lambda phi: phi / np.linalg.norm(phi, ord=2, axis=-1, keepdims=True),  # unit rows
+    "unscaled": lambda phi: phi,
+}
+
+
 def load_first_k_eigenfunctions(eigenfunctions_path, k, rescale_strategy="standard", embed_strategy=None,
                                 eigenvalues_path=None, ts=128):
-    """Reference mesh.py:53-108: column select, optional GPS/HKS embedding, rescale."""
-    all_eigenfunctions = np.load(eigenfunctions_path)
-    if isinstance(k, list):
-        eigenfunctions = all_eigenfunctions[:, np.array(k)]
-    else:
-        stored_k = all_eigenfunctions.shape[1]
-        assert k <= stored_k
-        eigenfunctions = all_eigenfunctions[:, :k]
-
-    eigenvalues = None
-    if eigenvalues_path is not None:
-        all_eigenvalues = np.load(eigenvalues_path)
-        if isinstance(k, list):
-            eigenvalues = all_eigenvalues[np.array(k)] if all_eigenvalues.ndim == 1 else \
-                all_eigenvalues[:, np.array(k)]
-        else:
-            assert k <= all_eigenvalues.shape[0]
-            eigenvalues = all_eigenvalues[:k]
-        if np.abs(eigenvalues[0]) < 1e-10 and eigenvalues[0] < 0:
-            eigenvalues[0] *= -1
-        assert np.all(eigenvalues > 0), f"Min value: {eigenvalues.min()}"
-
-    if embed_strategy is not None:
-        if embed_strategy == "gps":
-            assert eigenvalues is not None
-            weights = np.sqrt(eigenvalues)
-            weights /= weights[0]
-            return eigenfunctions / weights
-        elif embed_strategy == "hks":
-            assert eigenvalues is not None
-            timesteps = np.logspace(-2, 0, num=ts)
-            eigenfunctions = (eigenfunctions * eigenfunctions) @ np.exp(-eigenvalues[..., None] @ timesteps[None, ...])
-        else:
-            raise ValueError(f"Unknown embedding strategy {embed_strategy}")
-
-    if rescale_strategy == "standard":
-        eigenfunctions = eigenfunctions / (np.max(eigenfunctions, axis=0, keepdims=True) -
-                                           np.min(eigenfunctions, axis=0, keepdims=True))
-    elif rescale_strategy == "one-norm":
-        eigenfunctions = eigenfunctions / np.linalg.norm(eigenfunctions, ord=2, axis=-1, keepdims=True)
-    elif rescale_strategy != "unscaled":
+    """The per-vertex input table (reference mesh.py:53-108): eigenfunction columns `k`, an
+    optional spectral embedding -- "gps" (phi_i / sqrt(lambda_i / lambda_0), returned as is,
+    a numpy array, like the reference) or "hks" (heat kernel signature) -- then a rescale.
+    Same float64 expressions as the reference, so the table is bitwise the same."""
+    phi = _first_k(np.load(eigenfunctions_path), k, axis=1)
+    lam = _spectrum(eigenvalues_path, k) if eigenvalues_path is not None else None
+    if embed_strategy == "gps":
+        assert lam is not None
+        w = np.sqrt(lam)
+        w /= w[0]
+        return phi / w
+    if embed_strategy == "hks":
+        assert lam is not None
+        phi = _heat_kernel_signature(phi, lam, ts)
+    elif embed_strategy is not None:
+        raise ValueError(f"Unknown embedding strategy {embed_strategy}")
+    if rescale_strategy not in _RESCALE:
         raise RuntimeError(f"Unknown rescaling strategy: {rescale_strategy}")
-
-    return torch.from_numpy(np.ascontiguousarray(eigenfunctions)).to(dtype=torch.float32)
+    return torch.from_numpy(np.ascontiguousarray(_RESCALE[rescale_strategy](phi))).to(dtype=torch.float32)
 
 
 def get_k_eigenfunc_vec_vals(E, vertex_idxs_of_hit_faces, barycentric_coords):
