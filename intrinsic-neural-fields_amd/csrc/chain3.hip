@@ -39,8 +39,6 @@
 // is copied to HBM by a ninth "store" wave that mirrors the compute waves' barriers and
 // does the ray-major -> feature-major transposes from the LDS tile.  Stores in the compute
 // waves would join the in-order vmcnt queue and make the next fragment wait for them.
-#include <cstdlib>
-
 #include "chain3.hpp"
 #include "c3common.hpp"
 
@@ -58,9 +56,6 @@ constexpr int C3_LDS_CAP = 160 * 1024;
 #define C3_DEPTH 8
 #endif
 constexpr int C3BM = 16;  // rays per workgroup
-#ifndef C3_XSTAGE
-#define C3_XSTAGE 1  // chunked tile: the store wave stages the next chunk's rows (0: the compute waves gather each chunk)
-#endif
 #ifndef C3_GATHER_CPOL
 #define C3_GATHER_CPOL 2  // table rows are read once per step: non-temporal, spare the weights' L2 lines
 #endif
@@ -92,18 +87,6 @@ struct L3 {
   __host__ __device__ static int off_x(int L) { return OFF_VEC + L * H * 4; }
   __host__ __device__ static int off_stamp(int L, int kx) { return off_x(L) + BM * kx * 2; }
   static int lds_bytes(int L, int kx) { return off_stamp(L, kx) + (7 * C3_MAX_PHASES + 8) * 8; }
-  // chunked tile (XC): the next chunk's raw table rows, staged by the store wave's LDS-DMA
-  // loads while the current chunk streams.  1 KiB blocks: block 3 G + i = corner i of
-  // item group G (64 consecutive 16-byte chunks of one row: row G / 2, chunks 64 (G % 2)
-  // ..), lane l's piece at 16 l.  The first STG_ACT blocks overlay the activation tiles
-  // (idle until phase 0's epilogue, after the last chunk), the rest follow the stamps.
-  static constexpr int STG_GROUPS = BM * (C3_KC / 8) / 64;
-  static constexpr int STG_BLOCKS = 3 * STG_GROUPS;
-  static constexpr int STG_ACT = 2 * ACT_BYTES / 1024 < STG_BLOCKS ? 2 * ACT_BYTES / 1024 : STG_BLOCKS;
-  __host__ __device__ static int stg_off(int L, int kx, int b) {
-    return b < STG_ACT ? OFF_ACT + b * 1024 : off_stamp(L, kx) + (7 * C3_MAX_PHASES + 8) * 8 + (b - STG_ACT) * 1024;
-  }
-  static int lds_bytes_staged(int L, int kx) { return lds_bytes(L, kx) + (STG_BLOCKS - STG_ACT) * 1024; }
   static_assert(TN >= 1 && TN * 4 <= 8, "ReLU bits of a lane: at most 8 per layer");
   static_assert(OFF_LS % 8 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
@@ -114,11 +97,8 @@ struct L3 {
 // k = 4096).  Phase 0 then runs BOTH input layers over each chunk -- Ly's product
 // W_y x is independent of h, so it is accumulated in a second register set (accy) while
 // the chunk is resident and added in the skip layer's epilogue; each chunk is gathered
-// once: chunk 0 by the compute waves at the start, every later one staged raw (three
-// rows per ray) in LDS by the store wave's LDS-DMA loads while the previous chunk
-// streams, and folded into the tile at the chunk's first block (two barriers: everyone
-// is done with the previous chunk / the new one is in LDS); the store wave copies each
-// chunk's X^T between them.
+// once, at its first block (two barriers: everyone is done with the previous chunk /
+// the new one is in LDS), and the store wave copies its X^T between them.
 template <int H, int LOSS, bool ENC, bool XC>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
   using C = L3<H>;
@@ -468,37 +448,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           const int c = B.flags >> C3F_CHUNK_SHIFT;
           lbar();  // G1: every wave is done with the previous chunk (and the store wave with its X^T)
           const int nc = min(C3_KC, k_pad - c * C3_KC);
-#if !C3_XSTAGE
           if (a.table_big) gather_cols(std::integral_constant<int, 2>{}, std::true_type{}, c * C3_KC, nc);
           else gather_cols(std::integral_constant<int, 2>{}, std::false_type{}, c * C3_KC, nc);
-#else
-          {
-            // the store wave staged the chunk's raw rows (landed before it joined G1): fold
-            // them into the tile -- item group G = wave + 8 m, the gather's arithmetic
-#pragma unroll 1
-            for (int m = 0; m < C::STG_GROUPS / C3_CW; ++m) {
-              const int G = wc + C3_CW * m, r = G >> 1, ch = (G & 1) * 64 + lane;
-              if (ch < (nc >> 3) && a.xpre != nullptr) {  // pre-gathered rows: staged as corner 0
-                *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) =
-                    *reinterpret_cast<const u16x8*>(smem + C::stg_off(L, kx, 3 * G) + lane * 16);
-              } else if (ch < (nc >> 3)) {
-                u16x8 ev[3];
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-                  ev[i] = *reinterpret_cast<const u16x8*>(smem + C::stg_off(L, kx, 3 * G + i) + lane * 16);
-                const int ok = rvid[BM * 4 + r * 3] & rvid[BM * 4 + r * 3 + 1] & rvid[BM * 4 + r * 3 + 2];
-                const float w0 = rbary[r * 3], w1 = rbary[r * 3 + 1], w2 = rbary[r * 3 + 2];
-                u16x8 o;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                  const float x = fmaf(w2, bf_val3(ev[2][e]), fmaf(w1, bf_val3(ev[1][e]), w0 * bf_val3(ev[0][e])));
-                  o[e] = bf_bits3(ok ? x : 0.f);
-                }
-                *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
-              }
-            }
-          }
-#endif
           lbar();  // G2: chunk c in LDS
         }
         if (B.flags & C3F_SWAP) {
@@ -531,7 +482,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
       // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
       // latency is exposed at every k-block, behind only TN MFMAs)
-      // (not in the chunked variant: measured 2-3 us slower over config D's input phase)
+      // (not in the chunked variant: its second accumulator set leaves no room -- it spills)
       constexpr bool BPF = !XC;
       bf16x8 bq[2];
       if constexpr (BPF) bq[0] = bread(0);
@@ -831,38 +782,13 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     if constexpr (XC) {
       // chunked tile: X^T of chunk c between barriers G2(c) and G1(c + 1) (x_tile0 shifts
       // the image's tile index to the chunk's LDS columns)
-      // xc_stage: the next chunk's raw rows go to the staging blocks by LDS-DMA loads issued
-      // here, after the compute waves folded the current chunk (G2) and this wave read its
-      // X^T (the compiler drains vmcnt before any LDS read behind an LDS-DMA load), so
-      // they land while the chunk's input-layer blocks stream (~10 us); this wave does no
-      // other loads, so its one full wait before G1 is all the hand-off needs
-      auto stage_chunk = [&](int c) {
-        const int nc = min(C3_KC, k_pad - c * C3_KC);
-#pragma unroll 1
-        for (int G = 0; G < C::STG_GROUPS; ++G) {
-          const int r = G >> 1, ch = (G & 1) * 64 + lane;
-          const int64_t col = (int64_t)c * C3_KC + (ch < (nc >> 3) ? ch : 0) * 8;
-          if (a.xpre != nullptr) {  // pre-gathered rows (no ray records were read): the row itself
-            const bf16* src = a.xpre + (int64_t)(b0 + r) * k_pad + col;
-            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(smem + C::stg_off(L, kx, 3 * G)), 16, 0, 0);
-            continue;
-          }
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const bf16* src = a.table + (int64_t)rvid[r * 4 + i] * k_pad + col;
-            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(smem + C::stg_off(L, kx, 3 * G + i)), 16, 0, 0);
-          }
-        }
-      };
       for (int c = 0; c < a.nchunk; ++c) {
         if (c > 0) {
-          if (a.xc_stage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           lbar();  // G1(c)
           lbar();  // G2(c)
         }
         x_tile0 = c * (C3_KC / 16);
         copy_image(x_addr, k_pad, a.XT, c * (C3_KC / 32), min((c + 1) * C3_KC, k_pad) / 32);
-        if (a.xc_stage && c + 1 < a.nchunk) stage_chunk(c + 1);
       }
     } else {
       copy_image(x_addr, k_pad, a.XT, 0, xs_mid);
@@ -915,12 +841,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 }
 
 template <int H, int LOSS, bool ENC, bool XC>
-int launch3_enc(const Chain3Args& a_in, hipStream_t stream) {
+int launch3_enc(const Chain3Args& a, hipStream_t stream) {
   using C = L3<H>;
-  Chain3Args a = a_in;
-  // chunked tile: the next chunk's rows are always staged (the blocks fit at every depth)
-  a.xc_stage = XC && C3_XSTAGE;
-  const int lds = a.xc_stage ? C::lds_bytes_staged(a.L, a.kc) : C::lds_bytes(a.L, a.kc);
+  const int lds = C::lds_bytes(a.L, a.kc);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {

@@ -51,7 +51,6 @@ struct Chain3Args {
   // feature columns held in LDS at a time: k_pad (whole tile) or C3_KC (chunked, k_pad >
   // C3_KC: config D's k = 4096 tile is 128 KiB for 16 rays, above the LDS budget)
   int32_t kc, nchunk;
-  int32_t xc_stage;   // chunked tile: next chunk's rows staged in LDS by the store wave (set by the launcher)
   int32_t table_big;  // table of 4 GiB or more: 64-bit row addresses (set by launch_chain3)
   // pre-gathered features (inf_prefetch_batch): row b of xpre [rows][k_pad] bf16 is ray b's
   // feature row, read instead of gathering three table rows (null: gather)
