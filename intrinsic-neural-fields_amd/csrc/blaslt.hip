@@ -85,7 +85,10 @@ int blaslt_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, 
     LT_TRY(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)));
     // the heuristic may rank algorithms that need more workspace than offered first (a
     // 400k-row problem came back with one): take the best that fits
-    constexpr int NREQ = 16;
+#ifndef BLASLT_NREQ
+#define BLASLT_NREQ 16
+#endif
+    constexpr int NREQ = BLASLT_NREQ;
     hipblasLtMatmulHeuristicResult_t res[NREQ] = {};
     int n = 0;
     const hipblasStatus_t hs =

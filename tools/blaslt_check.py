@@ -34,3 +34,13 @@ for V in (1000, 400_000):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
     print(f"   {ms * 1e3:.1f} us -> {V * 512 * 1024 * 2 / ms / 1e9:.0f} TFLOP/s", flush=True)
+    Wb = Wc.bfloat16()
+    for _ in range(3):
+        torch.matmul(T, Wb.t())
+    e0.record()
+    for _ in range(10):
+        torch.matmul(T, Wb.t())
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    print(f"   torch.matmul {ms * 1e3:.1f} us -> {V * 512 * 1024 * 2 / ms / 1e9:.0f} TFLOP/s", flush=True)
