@@ -141,8 +141,7 @@ class Trainer:
         """all-reduce of the flat gradient bucket, then the replicated Adam + batch advance"""
         if torch.distributed.is_initialized():
             torch.distributed.all_reduce(self.plan.grads)
-        self.plan.adam(0, 0.0)
-        self.plan.ctrl_advance()
+        self.plan.adam(0, 0.0, advance=True)
 
     def _capture_dp_steps(self, s):
         """GRAPH_STEPS whole data-parallel steps (RCCL all-reduce included) in one graph: no
@@ -177,8 +176,7 @@ class Trainer:
                 gm = self._capture_dp_steps(s)
                 g2 = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g2, stream=s):
-                    self.plan.adam(0, 0.0)
-                    self.plan.ctrl_advance()
+                    self.plan.adam(0, 0.0, advance=True)
             else:
                 # several steps per graph: one replay launch per GRAPH_STEPS steps (an even
                 # number: the pre-gather slots alternate)

@@ -243,6 +243,11 @@ int inf_prefetch_batch(inf_plan* plan, const inf_batch* batch, int slot, inf_str
  * ctrl->step). */
 int inf_adam(inf_plan* plan, int step, float lr, inf_stream_t stream);
 
+/* inf_adam with flags: INF_STEP_ADVANCE also advances ctrl->batch_index by one in the same
+ * launch (the data-parallel step's tail: all-reduce -> Adam + advance, instead of a
+ * separate inf_ctrl_advance launch).  flags = 0 is inf_adam. */
+int inf_adam_ex(inf_plan* plan, int step, float lr, int flags, inf_stream_t stream);
+
 /* Render slice (renderer.py:112-146): forward of `batch` and placement of each
  * predicted colour at image row pixel_map[hit[b]] (hit = hit_ray_idxs; pixel_map maps
  * masked-pixel index -> full-image pixel, NULL for identity).  img is [H*W][3] fp32

@@ -32,6 +32,9 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef LG_SLAB_SC1
+#define LG_SLAB_SC1 0
+#endif
 #ifndef LG_DEPTH
 #define LG_DEPTH 4
 #endif
@@ -210,10 +213,14 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
       const f32x4 v = {Cs[(mq * 4 + 0) * CLD + col], Cs[(mq * 4 + 1) * CLD + col], Cs[(mq * 4 + 2) * CLD + col],
                        Cs[(mq * 4 + 3) * CLD + col]};
       const int64_t eo = (int64_t)(n0 + col) * P.slab_ld + m0 + mq * 4;
-      if (FUSED)
+      if (FUSED || LG_SLAB_SC1)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (unsigned)(eo * 4), 0, 16);
       else
+#ifdef LG_SLAB_NT
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst + eo));
+#else
         *reinterpret_cast<f32x4*>(dst + eo) = v;
+#endif
     }
     if (FUSED) {
       // publish this partial (sc1 stores drained by every wave, then a relaxed agent-scope

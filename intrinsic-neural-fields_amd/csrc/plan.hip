@@ -1240,7 +1240,10 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   return launch_update(step_update(Bp, nloss), p->mode, st);
 }
 
-int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) {
+int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) { return inf_adam_ex(p, step, lr, 0, stream); }
+
+int inf_adam_ex(inf_plan* p, int step, float lr, int flags, inf_stream_t stream) {
+  INF_CHECK_ARG((flags & ~INF_STEP_ADVANCE) == 0, "adam: unknown flags");
   if (p == nullptr || !p->bound || p->grads == nullptr || p->exp_avg == nullptr || p->exp_avg_sq == nullptr) {
     set_error("adam: plan not bound with grads and Adam state");
     return INF_ERR_STATE;
@@ -1251,6 +1254,7 @@ int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) {
   a.write_shadow = 1;
   a.step_host = step;
   a.lr_host = lr;
+  a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
   return launch_update(a, p->mode, (hipStream_t)stream);
 }
 

@@ -112,8 +112,7 @@ class DataParallelEpoch:
 
     def _tail_all_reduce(self, rt, plan):
         allreduce_grads(rt.grads, self.group)
-        plan.adam(0, 0.0)
-        plan.ctrl_advance()
+        plan.adam(0, 0.0, advance=True)
 
     def _step(self, rt, plan, batch, xslot=None):
         plan.train_step(batch, None, apply_adam=False, xslot=xslot)

@@ -94,6 +94,7 @@ _SIGNATURES = {
     "inf_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_train_step": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_int, c_void_p]),
     "inf_adam": (c_int, [c_void_p, c_int, c_float, c_void_p]),
+    "inf_adam_ex": (c_int, [c_void_p, c_int, c_float, c_int, c_void_p]),
     "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_projected_rows": (c_int64, [c_int64]),
     "inf_project_table": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),

@@ -409,8 +409,11 @@ class Plan:
             return False
         check(rc, "prefetch_batch")
 
-    def adam(self, step: int = 0, lr: float = 0.0):
-        check(lib.inf_adam(self.handle, int(step), float(lr), stream_handle()), "adam")
+    def adam(self, step: int = 0, lr: float = 0.0, advance: bool = False):
+        """inf_adam; advance=True also moves ctrl.batch_index on in the same launch
+        (inf_adam_ex with INF_STEP_ADVANCE: the data-parallel step's tail)."""
+        check(lib.inf_adam_ex(self.handle, int(step), float(lr), STEP_ADVANCE if advance else 0, stream_handle()),
+              "adam")
 
     def render(self, b: Batch, hit: torch.Tensor, pixel_map: torch.Tensor | None, img: torch.Tensor):
         check(lib.inf_render(self.handle, ctypes.byref(b), ptr(hit), ptr(pixel_map), ptr(img), stream_handle()),

@@ -364,22 +364,26 @@ def test_dp_step_shape_bitwise_equals_fused_step():
                          torch.from_numpy(rng.random((N, 3)).astype(np.float32)).cuda())
     perm = torch.from_numpy(rng.permutation(N)).cuda()
     out = {}
-    for shape in ("fused", "dp"):
+    for shape in ("fused", "dp", "dp_adam_advance"):
         plan, params, _ = make_plan("B", mode="bf16", max_batch=B, adam=True)
         plan.set_lr(1e-3)
         b = plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B, offset_from_ctrl=True, loss_count=3 * B)
         for _ in range(nb):
             if shape == "fused":
                 plan.train_step(b, None, apply_adam=True, advance=True)
-            else:
+            elif shape == "dp":
                 plan.train_step(b, None, apply_adam=False)
                 plan.adam(0, 0.0)
                 plan.ctrl_advance()
+            else:  # inf_adam_ex(INF_STEP_ADVANCE): Adam and the advance in one launch
+                plan.train_step(b, None, apply_adam=False)
+                plan.adam(0, 0.0, advance=True)
         c = plan.read_ctrl()
         out[shape] = (params.cpu().numpy(), plan.exp_avg.cpu().numpy(), plan.exp_avg_sq.cpu().numpy(),
                       c["step"], c["batch_index"], c["epoch_loss"])
-    f, d = out["fused"], out["dp"]
-    assert f[3] == d[3] == nb and f[4] == d[4] == nb
-    for a, b_ in zip(f[:3], d[:3]):
-        np.testing.assert_array_equal(a, b_)
-    assert f[5] == d[5]
+    f = out["fused"]
+    for d in (out["dp"], out["dp_adam_advance"]):
+        assert f[3] == d[3] == nb and f[4] == d[4] == nb
+        for a, b_ in zip(f[:3], d[:3]):
+            np.testing.assert_array_equal(a, b_)
+        assert f[5] == d[5]
