@@ -2,8 +2,6 @@
 // (lgemm.hip), which runs the same work items for a tile once its last split-K partial
 // has landed: one definition, bitwise-identical results either way.
 #pragma once
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 
 #include <cmath>
 
@@ -75,29 +73,6 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
       for (int i = 0; i < NR; ++i) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) adam_elem(w[i][j], m[i][j], v[i][j], g[i][j], a, sc);
-#ifdef AD_MV_SC1
-        if (VEC4 && ok[i]) {  // write-through (sc1): the next update reads them from MALL/HBM
-          typedef float f32x4_t __attribute__((ext_vector_type(4)));
-          float* bases[3] = {a.params, a.exp_avg, a.exp_avg_sq};
-          const float (*vals[3])[4] = {&w[i], &m[i], &v[i]};
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bases[q], (short)0, 0x7FFFFFFF, 0x00020000);
-            const f32x4_t x = {(*vals[q])[0], (*vals[q])[1], (*vals[q])[2], (*vals[q])[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, x), rs, (unsigned)(e[i] * 4), 0, 16);
-          }
-          continue;
-        }
-#endif
-#ifdef AD_MV_NT
-        typedef float f32x4_t __attribute__((ext_vector_type(4)));
-        if (VEC4 && ok[i]) {
-          __builtin_nontemporal_store((f32x4_t){w[i][0], w[i][1], w[i][2], w[i][3]}, reinterpret_cast<f32x4_t*>(a.params + e[i]));
-          __builtin_nontemporal_store((f32x4_t){m[i][0], m[i][1], m[i][2], m[i][3]}, reinterpret_cast<f32x4_t*>(a.exp_avg + e[i]));
-          __builtin_nontemporal_store((f32x4_t){v[i][0], v[i][1], v[i][2], v[i][3]}, reinterpret_cast<f32x4_t*>(a.exp_avg_sq + e[i]));
-          continue;
-        }
-#endif
         st4(a.params, i, w[i]);
         st4(a.exp_avg, i, m[i]);
         st4(a.exp_avg_sq, i, v[i]);
@@ -105,11 +80,12 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
     }
   }
   if (!a.write_shadow) return;
+  const bool rowmajor = a.write_shadow != 2;
   // packed row-major shadow: 4 consecutive columns per store (padded columns stay zero)
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int r = rb + 32 * i;
-    if (ok[i]) {
+    if (ok[i] && rowmajor) {
       T* dst = reinterpret_cast<T*>(seg.W) + (int64_t)(item.r0 + r) * seg.ldw + gc;
       if (VEC4) {
         if constexpr (sizeof(T) == 2) {
@@ -136,13 +112,7 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
         const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
         const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
         const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
-#ifdef AD_IMG_SC1
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, pk),
-                                              __builtin_amdgcn_make_buffer_rsrc(seg.WF, (short)0, 0x7FFFFFFF, 0x00020000),
-                                              (unsigned)(e * 2), 0, 16);
-#else
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
-#endif
       }
     }
   }
@@ -158,17 +128,12 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
         const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
-#ifdef AD_IMG_SC1
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v),
-                                               __builtin_amdgcn_make_buffer_rsrc(seg.WTF, (short)0, 0x7FFFFFFF, 0x00020000),
-                                               (unsigned)(off * 2), 0, 16);
-#else
         *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
-#endif
       }
     }
   }
   // packed transposed shadow: 64 consecutive rows of one column per wave
+  if (!rowmajor) return;  // write_shadow = 2: fragment images only (plan.hip ensure_rowmajor)
 #pragma unroll
   for (int i = 0; i < ADAM_TILE_R * ADAM_TILE_C / 256; ++i) {
     const int idx = tid + 256 * i;

@@ -766,11 +766,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           if (s0 + u < s_end) {
             const int t = 2 * (s0 + u) + (tg >> 1);
             const s16x4x8 o = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
-#ifdef C3_IMG_NT
-            __builtin_nontemporal_store(o, reinterpret_cast<s16x4x8*>(d + (int64_t)t * 1024));
-#else
             *reinterpret_cast<s16x4x8*>(d + (int64_t)t * 1024) = o;
-#endif
           }
         }
       }
@@ -800,11 +796,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
       for (int c = lane * 16; c < bytes; c += 64 * 16)
-#ifdef C3_IMG_NT
-        __builtin_nontemporal_store(*reinterpret_cast<const u16x8*>(src + c), reinterpret_cast<u16x8*>(d + c));
-#else
         *reinterpret_cast<u16x8*>(d + c) = *reinterpret_cast<const u16x8*>(src + c);
-#endif
     };
 #ifdef C3_STREAM_ONLY
 #ifdef C3_STREAM_BARRIERS

@@ -97,6 +97,13 @@ struct inf_plan {
   bool saved = false;
   int last_chain = 0;  // fused chain of the last training step: 0 none, 2 LDS ring, 3 registers
   bool stepped = false;
+  // Row-major / transposed bf16 shadows (W, W^T) are read only off the fused path (layered
+  // and LDS-ring GEMMs, the table projection); the fused chain3 step's update writes the
+  // fragment images alone (write_shadow = 2) and marks them stale.  rm_stale: an eager
+  // lazy update ran since the last rewrite; rm_captured: a lazy update was captured into a
+  // graph, whose replays the host cannot see -- consumers then rewrite them every time.
+  bool rm_stale = false;
+  bool rm_captured = false;
   const uint64_t* dbg_ranges = nullptr;
   int dbg_n = 0;
   unsigned long long* dbg_out = nullptr;
@@ -296,6 +303,8 @@ GemmProblem blank_problem() {
 int dtype_of(const inf_plan* p) { return p->mode == INF_MODE_BF16 ? INF_DTYPE_BF16 : INF_DTYPE_F32; }
 
 // ---------------------------------------------------------------------------------
+int ensure_rowmajor(inf_plan* p, hipStream_t st);
+
 int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStream_t st) {
   void* x0 = p->W(p->o_x0);
   void* x0t = transposed ? (void*)p->W(p->o_x0t) : nullptr;
@@ -323,6 +332,7 @@ int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStrea
 int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t st);
 
 int run_forward_layers(inf_plan* p, int Bp, bool transposed, hipStream_t st) {
+  if (int rc = ensure_rowmajor(p, st)) return rc;
   for (int l = 0; l < p->L - 1; ++l) {
     int rc = run_forward_layer(p, Bp, transposed, l, st);
     if (rc) return rc;
@@ -376,6 +386,7 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const A
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
+  if (int rc = ensure_rowmajor(p, st)) return rc;
   const int H = p->H, L = p->L;
   const GemmTile tile = pick_tile(p, Bp, H);
   for (int l = L - 2; l >= 1; --l) {
@@ -511,6 +522,40 @@ AdamArgs update_args(inf_plan* p, int Bp) {
   return a;
 }
 
+bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// An update launch that leaves W / W^T behind (write_shadow = 2) or rewrites them (1).
+void note_shadow_write(inf_plan* p, const AdamArgs& a, hipStream_t st) {
+  const bool capturing = stream_capturing(st);
+  if (a.write_shadow == 2) {
+    p->rm_stale = true;
+    if (capturing) p->rm_captured = true;
+  } else if (a.write_shadow == 1 && !capturing) {
+    p->rm_stale = false;
+  }
+}
+
+// Before any launch that reads W / W^T: rewrite every shadow from the fp32 masters if a
+// lazy update may have run since they were last written (always, once one was captured).
+int ensure_rowmajor(inf_plan* p, hipStream_t st) {
+  if (!p->rm_stale && !p->rm_captured) return INF_OK;
+  AdamArgs a = update_args(p, p->bp_max);
+  a.grad_src = GRAD_NONE;
+  a.write_shadow = 1;
+  const int rc = launch_update(a, p->mode, st);
+  if (rc == INF_OK && !stream_capturing(st)) p->rm_stale = false;
+  return rc;
+}
+
+// fused chain3 steps in bf16 leave the row-major shadows to ensure_rowmajor
+// (INF_EAGER_SHADOWS=1: every update rewrites all shadows)
+int step_shadow_mode(const inf_plan* p, int chain) {
+  return chain == 3 && p->mode == INF_MODE_BF16 && std::getenv("INF_EAGER_SHADOWS") == nullptr ? 2 : 1;
+}
+
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
   const int parts = chain == 3 ? Bp / chain3_bm(Bp) : chain ? Bp / chain_partial_rows(chain_bm(Bp)) : Bp / 64;
@@ -611,6 +656,7 @@ bool use_chain(const inf_plan* p) {
 // batch whose features are already in X0 (csrc/chain.hip).
 int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, const int64_t* hit,
               const int64_t* pixel_map, float* img, hipStream_t st) {
+  if (int rc = ensure_rowmajor(p, st)) return rc;
   const int H = p->H, L = p->L, s = p->s;
   const int bm = chain_bm(Bp);
   const int BK = chain_bk(bm);
@@ -1119,7 +1165,9 @@ int inf_sync_shadow(inf_plan* p, inf_stream_t stream) {
   AdamArgs a = update_args(p, p->bp_max);
   a.grad_src = GRAD_NONE;
   a.write_shadow = 1;
-  return launch_update(a, p->mode, (hipStream_t)stream);
+  const int rc = launch_update(a, p->mode, (hipStream_t)stream);
+  if (rc == INF_OK) note_shadow_write(p, a, (hipStream_t)stream);
+  return rc;
 }
 
 int inf_forward(inf_plan* p, const inf_batch* batch, float* pred, int save, inf_stream_t stream) {
@@ -1179,7 +1227,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     a.grad_src = GRAD_SLABS;
     if (apply_adam) {
       a.do_adam = 1;
-      a.write_shadow = 1;
+      a.write_shadow = step_shadow_mode(p, ck);
     } else {
       a.write_grads = 1;
     }
@@ -1210,7 +1258,9 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       p->last_chain = 3;
       if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
       const AdamArgs a = step_update(Bp, nloss);
-      return run_weight_grads(p, Bp, st, 3, &a);
+      if ((rc = run_weight_grads(p, Bp, st, 3, &a))) return rc;
+      note_shadow_write(p, a, st);
+      return INF_OK;
     }
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
   } else if (chain) {
@@ -1237,7 +1287,10 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   p->stepped = true;
   const int Bp = p->saved_bp;
   if ((rc = refresh_tables(p, Bp, st, ck))) return rc;
-  return launch_update(step_update(Bp, nloss), p->mode, st);
+  const AdamArgs ua = step_update(Bp, nloss);
+  if ((rc = launch_update(ua, p->mode, st))) return rc;
+  note_shadow_write(p, ua, st);
+  return INF_OK;
 }
 
 int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) { return inf_adam_ex(p, step, lr, 0, stream); }
@@ -1255,7 +1308,11 @@ int inf_adam_ex(inf_plan* p, int step, float lr, int flags, inf_stream_t stream)
   a.step_host = step;
   a.lr_host = lr;
   a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
-  return launch_update(a, p->mode, (hipStream_t)stream);
+  // after a fused chain3 step (the data-parallel tail) only the fragment images
+  a.write_shadow = step_shadow_mode(p, p->last_chain);
+  const int rc = launch_update(a, p->mode, (hipStream_t)stream);
+  if (rc == INF_OK) note_shadow_write(p, a, (hipStream_t)stream);
+  return rc;
 }
 
 int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const int64_t* pixel_map, float* img,
@@ -1289,6 +1346,7 @@ int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void
   const int H = p->H, k_pad = p->k_pad;
   const ParamSeg* w[2] = {p->weight_seg(0, 0), p->weight_seg(p->s, 1)};
   INF_CHECK_ARG(p->o_pcat >= 0 && w[0]->c_pad == k_pad && w[1]->c_pad == k_pad, "project_table: weight layout");
+  if (int rc = ensure_rowmajor(p, st)) return rc;  // W_0 / W_y rows below
   char* pcat = p->shadow + p->o_pcat;
   const size_t wbytes = (size_t)H * k_pad * 2;
   for (int h = 0; h < 2; ++h)
@@ -1363,6 +1421,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       break;
     case INF_STAGE_FWD_GEMM: {
       INF_CHECK_ARG(layer >= 1 && layer <= p->L - 2, "forward stage layer must be a hidden layer");
+      if ((rc = ensure_rowmajor(p, st))) return rc;
       rc = run_forward_layer(p, Bp, true, layer, st);
       const double K = (layer == p->s) ? H + k : H;
       f = 2.0 * B * H * K;
@@ -1404,16 +1463,18 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
         // the step's update as launched by inf_train_step: Adam and the weight images
         // (parameters change; lr from ctrl)
         a.do_adam = 1;
-        a.write_shadow = 1;
+        a.write_shadow = step_shadow_mode(p, p->last_chain);
       } else {
         INF_CHECK_ARG(p->grads != nullptr, "update stage needs a bound grads arena");
         a.write_grads = 1;  // reduce only into the grads arena: parameters unchanged
       }
       rc = launch_update(a, p->mode, st);
+      if (rc == INF_OK) note_shadow_write(p, a, st);
+      const int nimg_rm = a.write_shadow == 2 ? 0 : 2;  // W, W^T
       for (const auto& g : p->segs) {
         const double n = (double)g.R * g.C;
         by += 4.0 * n * (g.gemm ? p->dw_splits : 1) + 4.0 * n;  // partials in, gradient out
-        if (layer == 1) by += 20.0 * n + (g.gemm ? 2.0 * n * (g.ft_off >= 0 ? 4 : 3) : 0.0);
+        if (layer == 1) by += 20.0 * n + (g.gemm ? 2.0 * n * ((g.ft_off >= 0 ? 2 : 1) + nimg_rm) : 0.0);
       }
       break;
     }
