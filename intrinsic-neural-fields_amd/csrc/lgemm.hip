@@ -38,12 +38,16 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef LG_DEPTH
 #define LG_DEPTH 4
 #endif
+#ifndef LG_RA
+#define LG_RA 4
+#endif
 
 template <int BM>
 struct LG {
   static constexpr int TM = BM / 16, TN = 2;
   static constexpr int D = LG_DEPTH;  // B units in flight per wave (fragment register ring)
-  static constexpr int RA = 4;  // A stages (64 deep) in flight in registers
+  static constexpr int RA = LG_RA;  // A stages (64 deep) in flight in registers
+  static_assert((2 * RA) % D == 0, "the B ring index must repeat every RA stages");
   static constexpr int ACH = BM * 8 / 256;  // 16-byte A chunks per thread per stage
   static constexpr int A_STAGE = BM * 128;  // bytes: BM rows x 64 bf16
   static constexpr int CLD = LG_BN + 4;     // f32 staging row stride
@@ -162,9 +166,9 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   if (stl != nullptr) stl[1] = wall_clock64();
 
 #pragma unroll 1
-  for (int s0 = 0; s0 < nst; s0 += 4) {
+  for (int s0 = 0; s0 < nst; s0 += RA) {
 #pragma unroll
-    for (int ss = 0; ss < 4; ++ss) {
+    for (int ss = 0; ss < RA; ++ss) {
       const int s = s0 + ss;
       const int nxt = (ss + 1) % RA;  // compile-time after unrolling
       if (s + 1 < nst) storeA((s + 1) & 1, ar[nxt]);
@@ -335,7 +339,7 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     if (p.splits < 1) p.splits = 1;
     INF_CHECK_ARG(p.Af != nullptr && p.Bf != nullptr, "lgemm: null operand");
     INF_CHECK_ARG(p.M > 0 && p.M % bm == 0 && p.N > 0 && p.N % LG_BN == 0, "lgemm: M/N not tile multiples");
-    INF_CHECK_ARG(p.K > 0 && p.K % (256 * p.splits) == 0, "lgemm: K per split must be a multiple of 256");
+    INF_CHECK_ARG(p.K > 0 && p.K % (64 * LG_RA * p.splits) == 0, "lgemm: K per split must be a multiple of 64 RA");
     INF_CHECK_ARG(p.a_row0 % 16 == 0 && p.a_row0 + p.M <= 16 * p.a_tiles && p.b_row0 % 16 == 0 &&
                       p.b_row0 + p.N <= 16 * p.b_tiles, "lgemm: operand layout");
     INF_CHECK_ARG(p.splits == 1 || p.slab != nullptr, "lgemm: split-K needs a slab");
