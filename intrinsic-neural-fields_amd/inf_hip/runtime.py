@@ -380,6 +380,9 @@ class Plan:
             b.batch = int(batch)
         b.loss_count = int(loss_count)
         b.loss = -1 if loss is None else LOSS_CODES[loss]
+        # the struct holds raw device pointers: keep their tensors alive with it (a
+        # temporary ray_idx would otherwise return to the caching allocator)
+        b._refs = (features, rgb, source, ray_idx, xyz, projected, enc)
         if b.batch < 1 or (b.batch > self.max_batch and b.encoding != ENC_PROJECTED):
             raise ValueError(f"batch of {b.batch} rays outside this plan's range 1..{self.max_batch}")
         return b

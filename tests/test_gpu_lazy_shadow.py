@@ -48,7 +48,8 @@ def test_rowmajor_shadows_follow_fused_steps():
     bary = rng.dirichlet([1, 1, 1], N).astype(np.float32)
     src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
                          torch.from_numpy(rng.random((N, 3)).astype(np.float32)).cuda())
-    b = plan.make_batch(source=src, ray_idx=torch.arange(N, device="cuda"), offset=0, batch=B,
+    idx = torch.arange(N, device="cuda")
+    b = plan.make_batch(source=src, ray_idx=idx, offset=0, batch=B,
                         offset_from_ctrl=True, loss_count=3 * B)
     X = O.gather(E, vids[:B], bary[:B])
 
