@@ -33,10 +33,13 @@ def _copy_config_file_into_out_dir(config, config_path):
     copyfile(config_path, os.path.join(config["training"]["out_dir"], "config.yaml"))
 
 
-def load_config_file(path, allow_checkpoint_loading=False):
-    """Reference config.py:26-36."""
+def load_config_file(path, allow_checkpoint_loading=False, follower=False):
+    """Reference config.py:26-36.  follower: a data-parallel rank other than 0 only reads
+    the file (rank 0 checks and creates out_dir; the others would find it existing)."""
     with open(path, "r") as f:
         config = yaml.safe_load(f)
+    if follower:
+        return config
     out_dir = config["training"]["out_dir"]
     if os.path.exists(out_dir) and not allow_checkpoint_loading:
         raise RuntimeError(f"out_dir '{out_dir}' exists. Exit to not overwrite old results.")

@@ -110,6 +110,10 @@ class DataParallelEpoch:
         self.steps_done = 0
         self.pipe = None
 
+    def graph_collective(self) -> bool:
+        """The all-reduce can be captured into the step graphs (RCCL; not gloo)."""
+        return self.world == 1 or dist.get_backend(self.group) != "gloo"
+
     def _tail_all_reduce(self, rt, plan):
         allreduce_grads(rt.grads, self.group)
         plan.adam(0, 0.0, advance=True)
@@ -181,7 +185,7 @@ class DataParallelEpoch:
         optim.sync_runtime_state(model, rt, plan, group)
         plan.reset_epoch_sums()
         steps = 0
-        use_graph = os.environ.get("INF_GRAPH", "1") != "0" and full >= 2
+        use_graph = os.environ.get("INF_GRAPH", "1") != "0" and full >= 2 and self.graph_collective()
         if full:
             batch = plan.make_batch(source=loader.source, ray_idx=self.idx, offset=0, batch=bs,
                                     offset_from_ctrl=True, loss_count=3 * B, loss=loss_type)
@@ -242,8 +246,17 @@ def main_distributed(config, seed, allow_checkpoint_loading=False):
     from trainer import Trainer
     from utils import model_summary
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # INF_DP_BACKEND=gloo: a rehearsal backend -- ranks may then share a GPU (local rank
+    # modulo the visible devices; RCCL refuses two ranks on one device) and the collective
+    # runs eagerly between the captured steps (gloo cannot be captured into a HIP graph)
+    backend = os.environ.get("INF_DP_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = f"cuda:{local}"
     try:
         mesh_path = config["data"].get("mesh_path")

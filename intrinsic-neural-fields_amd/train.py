@@ -30,7 +30,9 @@ def parse_args():
 
 def main():
     args = parse_args()
-    config = load_config_file(args.config_path, args.allow_checkpoint_loading)
+    distributed = args.data_parallel and "WORLD_SIZE" in os.environ  # launched by torchrun
+    follower = distributed and int(os.environ.get("RANK", "0")) != 0
+    config = load_config_file(args.config_path, args.allow_checkpoint_loading, follower=follower)
     seed = get_seed(config)
     random.seed(seed)
     np.random.seed(seed)
@@ -38,7 +40,7 @@ def main():
     if not torch.cuda.is_available():
         raise RuntimeError("this build trains on MI355X (HIP) devices; no GPU is visible")
     device = "cuda"
-    if args.data_parallel and "WORLD_SIZE" in os.environ:  # launched by torchrun
+    if distributed:
         import dp
         return dp.main_distributed(config, seed)
     # train.py:38 loads the mesh: the renderer casts against it and the extrinsic

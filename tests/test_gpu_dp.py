@@ -1,8 +1,9 @@
 """Data-parallel training on the GPU (dp.py): the Trainer's data-parallel epochs at world
 size 1 are bitwise its single-GPU fused epochs, and `train.py --data_parallel` under
 torchrun (an RCCL communicator, the collective captured in the step graphs) writes the
-same models and scalars as the single-process run.  World sizes above one are covered by
-tests/test_dp_gloo.py on the CPU (no multi-GPU box is available to this suite)."""
+same models and scalars as the single-process run; two ranks sharing the one GPU over gloo
+run the HIP step at world 2 against the single-process run.  tests/test_dp_gloo.py covers
+the sharding arithmetic on the CPU (no multi-GPU box is available to this suite)."""
 import json
 import os
 import socket
@@ -113,3 +114,60 @@ def test_train_data_parallel_torchrun_world1(tmp_path):
         assert torch.equal(ws[k], wd[k]), k
     assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
     np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=1e-9)
+
+
+@pytest.mark.parametrize("mode,w_rel,loss_rtol", [("fp32", 1e-6, 1e-6), ("bf16", 5e-2, 2e-3)])
+def test_train_data_parallel_two_ranks_one_gpu_gloo(tmp_path, mode, w_rel, loss_rtol):
+    """`torchrun --nproc-per-node 2 train.py <cfg> --data_parallel` with INF_DP_BACKEND=gloo:
+    two ranks share the box's one GPU (RCCL refuses that; gloo all-reduces the flat gradient
+    eagerly between the fused steps).  The HIP step at world 2 -- rank-sharded batches, the
+    loss normalised by the global batch, the all-reduced gradient, replicated Adam --
+    against the single-process run of the same config: the same files, the same logged
+    scalars up to the summation order of two half-batch gradients, and weights close in
+    relative L2 norm.  fp32 (parity mode) holds tight bounds; in bf16 a master-weight
+    difference at rounding level can flip a bf16 weight image's rounding, so the runs
+    part faster (seen after two epochs: fp32 weights 4e-8 relative, losses 5e-9; bf16
+    losses 3e-4, weights up to 1.9e-2 relative)."""
+    import synthetic_views as S
+    S.build(str(tmp_path), views=(4, 1, 1))
+    epochs, batch = 2, 512
+    cfg = S.intrinsic_config(epochs=epochs, batch=batch)
+    cfg["model"]["kernels"] = {"mode": mode}
+    # L2: with L1 a rounding-level change of a residual near zero flips its gradient's sign,
+    # and the two runs' trajectories part within a few epochs (seen: 2 % in val loss at 3)
+    cfg["training"]["loss_type"] = "L2"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", INF_DP_BACKEND="gloo")
+    results = {}
+    for tag in ("single", "dp2"):
+        cfg["training"]["out_dir"] = f"out/{tag}"
+        path = tmp_path / f"{tag}.yaml"
+        with open(path, "w") as fh:
+            yaml.safe_dump(cfg, fh)
+        if tag == "single":
+            cmd = [sys.executable, os.path.join(PKG, "train.py"), str(path)]
+        else:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(PKG, "train.py"),
+                   str(path), "--data_parallel"]
+        r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+        print(tag, r.stdout[-2000:], r.stderr[-3000:])
+        assert r.returncode == 0, tag
+        out = tmp_path / "out" / tag
+        files = sorted(os.listdir(out))
+        sd = torch.load(out / "model_last_epoch.pt", map_location="cpu", weights_only=True)
+        rows = [json.loads(x) for x in open(out / "logs" / "scalars.jsonl")]
+        results[tag] = (files, sd, rows)
+    (fs, ws, rs), (fd, wd, rd) = results["single"], results["dp2"]
+    assert fs == fd and {"model.pt", "model_last_epoch.pt", "checkpoint.pt", "logs"} <= set(fs)
+    lr = float(cfg["training"]["lr"])
+    for k in ws:
+        a, b = ws[k].float().numpy().reshape(-1), wd[k].float().numpy().reshape(-1)
+        # Adam moves every element by ~lr per step whatever its gradient's size, so order-
+        # level gradient differences leave element-wise drift of that order; a sharding or
+        # normalisation error would move whole tensors (and the logged losses, below)
+        d = np.abs(a - b)
+        rel = float(np.linalg.norm(a - b) / max(np.linalg.norm(a), 1e-12))
+        print(k, "max", float(d.max()), "rel", rel)
+        assert d.max() <= 2 * lr * 200 and rel <= w_rel, (k, float(d.max()), rel)
+    assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
+    np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=loss_rtol)
