@@ -148,6 +148,8 @@ class Trainer:
         host round trip per step.  INF_DP_EAGER_AR=1 keeps the all-reduce outside the graphs."""
         if os.environ.get("INF_DP_EAGER_AR"):
             return None
+        if torch.distributed.is_initialized() and torch.distributed.get_backend() == "gloo":
+            return None  # gloo cannot run inside a HIP graph capture (rehearsal backend)
         try:
             gm = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, stream=s):
@@ -739,8 +741,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 or os.environ.get("INF_BENCH_DP"):
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("INF_DP_BACKEND") == "gloo":
+            # rehearsal of the N > 1 code path on a box with fewer GPUs than ranks (RCCL
+            # refuses two ranks on one device): ranks share devices, eager all-reduce
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
