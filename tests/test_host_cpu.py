@@ -168,3 +168,22 @@ def test_viewdep_model_init_matches_reference(strategy):
     assert list(sd) == list(ref)
     for k, v in ref.items():
         np.testing.assert_array_equal(sd[k].numpy(), v, err_msg=k)
+
+
+def test_config_guard_only_on_rank0(tmp_path):
+    """config.load_config_file: the reference's "out_dir exists" guard (config.py:26-36)
+    for the leading process; a data-parallel follower rank (train.py --data_parallel,
+    RANK > 0) only reads the file -- rank 0 has created out_dir by then."""
+    import yaml
+
+    import config
+    out = tmp_path / "out"
+    path = tmp_path / "c.yaml"
+    with open(path, "w") as fh:
+        yaml.safe_dump({"training": {"out_dir": str(out)}, "model": {}}, fh)
+    c0 = config.load_config_file(str(path))
+    assert (out / "config.yaml").exists()
+    with pytest.raises(RuntimeError):
+        config.load_config_file(str(path))
+    c1 = config.load_config_file(str(path), follower=True)
+    assert c1 == c0
