@@ -559,7 +559,9 @@ def render_e2e_bench(args, device):
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
             "faces": int(Fn.shape[0]), "hits": hits, "raycast_ms": cast_ms,
             "raycast_rays_per_s": H * W / (cast_ms * 1e-3), "bvh_nodes": bvh.num_nodes, "bvh_depth": bvh.depth,
-            "bvh_build_s": build_s, "timing": "host wall clock per Renderer.render call (incl. the hit-count readback)"}
+            "bvh_build_s": build_s, "timing": "host wall clock per Renderer.render call (incl. the hit-count readback)",
+            "projected_table": "computed on the warm-up frame and kept by the Renderer across the timed frames "
+                               "(the weights do not change between them: inf_plan_weight_generation)"}
 
 
 def rff_bench(args, device, B=4096, reps=6):

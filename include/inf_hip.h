@@ -309,6 +309,13 @@ int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
  * -1 before any step. */
 int inf_plan_last_step_path(const inf_plan* plan);
 
+/* Weight generation: a counter of the launches issued through this plan that may have
+ * changed its parameters or weight images (training-step updates, inf_adam*,
+ * inf_sync_shadow), for caching what derives from the weights (the render slice's
+ * projected table across frames).  -1 once such a launch was captured into a graph:
+ * replays are invisible to the host, so nothing derived may then be cached. */
+int64_t inf_plan_weight_generation(const inf_plan* plan);
+
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);
 

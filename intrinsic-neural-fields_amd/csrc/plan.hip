@@ -104,6 +104,9 @@ struct inf_plan {
   // graph, whose replays the host cannot see -- consumers then rewrite them every time.
   bool rm_stale = false;
   bool rm_captured = false;
+  // inf_plan_weight_generation: update launches so far; gen_captured once one was captured
+  int64_t weight_gen = 0;
+  bool gen_captured = false;
   const uint64_t* dbg_ranges = nullptr;
   int dbg_n = 0;
   unsigned long long* dbg_out = nullptr;
@@ -530,6 +533,10 @@ bool stream_capturing(hipStream_t st) {
 // An update launch that leaves W / W^T behind (write_shadow = 2) or rewrites them (1).
 void note_shadow_write(inf_plan* p, const AdamArgs& a, hipStream_t st) {
   const bool capturing = stream_capturing(st);
+  if (a.write_shadow != 0 || a.do_adam) {
+    ++p->weight_gen;
+    if (capturing) p->gen_captured = true;
+  }
   if (a.write_shadow == 2) {
     p->rm_stale = true;
     if (capturing) p->rm_captured = true;
@@ -1536,6 +1543,11 @@ int inf_prefetch_batch(inf_plan* p, const inf_batch* b, int slot, inf_stream_t s
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;
   return p->last_chain == 3 && p->k_pad > C3_KC ? 4 : p->last_chain;
+}
+
+int64_t inf_plan_weight_generation(const inf_plan* p) {
+  if (p == nullptr) return -1;
+  return p->gen_captured ? -1 : p->weight_gen;
 }
 
 int inf_ctrl_advance(inf_plan* p, inf_stream_t stream) {

@@ -100,6 +100,7 @@ _SIGNATURES = {
     "inf_project_table": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_plan_last_step_path": (c_int, [c_void_p]),
+    "inf_plan_weight_generation": (c_int64, [c_void_p]),
     "inf_prefetch_batch": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "inf_debug_timing": (c_int, [c_void_p, c_void_p, c_int]),

@@ -451,6 +451,11 @@ class Plan:
         return {-1: None, 0: "layered", 2: "chain", 3: "chain3", 4: "chain3_chunked"}[
             int(lib.inf_plan_last_step_path(self.handle))]
 
+    def weight_generation(self) -> int:
+        """inf_plan_weight_generation: changes whenever an update launch may have moved the
+        weights; -1 once one was graph-captured (then nothing derived may be cached)."""
+        return int(lib.inf_plan_weight_generation(self.handle))
+
     def ctrl_advance(self):
         check(lib.inf_ctrl_advance(self.handle, stream_handle()), "ctrl_advance")
 

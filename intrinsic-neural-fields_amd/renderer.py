@@ -100,6 +100,11 @@ class Renderer:
         self.W = width
 
     def _features_on_device(self, device):
+        # "cuda" (no index) names the current device: compare resolved devices, or the
+        # table would be uploaded (and re-packed) on every frame
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         if self._dev_features is None or self._dev_features.device != device:
             self._dev_features = self.features.to(device=device, dtype=torch.float32).contiguous()
         return self._dev_features
@@ -157,10 +162,19 @@ class Renderer:
         chunk = min(RENDER_CHUNK, num_rays)
         plan = self.model.hip_plan(chunk)
         # enough hits per vertex: interpolate the vertices' first-layer projections instead
-        # of their features (inf_project_table; recomputed per call, the weights may move)
+        # of their features (inf_project_table).  The projected table is kept for the next
+        # frame while the plan's weight generation is unchanged (several views of one
+        # trained model: eval.py); recomputed whenever an update may have moved the weights
         proj = None
         if plan.can_project() and _project_enabled(num_rays, E.shape[0]):
-            proj = plan.project_table(src.table_for(plan))
+            T = src.table_for(plan)
+            gen = plan.weight_generation()
+            pc = self._table_cache.get("proj")
+            if pc is not None and gen >= 0 and pc[0] is plan and pc[1] == gen and pc[2] is T:
+                proj = pc[3]
+            else:
+                proj = plan.project_table(T)
+                self._table_cache["proj"] = (plan, gen, T, proj) if gen >= 0 else None
             chunk = min(num_rays, PROJECTED_CHUNK)  # no workspace: the frame in one persistent launch
         for low in range(0, num_rays, chunk):
             n = min(chunk, num_rays - low)

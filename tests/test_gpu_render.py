@@ -267,3 +267,51 @@ def test_render_projected_layer_schedules(L, s):
     X = O.gather(E.cpu().numpy(), vids.numpy(), bary.numpy())
     p_ref, _ = O.mlp_forward(w, X, L, s)
     assert np.abs(img[hit_np] - p_ref).max() < 2e-2
+
+
+def test_renderer_projection_cache_follows_weights(monkeypatch):
+    """Renderer.render_hits keeps the projected table across frames while the plan's weight
+    generation is unchanged, and recomputes it after a device-side training step (the
+    cached frame would otherwise show the old weights) and after host-side edits."""
+    import model as M
+    from inf_hip import runtime
+    from renderer import Renderer
+    rng = np.random.default_rng(9)
+    V, N, Hh, Ww, k = 500, 2000, 64, 64, 256
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32) * 0.3)
+    torch.manual_seed(0)
+    m = M.make_model({"k": k, "num_layers": 6, "mlp_hidden_dim": 128, "skip_layer_idx": 3}).cuda()
+    m.kernel_mode = "bf16"
+    m.hip_runtime().ensure_optimizer_arenas()
+    r = Renderer(m, None, eigenfunctions=E, H=Hh, W=Ww, device="cuda")
+    vids = torch.from_numpy(rng.integers(0, V, (N, 3)))
+    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32))
+    hit = torch.from_numpy(np.sort(rng.choice(Hh * Ww, N, replace=False)))
+    monkeypatch.setenv("INF_RENDER_PROJECT", "1")
+    a = r.render_hits(vids, bary, hit)
+    cached = r._table_cache["proj"]
+    assert cached is not None and cached[1] >= 0
+    a2 = r.render_hits(vids, bary, hit)
+    assert r._table_cache["proj"][3] is cached[3]  # reused, not recomputed
+    np.testing.assert_array_equal(a, a2)
+    # a device-side Adam step through the same plan
+    plan = m.hip_plan(N)
+    plan.set_lr(3e-2)
+    src = runtime.RaySource(E.cuda(), vids.cuda(), bary.cuda(), torch.rand((N, 3), device="cuda"))
+    for _ in range(3):
+        plan.train_step(plan.make_batch(source=src, batch=N, loss_count=3 * N), None, apply_adam=True)
+    b = r.render_hits(vids, bary, hit)
+    assert r._table_cache["proj"][3] is not cached[3]
+    monkeypatch.setenv("INF_RENDER_PROJECT", "0")
+    b_gather = r.render_hits(vids, bary, hit)
+    np.testing.assert_allclose(b, b_gather, atol=5e-3)
+    assert np.abs(b - a).max() > 2e-2  # the steps moved the frame
+    # host-side edit of the parameters (sync_shadow through hip_plan)
+    monkeypatch.setenv("INF_RENDER_PROJECT", "1")
+    with torch.no_grad():
+        for p in m.parameters():
+            p.mul_(0.5)
+    c = r.render_hits(vids, bary, hit)
+    monkeypatch.setenv("INF_RENDER_PROJECT", "0")
+    c_gather = r.render_hits(vids, bary, hit)
+    np.testing.assert_allclose(c, c_gather, atol=5e-3)
