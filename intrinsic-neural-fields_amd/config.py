@@ -20,37 +20,38 @@ from ray_dataloader import create_ray_dataloader
 from renderer import Renderer
 
 
-def _pretty_print_config(config, path):
-    print("----------------------------------------------------------------")
-    print(f"Loaded Config from {path}")
-    print("================================================================")
-    print(yaml.dump(config, default_flow_style=False))
-    print("================================================================\n")
+def _read_yaml(path):
+    with open(path, "r") as fh:
+        return yaml.safe_load(fh)
 
 
-def _copy_config_file_into_out_dir(config, config_path):
-    os.makedirs(config["training"]["out_dir"], exist_ok=True)
-    copyfile(config_path, os.path.join(config["training"]["out_dir"], "config.yaml"))
+def _announce(config, path):
+    """The banner the reference prints for a loaded training config."""
+    rule = "=" * 64
+    print("\n".join(["-" * 64, f"Loaded Config from {path}", rule,
+                     yaml.dump(config, default_flow_style=False), rule + "\n"]))
 
 
 def load_config_file(path, allow_checkpoint_loading=False, follower=False):
-    """Reference config.py:26-36.  follower: a data-parallel rank other than 0 only reads
-    the file (rank 0 checks and creates out_dir; the others would find it existing)."""
-    with open(path, "r") as f:
-        config = yaml.safe_load(f)
+    """Reference config.py:26-36: read the YAML, refuse an existing out_dir unless resuming,
+    print it, and keep a copy of the file as out_dir/config.yaml.  follower: a data-parallel
+    rank other than 0 only reads the file (rank 0 checks and creates out_dir; the others
+    would find it existing)."""
+    config = _read_yaml(path)
     if follower:
         return config
     out_dir = config["training"]["out_dir"]
     if os.path.exists(out_dir) and not allow_checkpoint_loading:
         raise RuntimeError(f"out_dir '{out_dir}' exists. Exit to not overwrite old results.")
-    _pretty_print_config(config, path)
-    _copy_config_file_into_out_dir(config, path)
+    _announce(config, path)
+    os.makedirs(out_dir, exist_ok=True)
+    copyfile(path, os.path.join(out_dir, "config.yaml"))
     return config
 
 
 def load_config(path):
-    with open(path, "r") as f:
-        return yaml.safe_load(f)
+    """A config file as a dict, nothing else (eval.py, renderer helpers)."""
+    return _read_yaml(path)
 
 
 def get_seed(config):
@@ -58,9 +59,10 @@ def get_seed(config):
 
 
 def get_log_dir(config):
-    if not os.path.exists(config["training"]["out_dir"]):
-        os.makedirs(config["training"]["out_dir"])
-    return os.path.join(config["training"]["out_dir"], "logs")
+    """out_dir/logs; out_dir is created if missing."""
+    out_dir = config["training"]["out_dir"]
+    os.makedirs(out_dir, exist_ok=True)
+    return os.path.join(out_dir, "logs")
 
 
 def get_data(config, device, num_workers_per_data_loader=6):
