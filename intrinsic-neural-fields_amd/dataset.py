@@ -14,19 +14,24 @@ import numpy as np
 import torch
 
 
+# (file, key in the returned dict, dtype) of a preprocessed split; the last two files are
+# written only for the view-dependent / extrinsic strategies and load as a pair
+_PREPROC_FILES = (("vids_of_hit_faces.npy", "vertex_idxs_of_hit_faces", torch.int64),
+                  ("barycentric_coords.npy", "barycentric_coords", torch.float32),
+                  ("expected_rgbs.npy", "expected_rgbs", torch.float32))
+_PREPROC_OPTIONAL = (("unit_ray_dirs.npy", "unit_ray_dirs", torch.float32),
+                     ("face_idxs.npy", "face_idxs", torch.int64))
+
+
 def load_preprocessed_data(preproc_data_path):
-    data = {}
-    v = np.load(os.path.join(preproc_data_path, "vids_of_hit_faces.npy"))
-    data["vertex_idxs_of_hit_faces"] = torch.from_numpy(v).to(dtype=torch.int64)
-    b = np.load(os.path.join(preproc_data_path, "barycentric_coords.npy"))
-    data["barycentric_coords"] = torch.from_numpy(b).to(dtype=torch.float32)
-    c = np.load(os.path.join(preproc_data_path, "expected_rgbs.npy"))
-    data["expected_rgbs"] = torch.from_numpy(c).to(dtype=torch.float32)
-    dirs_path = os.path.join(preproc_data_path, "unit_ray_dirs.npy")
-    face_path = os.path.join(preproc_data_path, "face_idxs.npy")
-    if os.path.exists(dirs_path) and os.path.exists(face_path):
-        data["unit_ray_dirs"] = torch.from_numpy(np.load(dirs_path)).to(dtype=torch.float32)
-        data["face_idxs"] = torch.from_numpy(np.load(face_path)).to(dtype=torch.int64)
+    """Reference dataset.py:12-33: the split's ray arrays as tensors of the reference's
+    dtypes (the optional direction / face-id pair only when both files exist)."""
+    def load(name, dtype):
+        return torch.from_numpy(np.load(os.path.join(preproc_data_path, name))).to(dtype=dtype)
+
+    data = {key: load(name, dt) for name, key, dt in _PREPROC_FILES}
+    if all(os.path.exists(os.path.join(preproc_data_path, name)) for name, _, _ in _PREPROC_OPTIONAL):
+        data.update({key: load(name, dt) for name, key, dt in _PREPROC_OPTIONAL})
     return data
 
 

@@ -77,16 +77,11 @@ def model_summary(model, data):
 
 
 def batchify_dict_data(data_dict, input_total_size, batch_size):
-    """Reference utils.py:72-83."""
-    idxs = np.arange(0, input_total_size)
-    batch_idxs = np.split(idxs, np.arange(batch_size, input_total_size, batch_size), axis=0)
-    batches = []
-    for cur_idxs in batch_idxs:
-        data = {}
-        for key in data_dict.keys():
-            data[key] = data_dict[key][cur_idxs]
-        batches.append(data)
-    return batches
+    """Reference utils.py:72-83: consecutive batch_size-row batches of every entry (the
+    last one shorter; one empty batch for an empty input), indexed by numpy index arrays."""
+    starts = range(0, max(input_total_size, 1), batch_size)
+    return [{key: val[np.arange(lo, min(lo + batch_size, input_total_size))] for key, val in data_dict.items()}
+            for lo in starts]
 
 
 def to_device(x, *, device):
