@@ -56,9 +56,13 @@ constexpr int C3_LDS_CAP = 160 * 1024;
 #define C3_DEPTH 8
 #endif
 constexpr int C3BM = 16;  // rays per workgroup
-#ifndef C3_GATHER_CPOL
-#define C3_GATHER_CPOL 2  // table rows are read once per step: non-temporal, spare the weights' L2 lines
-#endif
+// Cache policy of the table-row loads: non-temporal for tables larger than the MALL (rows
+// read once per step would evict the weight stream's L2 lines; config D's 4.1 GB table),
+// the default policy below it -- a MALL-resident table (config B's 102 MB) measured 0.8-1.0
+// us per step faster that way (profiles/r02/sweeps/gather_policy.log); config D with it 2.5
+// us slower
+constexpr int C3_CPOL_NT = 2;
+constexpr size_t C3_NT_TABLE_BYTES = (size_t)256 << 20;
 
 template <int H>
 struct L3 {
@@ -233,7 +237,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         for (int g = 0; g < GR; ++g) {
           const int q = q0 + C3_CT * g;
           const int r = (q < nch ? q : 0) / cpr, ch = (q < nch ? q : 0) % cpr;
-          v[g] = __builtin_amdgcn_raw_buffer_load_b128(rxp, (unsigned)(r * k_pad + col0 + ch * 8) * 2u, 0, C3_GATHER_CPOL);
+          v[g] = __builtin_amdgcn_raw_buffer_load_b128(rxp, (unsigned)(r * k_pad + col0 + ch * 8) * 2u, 0, 0);
         }
 #pragma unroll
         for (int g = 0; g < GR; ++g) {
@@ -245,9 +249,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       }
     };
-    auto gather_cols = [&](auto GRc, auto BIGc, int col0, int ncols) {
+    auto gather_cols = [&](auto GRc, auto BIGc, auto NTc, int col0, int ncols) {
       constexpr int GR = decltype(GRc)::value;
       constexpr bool BIG = decltype(BIGc)::value;
+      constexpr int CPOL = decltype(NTc)::value ? C3_CPOL_NT : 0;
       if (a.xpre != nullptr) {
         copy_cols(col0, ncols);
         return;
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               ev[g][i] = __builtin_bit_cast(u16x8, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src)));
             } else {
               const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + col0 + ch * 8) * 2u;
-              ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rt, off, 0, C3_GATHER_CPOL));
+              ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rt, off, 0, CPOL));
             }
           }
         }
@@ -366,8 +371,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       }
     } else {
       const int n0 = XC ? min(C3_KC, k_pad) : k_pad;
-      if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, 0, n0);
-      else gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, 0, n0);
+      if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, std::true_type{}, 0, n0);
+      else if (a.gather_nt || XC) gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, std::true_type{}, 0, n0);
+      else gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, std::false_type{}, 0, n0);
     }
     // every load issued so far has landed (the gather's data is in LDS and the fragment
     // prologue was issued before it; vmcnt is in order): an explicit wait here costs
@@ -448,8 +454,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           const int c = B.flags >> C3F_CHUNK_SHIFT;
           lbar();  // G1: every wave is done with the previous chunk (and the store wave with its X^T)
           const int nc = min(C3_KC, k_pad - c * C3_KC);
-          if (a.table_big) gather_cols(std::integral_constant<int, 2>{}, std::true_type{}, c * C3_KC, nc);
-          else gather_cols(std::integral_constant<int, 2>{}, std::false_type{}, c * C3_KC, nc);
+          // chunked tiles (k_pad > C3_KC) are the large tables: non-temporal rows
+          if (a.table_big) gather_cols(std::integral_constant<int, 2>{}, std::true_type{}, std::true_type{}, c * C3_KC, nc);
+          else gather_cols(std::integral_constant<int, 2>{}, std::false_type{}, std::true_type{}, c * C3_KC, nc);
           lbar();  // G2: chunk c in LDS
         }
         if (B.flags & C3F_SWAP) {
@@ -877,6 +884,7 @@ int launch3_typed(const Chain3Args& a, hipStream_t stream) {
 int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
   Chain3Args a = a_in;
   a.table_big = a.encoding == INF_ENC_NONE && a.num_vertices * (int64_t)a.k_pad * 2 >= ((int64_t)1 << 32);
+  a.gather_nt = a.encoding == INF_ENC_NONE && (size_t)a.num_vertices * (size_t)a.k_pad * 2 > C3_NT_TABLE_BYTES;
   INF_CHECK_ARG(chain3_supported(a.H, a.L, a.k_pad, a.rows), "chain3: unsupported shape");
   INF_CHECK_ARG(bm == C3BM, "chain3: tile height");
   INF_CHECK_ARG(a.rows % bm == 0 && a.rows >= bm, "chain3: rows must be a multiple of the tile height");

@@ -52,6 +52,7 @@ struct Chain3Args {
   // C3_KC: config D's k = 4096 tile is 128 KiB for 16 rays, above the LDS budget)
   int32_t kc, nchunk;
   int32_t table_big;  // table of 4 GiB or more: 64-bit row addresses (set by launch_chain3)
+  int32_t gather_nt;  // table rows read non-temporally: tables above the MALL (set by launch_chain3)
   // pre-gathered features (inf_prefetch_batch): row b of xpre [rows][k_pad] bf16 is ray b's
   // feature row, read instead of gathering three table rows (null: gather)
   const bf16* xpre;
