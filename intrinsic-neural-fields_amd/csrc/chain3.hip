@@ -773,7 +773,12 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           if (s0 + u < s_end) {
             const int t = 2 * (s0 + u) + (tg >> 1);
             const s16x4x8 o = {lo[u][0], lo[u][1], lo[u][2], lo[u][3], hi[u][0], hi[u][1], hi[u][2], hi[u][3]};
-            *reinterpret_cast<s16x4x8*>(d + (int64_t)t * 1024) = o;
+            // write-through (sc1): the dW GEMM reads these images in the next launch, and
+            // lines left dirty in the XCD L2s are written back at the kernel boundary
+            // (measured -0.8 us per step against plain stores; profiles/r02/sweeps/chain_images_sc1.log)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4, o), __builtin_amdgcn_make_buffer_rsrc(img, (short)0, 0x7FFFFFFF, 0x00020000),
+                (unsigned)(d - reinterpret_cast<char*>(img) + (int64_t)t * 1024), 0, 16);
           }
         }
       }
@@ -802,8 +807,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     }
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(d, (short)0, 0x7FFFFFFF, 0x00020000);
       for (int c = lane * 16; c < bytes; c += 64 * 16)
-        *reinterpret_cast<u16x8*>(d + c) = *reinterpret_cast<const u16x8*>(src + c);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(src + c), rd, (unsigned)c, 0, 16);
     };
 #ifdef C3_STREAM_ONLY
 #ifdef C3_STREAM_BARRIERS
