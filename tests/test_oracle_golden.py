@@ -224,3 +224,27 @@ def test_torch_cpu_gather_golden():
     d = golden("g1_gather_k64.npz")
     out = T.gather(torch.from_numpy(d["E"]), torch.from_numpy(d["vids"]), torch.from_numpy(d["bary"]))
     np.testing.assert_allclose(out.numpy(), d["out"], atol=1e-6)
+
+
+def test_bf16_oracle_rounding_and_profile():
+    """oracle.bf16_round is torch's round-to-nearest-even bfloat16; the bf16-mode oracle
+    (mlp_forward_bf16 / mlp_backward_bf16) stays within the bf16 profile of the fp32 oracle
+    on G2's config-A weights (the GPU bar against it is in test_gpu_kernels.py)."""
+    import torch
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(50000) * 4).astype(np.float32)
+    assert np.array_equal(O.bf16_round(x), torch.from_numpy(x).to(torch.bfloat16).float().numpy())
+    d = golden("g2_forward_A.npz")
+    w = {k[2:]: d[k] for k in d.files if k.startswith("w:")}
+    k, L, s, B, V = 64, 4, 2, 512, 400
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    p32, c32 = O.mlp_forward(w, O.gather(E, vids, bary), L, s)
+    p16, c16 = O.mlp_forward_bf16(w, O.gather_bf16(E, vids, bary), L, s)
+    assert np.abs(p16 - p32).max() < 2e-2
+    g32 = O.mlp_backward(w, c32, O.loss_grad(p32, rgb, "L2"), L, s)
+    g16 = O.mlp_backward_bf16(w, c16, O.loss_grad(p16, rgb, "L2"), L, s)
+    for n in O.layer_names(L, s):
+        assert np.abs(g16[n] - g32[n]).max() <= 0.25 * np.abs(g32[n]).max() + 1e-12, n
