@@ -226,6 +226,37 @@ def mlp_forward_bf16(w: dict, x_bf: np.ndarray, num_layers: int, skip: int):
     return p, cache
 
 
+def mlp_forward_bf16_projected(w: dict, E: np.ndarray, vids: np.ndarray, bary: np.ndarray, num_layers: int,
+                               skip: int) -> np.ndarray:
+    """The render slice over a projected table (csrc/rproj.hip, inf_project_table) in its
+    arithmetic: P = bf16(bf16(E) W_0^T), Q = bf16(bf16(E) W_y^T) per vertex (fp32
+    accumulation), each hit's pre-activations interpolated in fp32 (b0 r0 + b1 r1 + b2 r2)
+    and rounded to bf16 once more, then the hidden layers and the head as in
+    mlp_forward_bf16.  The same function as model.py:98-112, reassociated."""
+    e = bf16_round(E)
+    wb = {n: bf16_round(v) for n, v in w.items() if n.endswith("weight")}
+    b = bary.astype(np.float32)
+
+    def interp(T):
+        x = b[:, 0:1] * T[vids[:, 0]]
+        x = x + b[:, 1:2] * T[vids[:, 1]]
+        x = x + b[:, 2:3] * T[vids[:, 2]]
+        return bf16_round(x)
+
+    z0 = interp(bf16_round(e @ wb["layers.0.0.weight"].T))
+    zy = interp(bf16_round(e @ wb[f"layers.{skip}.Ly.weight"].T))
+    h = bf16_round(np.maximum(z0 + w["layers.0.0.bias"], 0))
+    for i in range(1, num_layers - 1):
+        if i == skip:
+            z = h @ wb[f"layers.{i}.Lx.weight"].T + zy + w[f"layers.{i}.Lx.bias"] + w[f"layers.{i}.Ly.bias"]
+        else:
+            z = h @ wb[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
+        h = bf16_round(np.maximum(z.astype(np.float32), 0))
+    i = num_layers - 1
+    z = h @ w[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
+    return _sigmoid(z.astype(np.float32)).astype(np.float32)
+
+
 def mlp_backward_bf16(w: dict, cache: dict, dpred: np.ndarray, num_layers: int, skip: int) -> dict:
     """Reverse mode in the bf16 perf mode's arithmetic: dZ of every hidden layer rounded to
     bf16 once (the MFMA operand of the dX chain and of the dW GEMM), bias gradients from the

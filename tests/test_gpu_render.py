@@ -315,3 +315,34 @@ def test_renderer_projection_cache_follows_weights(monkeypatch):
     monkeypatch.setenv("INF_RENDER_PROJECT", "0")
     c_gather = r.render_hits(vids, bary, hit)
     np.testing.assert_allclose(c, c_gather, atol=5e-3)
+
+
+@pytest.mark.parametrize("k,H,L,s,V,N", [(1024, 256, 8, 4, 20000, 8192), (64, 128, 4, 2, 2000, 4096)])
+def test_projected_render_matches_bf16_oracle(k, H, L, s, V, N):
+    """The projected-table render (inf_project_table + csrc/rproj.hip) against an independent
+    restatement of its bf16 arithmetic (oracle.mlp_forward_bf16_projected), not against the
+    builder's own feature-gather chain."""
+    import model as M
+    from inf_hip import runtime
+    rng = np.random.default_rng(41)
+    torch.manual_seed(0)
+    m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()
+    m.kernel_mode = "bf16"
+    w = {n: p.detach().cpu().numpy() for n, p in m.named_parameters()}
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (N, 3))
+    bary = rng.dirichlet([1, 1, 1], N).astype(np.float32)
+    src = runtime.RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                            None)
+    plan = m.hip_plan(min(N, 4096))
+    P = plan.project_table(src.table_for(plan))
+    pred = torch.empty((N, 3), device="cuda")
+    plan.forward(plan.make_batch(source=src, batch=N, projected=P), pred, save=False)
+    ref = O.mlp_forward_bf16_projected(w, E, vids, bary, L, s)
+    err = float(np.abs(pred.cpu().numpy() - ref).max())
+    print("projected vs bf16 oracle", k, H, L, s, err)
+    assert err < PROJ_BF16_ORACLE_RGB, err
+
+
+PROJ_BF16_ORACLE_RGB = 1e-3  # seen 1.7e-4 (k=1024, 8 x 256) / 5e-5 (k=64); profiles/r02/bf16_oracle_parity_render.log
