@@ -55,7 +55,9 @@ def parse():
     return ap.parse_args()
 
 
-def synthetic(V, k, N, seed, device):
+def synthetic(V, k, N, seed, device, ray_seed=None):
+    """The table from `seed` (the same on every rank: data-parallel replicas share one
+    eigenfunction table), the rays from `ray_seed` (each rank's own; default: `seed`)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     if V * k > (1 << 28):  # config D's 500k x 4096 table (8.2 GB fp32): drawn on the device
         gd = torch.Generator(device=device).manual_seed(seed)
@@ -64,6 +66,8 @@ def synthetic(V, k, N, seed, device):
     else:
         E = torch.randn((V, k), generator=g)
         E = E / (E.max(0, keepdim=True).values - E.min(0, keepdim=True).values)
+    if ray_seed is not None and ray_seed != seed:
+        g = torch.Generator(device="cpu").manual_seed(ray_seed)
     vids = torch.randint(0, V, (N, 3), generator=g)
     u = torch.rand((N, 3), generator=g).clamp_min(1e-12)
     bary = -torch.log(u)
@@ -83,11 +87,18 @@ def build_model(args, device):
 
 
 class Trainer:
-    """Graph-captured fused steps over one RaySource (one rank)."""
+    """Graph-captured fused steps over one RaySource (one rank).
 
-    def __init__(self, args, device, B, rank, world, nb=32):
+    shape (the data-parallel step, world > 1 or INF_BENCH_DP=1): "serial" -- fused step,
+    flat-gradient all-reduce, Adam, in order; "prefetch" -- the same with the next batch's
+    gather on a side stream beside the all-reduce (runtime.StepPipeline lead 0); "bucketed" --
+    the dW GEMM and gradient reduction in two halves (inf_train_step PART1 / PART2), bucket 1
+    all-reduced on a side stream while the second half runs (dp.DataParallelEpoch)."""
+
+    def __init__(self, args, device, B, rank, world, nb=32, shape="serial"):
         from inf_hip import runtime
         self.args, self.B, self.world = args, B, world
+        self.shape = shape
         self.model = build_model(args, device)
         rt = self.model.hip_runtime()
         rt.ensure_optimizer_arenas()
@@ -96,7 +107,8 @@ class Trainer:
         self.plan.set_lr(1e-4)
         self.nb = nb
         self.N = self.nb * B
-        E, vids, bary, rgb = synthetic(args.verts, args.k, self.N, seed=1 + rank, device=device)
+        # one table on every rank (replicas share E), each rank its own rays
+        E, vids, bary, rgb = synthetic(args.verts, args.k, self.N, seed=1, device=device, ray_seed=1 + rank)
         self.src = runtime.RaySource(E, vids, bary, rgb)
         self.perm = torch.randperm(self.N, device=device)
         self.batch = self.plan.make_batch(source=self.src, ray_idx=self.perm, offset=0, batch=B,
@@ -107,13 +119,11 @@ class Trainer:
         # INF_BENCH_DP=1 runs it at world 1 too (rehearses RCCL capture on a one-GPU box)
         self.dp = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
         self.ar_in_graph = False
-        # INF_PREFETCH=1: the next batch's gather on a side stream beside the gradient
-        # all-reduce (runtime.StepPipeline lead 0).  Off by default: on one MI355X the
-        # data-parallel step takes 94.2 us with it vs 77.4 us without (the gather and two
-        # cross-queue signals land on the critical path when the all-reduce is empty); it is
-        # meant for N > 1, where the all-reduce is long, and is unmeasured there
+        # shape "prefetch" (or INF_PREFETCH=1 on the single-GPU step): the next batch's gather
+        # on a side stream beside the gradient all-reduce (runtime.StepPipeline lead 0)
         self.pipe = runtime.StepPipeline(self.plan, self.batch, lead=int(os.environ.get("INF_PREFETCH_LEAD", "0")))
-        want = os.environ.get("INF_PREFETCH", "0") != "0"
+        self.side = torch.cuda.Stream(device=device)
+        want = shape == "prefetch" if self.dp else os.environ.get("INF_PREFETCH", "0") != "0"
         self.prefetch = want and self.pipe.start()
 
     # steps per replayed graph (divides nb)
@@ -126,8 +136,27 @@ class Trainer:
         else:
             self.plan.train_step(self.batch, None, apply_adam=False, xslot=xslot)
 
+    def _bucketed_step(self):
+        plan, dist = self.plan, torch.distributed
+        split = plan.grad_split()
+        plan.train_step(self.batch, None, apply_adam=False, part=1)
+        main = torch.cuda.current_stream()
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            if dist.is_initialized():
+                dist.all_reduce(plan.grads[split:])
+        plan.train_step(self.batch, None, apply_adam=False, part=2)
+        main.wait_stream(self.side)
+        if dist.is_initialized():
+            dist.all_reduce(plan.grads[:split])
+        plan.adam(0, 0.0, advance=True)
+
     def _steps(self, n):
-        """n steps: pipelined (side-stream prefetch of the next batch) or plain."""
+        """n steps: pipelined (side-stream prefetch of the next batch), bucketed or plain."""
+        if self.dp and self.shape == "bucketed":
+            for _ in range(n):
+                self._bucketed_step()
+            return
         tail = self._dp_tail if self.dp else None
         if self.prefetch:
             self.pipe.run(n, self._launch, first_slot=self.i % 2, tail_fn=tail)
@@ -206,7 +235,7 @@ class Trainer:
         self.i += 1
 
     def step(self):
-        if self.graphs is None or self.prefetch:
+        if self.graphs is None or self.prefetch or (self.dp and self.shape == "bucketed"):
             return self.step_eager()
         self._wrap()
         g1, g2, _ = self.graphs
@@ -250,6 +279,51 @@ def time_steps(tr, steps, warmup, world):
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t[0]) / steps, float(t[1]) / steps
+
+
+def time_allreduce(tr, steps, warmup, world):
+    """The flat-gradient all-reduce alone (P fp32, 3.68 MB at config B), issued as the step
+    issues it: captured into a graph of GRAPH_STEPS collectives over RCCL (eager over gloo),
+    barrier + synchronize around the timed region, max over ranks."""
+    dist = torch.distributed
+    grads = tr.plan.grads
+    graph = None
+    if dist.is_initialized() and dist.get_backend() != "gloo":
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            dist.all_reduce(grads)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=s):
+                for _ in range(tr.GRAPH_STEPS):
+                    dist.all_reduce(grads)
+        torch.cuda.current_stream().wait_stream(s)
+
+    def run(n):
+        while n > 0:
+            if graph is not None and n >= tr.GRAPH_STEPS:
+                graph.replay()
+                n -= tr.GRAPH_STEPS
+            else:
+                if dist.is_initialized():
+                    dist.all_reduce(grads)
+                n -= 1
+
+    run(warmup)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run(steps)
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([e0.elapsed_time(e1) / steps], device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), {"bytes": grads.numel() * 4, "in_graph": graph is not None}
 
 
 def time_stage(plan, stage, reps=20, batch=None, layer=0):
@@ -755,9 +829,39 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    tr = Trainer(args, device, args.batch, rank, world)
-    tr.capture()
-    ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
+    dp_mode = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
+    dp_shapes = None
+    if dp_mode:
+        # the data-parallel step in each of its shapes (dp.py picks the fastest the same way),
+        # and the gradient all-reduce alone; `value` is the fastest shape's
+        dp_shapes = {}
+        best = None
+        for shape in [x for x in os.environ.get("INF_DP_SHAPES", "serial,prefetch,bucketed").split(",") if x]:
+            tr = Trainer(args, device, args.batch, rank, world, shape=shape)
+            tr.capture()
+            ms_s, wall_s = time_steps(tr, args.steps, args.warmup, world)
+            dp_shapes[shape] = {"ms_per_step": ms_s, "value": world * args.batch / (ms_s * 1e-3),
+                                "allreduce_in_graph": tr.ar_in_graph, "prefetch_active": bool(tr.prefetch)}
+            if best is None or ms_s < best[1]:
+                if best is not None:
+                    del best[0]
+                best = [tr, ms_s, wall_s, shape]
+            else:
+                del tr
+            torch.cuda.empty_cache()
+        tr, ms, wall_ms, chosen = best[0], best[1], best[2], best[3]
+        ar_ms, ar_info = time_allreduce(tr, args.steps, args.warmup, world)
+        dp_shapes["allreduce_alone_ms"] = ar_ms
+        dp_shapes["allreduce"] = ar_info
+        dp_shapes["chosen"] = chosen
+        dp_shapes["note"] = ("serial: fused step -> flat-gradient all-reduce -> Adam in order; prefetch: the next "
+                             "batch's gather on a side stream beside the all-reduce; bucketed: the dW GEMM in two "
+                             "halves, bucket 1 all-reduced beside the second; value = the fastest shape (dp.py's "
+                             "autotune picks the same way)")
+    else:
+        tr = Trainer(args, device, args.batch, rank, world)
+        tr.capture()
+        ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
     tr_ar_in_graph = tr.ar_in_graph
     value = world * args.batch / (ms * 1e-3)
 
@@ -909,6 +1013,7 @@ def main():
                                            weight_bytes=2 if args.mode == "bf16" else 4),
             "stages": stage_lines,
             "host_wall_ms_per_step": wall_ms,
+            "data_parallel": dp_shapes,
             "large_batch": extra,
             "config_D": config_d,
             "secondary": secondary,

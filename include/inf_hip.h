@@ -102,6 +102,10 @@ typedef struct inf_batch {
   int32_t enc_k;         /* embedding size k (RFF/FF)                                  */
   const float* enc_proj; /* RFF: B [3][enc_k]; FF: freq_bands [enc_k]                  */
   int32_t enc_include_input; /* append x (embed_include_input)                        */
+  int64_t num_source_rays; /* rows of vids / bary / rgb (the ray arrays ray_idx indexes);   */
+                         /* a ray whose permutation entry names a row outside            */
+                         /* [0, num_source_rays) reads as a zero feature row and a zero   */
+                         /* target instead of being loaded.  0 = unchecked.                */
 } inf_batch;
 
 /* Device-resident step state (lets a captured HIP graph replay a whole epoch). */
@@ -119,16 +123,20 @@ typedef struct inf_ctrl {
 /* ---- library ----------------------------------------------------------------- */
 const char* inf_last_error(void);
 int inf_abi_version(void);
+/* "<16 hex digits of sha256> <file> <file> ...": the hash of the concatenated bytes of the
+ * listed source / header files (paths relative to csrc/) the library was linked from. */
+const char* inf_build_id(void);
 
 /* ---- gather: mesh.get_k_eigenfunc_vec_vals (mesh.py:313-324) and its chunked
  *      form get_k_eigenfunc_vec_vals_batched (mesh.py:327-339), with the loader's
  *      index-select fused in (ray_dataloader.py:122-129).
  *      out[b][j] = bary[r][0]*E[v0][j] + bary[r][1]*E[v1][j] + bary[r][2]*E[v2][j],
  *      r = idx ? idx[idx_offset+b] : idx_offset+b, j < k; columns k..ld_out-1 and rows
- *      batch..rows_out-1 are written as zero.                                        */
+ *      batch..rows_out-1 are written as zero, and so are rays whose r lies outside
+ *      [0, num_source_rays) (the rows of vids / bary; 0 = unchecked).                */
 int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, int64_t table_ld,
                const void* vids, int vid_dtype, const float* bary,
-               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
+               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch, int64_t num_source_rays,
                void* out, int out_dtype, int64_t ld_out, int rows_out,
                void* out_t, int64_t ld_out_t, inf_stream_t stream);
 
@@ -138,7 +146,7 @@ int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, 
  *      out[b][j], j < in_dim (3, 2k(+3) or 6k(+3)); columns in_dim..ld_out-1 and rows
  *      batch..rows_out-1 are written as zero.                                        */
 int inf_encode(const float* table, int64_t num_rows, const void* vids, int vid_dtype, const float* bary,
-               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
+               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch, int64_t num_source_rays,
                int encoding, int enc_k, const float* enc_proj, int include_input,
                void* out, int out_dtype, int64_t ld_out, int rows_out, inf_stream_t stream);
 /* in_dim of an encoding (3, 2k + 3*inc, 6k + 3*inc); -1 for a bad encoding */
@@ -221,7 +229,16 @@ int inf_backward(inf_plan* plan, const float* dpred, float* grads, inf_stream_t 
  * at the end of the step (a graph-replayed epoch; same as a following
  * inf_ctrl_advance).  pred may be NULL.  The step's loss / SSE sums are stored in
  * ctrl->loss_sum / sse_sum and added to the epoch sums. */
-enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2, INF_STEP_XSLOT0 = 4, INF_STEP_XSLOT1 = 8 };
+/* INF_STEP_PART1 / PART2 (gradient-only steps; not with ADAM / ADVANCE): the step split at
+ * inf_plan_grad_split for a bucketed data-parallel all-reduce.  PART1 runs the forward,
+ * loss and backward chain, the weight-gradient GEMM of the matrices in bucket 1 (arena
+ * [grad_split, P): the skip layer's Ly and every layer after it) and the reduction of
+ * bucket 1 (with every bias and the step's loss sums) into `grads`; PART2 (same batch)
+ * the GEMM and reduction of bucket 2 (arena [0, grad_split)).  The caller all-reduces
+ * bucket 1 while PART2 runs.  Where the step does not take the fused chain, PART1
+ * reduces the whole gradient and PART2 does nothing. */
+enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2, INF_STEP_XSLOT0 = 4, INF_STEP_XSLOT1 = 8, INF_STEP_PART1 = 16,
+       INF_STEP_PART2 = 32 };
 int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int flags,
                    inf_stream_t stream);
 
@@ -315,6 +332,10 @@ int inf_plan_last_step_path(const inf_plan* plan);
  * projected table across frames).  -1 once such a launch was captured into a graph:
  * replays are invisible to the host, so nothing derived may then be cached. */
 int64_t inf_plan_weight_generation(const inf_plan* plan);
+
+/* First float of gradient bucket 1 in the parameter arena (the skip layer's Ly weight;
+ * INF_STEP_PART1 / PART2): bucket 1 = [split, P), bucket 2 = [0, split). */
+int64_t inf_plan_grad_split(const inf_plan* plan);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

@@ -202,8 +202,8 @@ __global__ __launch_bounds__((BM >= 64 ? BM / 64 : 1) * 256) void chain_kernel(c
                                                       : (const void*)((const int32_t*)a.ray_idx + offset + b);
         (void)ip;
         if (a.ray_idx == nullptr || GOK(ip, 4, 10)) {
-          const int64_t rr = ray_row(a.ray_idx, a.idx_dtype, offset, b);
-          if (GOK(a.rgb + rr * 3 + i % 3, 4, 11)) t = a.rgb[rr * 3 + i % 3];
+          const int64_t rr = source_row(a.ray_idx, a.idx_dtype, offset, b, a.num_rays, a.num_src);
+          if (rr >= 0 && GOK(a.rgb + rr * 3 + i % 3, 4, 11)) t = a.rgb[rr * 3 + i % 3];
         }
       }
       tgs[i] = t;

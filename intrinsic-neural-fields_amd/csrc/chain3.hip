@@ -177,8 +177,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const int b = b0 + rl;
       int v = 0, ok = 0;
       float w = 0.f;
-      if (b < a.batch && ray_in_range(offset, b, a.num_rays)) {
-        const int64_t rr = ray_row(a.ray_idx, a.idx_dtype, offset, b);
+      const int64_t rr = b < a.batch ? source_row(a.ray_idx, a.idx_dtype, offset, b, a.num_rays, a.num_src) : -1;
+      if (rr >= 0) {
         const int64_t e = vid_at(a.vids, a.vid_dtype, 3 * rr + i);
         // an out-of-range vertex id reads as a zero feature row (gather.hip)
         ok = (uint64_t)e < (uint64_t)a.num_vertices;
@@ -198,9 +198,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const int rl = tid / 3, c = tid % 3;
       const int b = b0 + rl;
       float x = 0.f;
-      const bool live = b < a.batch && ray_in_range(offset, b, a.num_rays);
+      const int64_t rr = b < a.batch ? source_row(a.ray_idx, a.idx_dtype, offset, b, a.num_rays, a.num_src) : -1;
+      const bool live = rr >= 0;
       if (live) {
-        const int64_t rr = ray_row(a.ray_idx, a.idx_dtype, offset, b);
         const int64_t v0 = vid_at(a.vids, a.vid_dtype, 3 * rr), v1 = vid_at(a.vids, a.vid_dtype, 3 * rr + 1),
                       v2 = vid_at(a.vids, a.vid_dtype, 3 * rr + 2);
         const float w0 = a.bary[3 * rr], w1 = a.bary[3 * rr + 1], w2 = a.bary[3 * rr + 2];
@@ -731,8 +731,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
       const int bt = b0 + lane / 3;
       float tt = 0.f;
-      if (lane < BM * 3 && bt < a.batch && ray_in_range(offset, bt, a.num_rays))
-        tt = a.rgb[ray_row(a.ray_idx, a.idx_dtype, offset, bt) * 3 + lane % 3];
+      const int64_t trow =
+          lane < BM * 3 && bt < a.batch ? source_row(a.ray_idx, a.idx_dtype, offset, bt, a.num_rays, a.num_src) : -1;
+      if (trow >= 0) tt = a.rgb[trow * 3 + lane % 3];
       if (lane < BM * 3) tgs[lane] = tt;
     }
     // ---- fragment images for the dW GEMM (lgemm.hpp: rows = features, k = rays) ----------

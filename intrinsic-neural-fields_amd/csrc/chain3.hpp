@@ -42,6 +42,7 @@ struct Chain3Args {
   int32_t idx_dtype;
   int64_t idx_offset;
   int64_t num_rays;  // bound on idx_offset + b (0 = unchecked)
+  int64_t num_src;   // rows of vids / bary / rgb (inf_batch::num_source_rays; 0 = unchecked)
   int32_t offset_from_ctrl;
   // extrinsic front-end (INF_ENC_*, model.py:33-40): the feature tile is the encoding of
   // the rays' interpolated positions pos[V][3] (gather.hip encode_kernel's numerics)

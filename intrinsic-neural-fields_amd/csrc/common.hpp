@@ -67,6 +67,19 @@ __device__ __forceinline__ int64_t ray_row(const void* ray_idx, int idx_dtype, i
   return reinterpret_cast<const int32_t*>(ray_idx)[offset + b];
 }
 
+// Source row of ray b of a batch that starts at entry `offset` of ray_idx (or of the rays
+// themselves when ray_idx is null), or -1 when the position offset + b is past num_rays or
+// the row it names lies outside [0, num_src) (inf_batch::num_source_rays; 0 = unchecked).
+// Such a ray reads as a zero feature row and a zero target: a bad permutation entry is
+// never turned into a load outside vids / bary / rgb.
+__device__ __forceinline__ int64_t source_row(const void* ray_idx, int idx_dtype, int64_t offset, int b,
+                                              int64_t num_rays, int64_t num_src) {
+  if (!ray_in_range(offset, b, num_rays)) return -1;
+  const int64_t r = ray_row(ray_idx, idx_dtype, offset, b);
+  if (num_src > 0 && (uint64_t)r >= (uint64_t)num_src) return -1;
+  return r;
+}
+
 __device__ __forceinline__ int64_t vid_at(const void* vids, int vid_dtype, int64_t i) {
   if (vid_dtype == INF_DTYPE_I64) return reinterpret_cast<const int64_t*>(vids)[i];
   return reinterpret_cast<const int32_t*>(vids)[i];
@@ -101,11 +114,13 @@ __device__ __forceinline__ void fast_sincos(float e, float* s, float* c) {
 int encoded_dim(int enc, int k, int inc);
 int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype, const float* bary,
                   const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_batch_index,
-                  int64_t num_rays, int batch, int enc, int enc_k, const float* proj, int inc, void* out,
-                  int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream);
+                  int64_t num_rays, int64_t num_src, int batch, int enc, int enc_k, const float* proj, int inc,
+                  void* out, int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t,
+                  hipStream_t stream);
 int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
                   int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
-                  const int32_t* ctrl_batch_index, int64_t num_rays, int batch, void* out, int out_dtype,
+                  const int32_t* ctrl_batch_index, int64_t num_rays, int64_t num_src, int batch, void* out,
+                  int out_dtype,
                   int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream);
 
 // Pack fp32 features [B][ld_in] into the GEMM dtype [rows_out][ld_out] (+ transposed copy).

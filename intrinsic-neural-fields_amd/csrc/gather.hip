@@ -121,7 +121,7 @@ template <typename TabT, typename OutT, bool VEC>
 __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
     const TabT* __restrict__ table, int64_t V, int k, int64_t table_ld, const void* __restrict__ vids,
     int vid_dtype, const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype,
-    int64_t idx_offset, const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int batch,
+    int64_t idx_offset, const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int64_t num_src, int batch,
     OutT* __restrict__ out,
     int64_t ld_out, int rows_out, OutT* __restrict__ out_t, int64_t ld_out_t) {
   __shared__ float tile[GT_COLS][GT_ROWS + 1];
@@ -139,8 +139,8 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 
-  if (b < batch && ray_in_range(offset, b, num_rays)) {
-    const int64_t row = ray_row(ray_idx, idx_dtype, offset, b);
+  const int64_t row = b < batch ? source_row(ray_idx, idx_dtype, offset, b, num_rays, num_src) : -1;
+  if (row >= 0) {
     const float w0 = bary[3 * row + 0];
     const float w1 = bary[3 * row + 1];
     const float w2 = bary[3 * row + 2];
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
 template <typename TabT, typename OutT>
 int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const void* vids, int vid_dtype,
                  const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_bi,
-                 int64_t num_rays, int batch, void* out, int64_t ld_out, int rows_out, void* out_t,
+                 int64_t num_rays, int64_t num_src, int batch, void* out, int64_t ld_out, int rows_out, void* out_t,
                  int64_t ld_out_t, hipStream_t stream) {
   dim3 grid((unsigned)ceil_div(rows_out, GT_ROWS), (unsigned)ceil_div(ld_out, GT_COLS));
   const bool vec = (k % 16 == 0) && (table_ld % 16 == 0) && (ld_out % 16 == 0) &&
@@ -188,11 +188,11 @@ int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const vo
   if (vec) {
     gather_kernel<TabT, OutT, true><<<grid, GT_THREADS, 0, stream>>>(
         (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, num_rays,
-        batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
+        num_src, batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
   } else {
     gather_kernel<TabT, OutT, false><<<grid, GT_THREADS, 0, stream>>>(
         (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, num_rays,
-        batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
+        num_src, batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);
   }
   INF_LAUNCH_CHECK();
   return INF_OK;
@@ -202,8 +202,8 @@ int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const vo
 
 int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t table_ld, const void* vids,
                   int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset,
-                  const int32_t* ctrl_batch_index, int64_t num_rays, int batch, void* out, int out_dtype,
-                  int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
+                  const int32_t* ctrl_batch_index, int64_t num_rays, int64_t num_src, int batch, void* out,
+                  int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
   INF_CHECK_ARG(table != nullptr && vids != nullptr && bary != nullptr, "gather: null input");
   INF_CHECK_ARG(k > 0 && table_ld >= k && V > 0, "gather: bad table shape");
   INF_CHECK_ARG(batch >= 0 && rows_out >= batch && ld_out >= k, "gather: bad output shape");
@@ -218,18 +218,18 @@ int launch_gather(const void* table, int table_dtype, int64_t V, int k, int64_t 
   INF_CHECK_ARG(of || out_dtype == INF_DTYPE_BF16, "gather: out dtype must be f32/bf16");
   if (tf && of)
     return launch_typed<float, float>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                      ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                      ctrl_batch_index, num_rays, num_src, batch, out, ld_out, rows_out, out_t, ld_out_t,
                                       stream);
   if (tf && !of)
     return launch_typed<float, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                     ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                     ctrl_batch_index, num_rays, num_src, batch, out, ld_out, rows_out, out_t, ld_out_t,
                                       stream);
   if (!tf && of)
     return launch_typed<bf16, float>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                     ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                     ctrl_batch_index, num_rays, num_src, batch, out, ld_out, rows_out, out_t, ld_out_t,
                                       stream);
   return launch_typed<bf16, bf16>(table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset,
-                                  ctrl_batch_index, num_rays, batch, out, ld_out, rows_out, out_t, ld_out_t,
+                                  ctrl_batch_index, num_rays, num_src, batch, out, ld_out, rows_out, out_t, ld_out_t,
                                       stream);
 }
 
@@ -249,7 +249,7 @@ template <typename OutT, bool VEC>
 __global__ __launch_bounds__(GT_THREADS) void encode_kernel(
     const float* __restrict__ table, int64_t V, const void* __restrict__ vids, int vid_dtype,
     const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype, int64_t idx_offset,
-    const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int batch, int enc, int ek,
+    const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int64_t num_src, int batch, int enc, int ek,
     const float* __restrict__ proj, int in_dim, int ne, OutT* __restrict__ out, int64_t ld_out, int rows_out,
     OutT* __restrict__ out_t, int64_t ld_out_t) {
   __shared__ float tile[GT_COLS][GT_ROWS + 1];
@@ -264,8 +264,8 @@ __global__ __launch_bounds__(GT_THREADS) void encode_kernel(
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  if (b < batch && c0 < in_dim && ray_in_range(offset, b, num_rays)) {
-    const int64_t row = ray_row(ray_idx, idx_dtype, offset, b);
+  const int64_t row = b < batch && c0 < in_dim ? source_row(ray_idx, idx_dtype, offset, b, num_rays, num_src) : -1;
+  if (row >= 0) {
     float x[3] = {0.f, 0.f, 0.f};
     if (vids == nullptr) {
       if ((uint64_t)row < (uint64_t)V) {
@@ -321,8 +321,9 @@ int encoded_dim(int enc, int k, int inc) {
 
 int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype, const float* bary,
                   const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_batch_index,
-                  int64_t num_rays, int batch, int enc, int enc_k, const float* proj, int inc, void* out,
-                  int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t, hipStream_t stream) {
+                  int64_t num_rays, int64_t num_src, int batch, int enc, int enc_k, const float* proj, int inc,
+                  void* out, int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t,
+                  hipStream_t stream) {
   const int in_dim = encoded_dim(enc, enc_k, inc);
   INF_CHECK_ARG(in_dim > 0, "encode: bad encoding / k / include_input");
   INF_CHECK_ARG(table != nullptr && V > 0, "encode: null or empty vertex table");
@@ -342,7 +343,7 @@ int launch_encode(const float* table, int64_t V, const void* vids, int vid_dtype
                    ((uintptr_t)out_t % 16 == 0);
 #define INF_ENC_LAUNCH(T, V)                                                                                      \
   encode_kernel<T, V><<<grid, GT_THREADS, 0, stream>>>(table, V_rows, vids, vid_dtype, bary, ray_idx, idx_dtype,   \
-                                                       idx_offset, ctrl_batch_index, num_rays, batch, enc, enc_k, \
+                                                       idx_offset, ctrl_batch_index, num_rays, num_src, batch, enc, enc_k, \
                                                        proj, in_dim, ne, (T*)out, ld_out, rows_out, (T*)out_t,    \
                                                        ld_out_t)
   const int64_t V_rows = V;

@@ -33,9 +33,9 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadFwdArgs a) {
   int64_t offset = a.idx_offset;
   if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
   float tgt = 0.f;
-  if (a.rgb != nullptr && valid && lane16 < 3 && ray_in_range(offset, b, a.num_rays)) {
-    const int64_t row = ray_row(a.ray_idx, a.idx_dtype, offset, b);
-    tgt = a.rgb[row * 3 + lane16];
+  if (a.rgb != nullptr && valid && lane16 < 3) {
+    const int64_t row = source_row(a.ray_idx, a.idx_dtype, offset, b, a.num_rays, a.num_src);
+    if (row >= 0) tgt = a.rgb[row * 3 + lane16];
   }
   float hv[EPL];
   const T* hrow = reinterpret_cast<const T*>(a.h) + (int64_t)(in_rows ? b : 0) * a.ldh + lane16 * EPL;

@@ -23,6 +23,7 @@ struct HeadFwdArgs {
   int32_t idx_dtype;
   int64_t idx_offset;
   int64_t num_rays;     // bound on idx_offset + b (0 = unchecked)
+  int64_t num_src;   // rows of vids / bary / rgb (inf_batch::num_source_rays; 0 = unchecked)
   int32_t offset_from_ctrl;
   int32_t loss;
   float inv_count;      // 1 / (elements of the loss mean)

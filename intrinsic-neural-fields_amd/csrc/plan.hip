@@ -59,6 +59,12 @@ struct inf_plan {
   int k_pad = 0, H = 0, L = 0, s = 0, mode = 0;
   int64_t esz = 4;
   int dw_splits = 1;
+  // bucketed data-parallel steps (INF_STEP_PART1 / PART2): the dW GEMM runs as two launches
+  // of half the matrices each, with bucket_splits split-K partials (2 x dw_splits: the same
+  // blocks per launch as the single launch), reduced through their own seg table
+  int bucket_splits = 1;
+  int64_t grad_split = 0;  // bucket 1 = arena [grad_split, P) (Ly and the layers after it)
+  int n_items_b1 = 0;      // update work items of bucket 1 (listed first), end-of-step item included
   int train_unit = 128;
   int bp_max = 0;
   int grid_hb = 1;
@@ -67,7 +73,7 @@ struct inf_plan {
   int64_t shadow_bytes = 0;
 
   // workspace layout (byte offsets)
-  int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_ws_end = 0;
+  int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_tables_b = 0, o_ws_end = 0;
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
   int n_aux_items = 0;
@@ -226,6 +232,13 @@ int build_layout(inf_plan* p) {
     if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 128) S = want;
   }
   p->dw_splits = S;
+  p->bucket_splits = S;
+  if (d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && 2 * S <= 16 && (mb / (2 * S)) % 256 == 0)
+    p->bucket_splits = 2 * S;
+  if (const char* e = std::getenv("INF_BUCKET_SPLITS")) {  // = dw_splits: bitwise the unbucketed step
+    const int want = std::atoi(e);
+    if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 256) p->bucket_splits = want;
+  }
   p->train_unit = (int)std::max<int64_t>(128, (int64_t)S * 64);
   p->bp_max = (int)round_up(p->max_batch, p->train_unit);
   p->grid_hb = (int)std::min<int64_t>(256, p->bp_max / HEAD_BWD_RAYS);
@@ -257,7 +270,7 @@ int build_layout(inf_plan* p) {
   p->o_slab.assign(p->segs.size(), 0);
   for (size_t i = 0; i < p->segs.size(); ++i) {
     const auto& g = p->segs[i];
-    if (g.gemm) p->o_slab[i] = take((int64_t)S * g.R * g.c_pad * 4);
+    if (g.gemm) p->o_slab[i] = take((int64_t)std::max(S, p->bucket_splits) * g.R * g.c_pad * 4);
   }
   p->o_hw = take(max_parts * 3 * H * 4);
   p->o_hb = take(max_parts * 3 * 4);
@@ -268,6 +281,7 @@ int build_layout(inf_plan* p) {
   for (const auto& g : p->segs) nitems += g.gemm ? ceil_div(g.R, ADAM_TILE_R) * ceil_div(g.C, ADAM_TILE_C) : ceil_div((int64_t)g.R * g.C, ADAM_VEC);
   p->table_bytes = align_up((int64_t)p->segs.size() * sizeof(AdamSeg)) + align_up(nitems * sizeof(AdamItem));
   p->o_tables = take(p->table_bytes);
+  p->o_tables_b = take(align_up((int64_t)p->segs.size() * sizeof(AdamSeg)));
   p->o_aux_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
   int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
   for (const auto& g : p->segs)
@@ -317,14 +331,16 @@ int run_input(inf_plan* p, const inf_batch* b, int Bp, bool transposed, hipStrea
                   "encoding width does not match the model's in_dim");
     return launch_encode((const float*)b->table, b->num_vertices, b->vids, b->vid_dtype, b->bary, b->ray_idx,
                          b->idx_dtype, b->idx_offset, b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr,
-                         b->num_rays, b->batch, b->encoding, b->enc_k, b->enc_proj, b->enc_include_input, x0,
+                         b->num_rays, b->num_source_rays, b->batch, b->encoding, b->enc_k, b->enc_proj,
+                         b->enc_include_input, x0,
                          dtype_of(p), p->k_pad, Bp, x0t, Bp, st);
   }
   if (b->table != nullptr) {
     const int64_t k_table = p->k_pad;  // device tables are packed with k_pad zero-filled columns
     return launch_gather(b->table, b->table_dtype, b->num_vertices, (int)k_table, k_table, b->vids, b->vid_dtype,
                          b->bary, b->ray_idx, b->idx_dtype, b->idx_offset,
-                         b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr, b->num_rays, b->batch, x0, dtype_of(p),
+                         b->offset_from_ctrl ? &p->ctrl->batch_index : nullptr, b->num_rays, b->num_source_rays,
+                         b->batch, x0, dtype_of(p),
                          p->k_pad, Bp, x0t, Bp, st);
   }
   INF_CHECK_ARG(b->features != nullptr, "batch has neither a table nor features");
@@ -385,7 +401,8 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
   return INF_OK;
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr);
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr,
+                     int bucket = 0);
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
@@ -423,9 +440,12 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
 
 // chain (2, 3): Y^T / dZ^T were written by the fused chain in its 16-ray blocked layout;
 // with the register-streamed chain (3) Y_0^T comes plain from the input GEMM
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse) {
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket) {
   const int H = p->H, s = p->s;
   if (chain == 3) {
+    // bucket 1 / 2: only the matrices of arena [grad_split, P) / [0, grad_split), with
+    // bucket_splits partials each (the data-parallel bucketed step)
+    const int splits = bucket ? p->bucket_splits : p->dw_splits;
     // register-streamed chain: X^T, Y_l^T and dZ_l^T are fragment images (chain3.hip); one
     // lgemm launch computes every dW^T tile into the split-K slabs the update launch reduces
     LgemmBatch lb;
@@ -434,6 +454,7 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     for (size_t i = 0; i < p->segs.size(); ++i) {
       const ParamSeg& g = p->segs[i];
       if (!g.gemm) continue;
+      if ((bucket == 1 && g.off < p->grad_split) || (bucket == 2 && g.off >= p->grad_split)) continue;
       INF_CHECK_ARG(lb.nprob < LGEMM_MAX_PROBLEMS, "lgemm: too many weight matrices");
       LgemmProblem& q = lb.p[lb.nprob++];
       q.adam_seg = (int32_t)i;
@@ -451,7 +472,7 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       q.M = g.c_pad;
       q.N = g.R;
       q.K = Bp;
-      q.splits = p->dw_splits;
+      q.splits = splits;
       q.slab = p->W<float>(p->o_slab[i]);
       q.slab_ld = g.c_pad;
       q.slab_stride = (int64_t)g.R * g.c_pad;
@@ -563,6 +584,15 @@ int step_shadow_mode(const inf_plan* p, int chain) {
   return chain == 3 && p->mode == INF_MODE_BF16 && std::getenv("INF_EAGER_SHADOWS") == nullptr ? 2 : 1;
 }
 
+// The seg table of the bucketed steps: the matrices' gradients summed over bucket_splits
+// split-K partials.
+std::vector<AdamSeg> bucket_segs(const inf_plan* p) {
+  std::vector<AdamSeg> t = p->adam_segs;
+  for (auto& a : t)
+    if (a.matrix) a.nslab = p->bucket_splits;
+  return t;
+}
+
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
   const int parts = chain == 3 ? Bp / chain3_bm(Bp) : chain ? Bp / chain_partial_rows(chain_bm(Bp)) : Bp / 64;
@@ -585,6 +615,8 @@ int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
   // host vector may change afterwards.
   INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
                              hipMemcpyHostToDevice, st));
+  const std::vector<AdamSeg> tb = bucket_segs(p);
+  INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables_b, tb.data(), tb.size() * sizeof(AdamSeg), hipMemcpyHostToDevice, st));
   return INF_OK;
 }
 
@@ -615,6 +647,7 @@ int head_forward(inf_plan* p, const inf_batch* b, int Bp, float* pred, bool loss
     a.idx_dtype = b->idx_dtype;
     a.idx_offset = b->idx_offset;
     a.num_rays = b->num_rays;
+    a.num_src = b->num_source_rays;
     a.offset_from_ctrl = b->offset_from_ctrl;
     a.loss = b->loss >= 0 ? b->loss : p->d.loss;
     INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
@@ -740,6 +773,7 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
     a.idx_dtype = b->idx_dtype;
     a.idx_offset = b->idx_offset;
     a.num_rays = b->num_rays;
+    a.num_src = b->num_source_rays;
     a.offset_from_ctrl = b->offset_from_ctrl;
     a.loss = b->loss >= 0 ? b->loss : p->d.loss;
     INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
@@ -804,6 +838,7 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.idx_dtype = b->idx_dtype;
   a.idx_offset = b->idx_offset;
   a.num_rays = b->num_rays;
+  a.num_src = b->num_source_rays;
   a.offset_from_ctrl = b->offset_from_ctrl;
   auto img = [&](const ParamSeg* w, bool fwd) -> const bf16* {
     const int64_t off = fwd ? w->f_off : w->ft_off;
@@ -913,6 +948,7 @@ int run_rchain(inf_plan* p, const inf_batch* b, float* pred, const int64_t* hit,
   a.idx_dtype = b->idx_dtype;
   a.idx_offset = b->idx_offset;
   a.num_rays = b->num_rays;
+  a.num_src = b->num_source_rays;
   a.nchunk = (int)ceil_div(p->k_pad, RC_KC);
   auto add = [&](const ParamSeg* w, int kb0, int a_x, int ak0, int phase, int last, int flags) -> int {
     INF_CHECK_ARG(w != nullptr && w->f_off >= 0, "rchain: fragment image missing");
@@ -1006,22 +1042,23 @@ int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool l
 extern "C" {
 
 const char* inf_last_error(void) { return g_last_error.c_str(); }
-int inf_abi_version(void) { return 1; }
+int inf_abi_version(void) { return 2; }
 
 int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, int64_t table_ld, const void* vids,
                int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
-               void* out, int out_dtype, int64_t ld_out, int rows_out, void* out_t, int64_t ld_out_t,
-               inf_stream_t stream) {
+               int64_t num_source_rays, void* out, int out_dtype, int64_t ld_out, int rows_out, void* out_t,
+               int64_t ld_out_t, inf_stream_t stream) {
   return launch_gather(table, table_dtype, num_vertices, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype,
-                       idx_offset, nullptr, 0, batch, out, out_dtype, ld_out, rows_out, out_t, ld_out_t,
+                       idx_offset, nullptr, 0, num_source_rays, batch, out, out_dtype, ld_out, rows_out, out_t, ld_out_t,
                        (hipStream_t)stream);
 }
 
 int inf_encode(const float* table, int64_t num_rows, const void* vids, int vid_dtype, const float* bary,
-               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch, int encoding, int enc_k,
-               const float* enc_proj, int include_input, void* out, int out_dtype, int64_t ld_out, int rows_out,
-               inf_stream_t stream) {
-  return launch_encode(table, num_rows, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, nullptr, 0, batch,
+               const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch, int64_t num_source_rays,
+               int encoding, int enc_k, const float* enc_proj, int include_input, void* out, int out_dtype,
+               int64_t ld_out, int rows_out, inf_stream_t stream) {
+  return launch_encode(table, num_rows, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, nullptr, 0,
+                       num_source_rays, batch,
                        encoding, enc_k, enc_proj, include_input, out, out_dtype, ld_out, rows_out, nullptr, 0,
                        (hipStream_t)stream);
 }
@@ -1138,12 +1175,26 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
     p->adam_segs.push_back(a);
   }
   p->adam_items.push_back(AdamItem{-1, 0, 0, 0});  // end-of-step: loss sums, batch advance
+  // gradient buckets of the data-parallel step: bucket 1 = the arena from the skip layer's
+  // Ly weight on (its items listed first, with the end-of-step item), bucket 2 = the rest
+  const ParamSeg* ly = p->weight_seg(p->s, 1);
+  p->grad_split = ly != nullptr ? ly->off : 0;
+  std::stable_partition(p->adam_items.begin(), p->adam_items.end(), [&](const AdamItem& it) {
+    return it.seg < 0 || p->segs[it.seg].off >= p->grad_split;
+  });
+  p->n_items_b1 = 0;
+  for (const auto& it : p->adam_items)
+    if (it.seg < 0 || p->segs[it.seg].off >= p->grad_split) ++p->n_items_b1;
   const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
   INF_CHECK_ARG(seg_bytes + (int64_t)(p->adam_items.size() * sizeof(AdamItem)) <= p->table_bytes, "table size");
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
                         hipMemcpyHostToDevice));
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables + seg_bytes, p->adam_items.data(),
                         p->adam_items.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  {
+    const std::vector<AdamSeg> tb = bucket_segs(p);
+    INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables_b, tb.data(), tb.size() * sizeof(AdamSeg), hipMemcpyHostToDevice));
+  }
   // the vector and end-of-step items, run by the dW GEMM's first blocks when it fuses the update
   std::vector<AdamItem> aux;
   for (const auto& it : p->adam_items)
@@ -1211,8 +1262,13 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     return INF_ERR_STATE;
   }
   const bool apply_adam = (flags & INF_STEP_ADAM) != 0;
-  INF_CHECK_ARG((flags & ~(INF_STEP_ADAM | INF_STEP_ADVANCE | INF_STEP_XSLOT0 | INF_STEP_XSLOT1)) == 0,
+  INF_CHECK_ARG((flags & ~(INF_STEP_ADAM | INF_STEP_ADVANCE | INF_STEP_XSLOT0 | INF_STEP_XSLOT1 | INF_STEP_PART1 |
+                           INF_STEP_PART2)) == 0,
                 "train_step: unknown flags");
+  const int part = (flags & INF_STEP_PART1) ? 1 : (flags & INF_STEP_PART2) ? 2 : 0;
+  INF_CHECK_ARG(part == 0 || (!apply_adam && (flags & INF_STEP_ADVANCE) == 0 && !((flags & INF_STEP_PART1) &&
+                                                                                  (flags & INF_STEP_PART2))),
+                "train_step: PART1 / PART2 are gradient-only halves of one step");
   const int xslot = (flags & INF_STEP_XSLOT0) ? 0 : (flags & INF_STEP_XSLOT1) ? 1 : -1;
   INF_CHECK_ARG(batch != nullptr && batch->rgb != nullptr, "train_step: batch with target colours required");
   if (batch->encoding == INF_ENC_PROJECTED) {
@@ -1228,6 +1284,24 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   int ck = 0;
   int Bp3 = 0;
   if ((rc = pad_batch(p, batch->batch, true, &Bp3))) return rc;
+  // bucketed halves of a gradient-only step (fused chain3 path): PART1 = the fused chain,
+  // the dW GEMM of bucket 1's matrices and the reduction of bucket 1 (arena [grad_split, P),
+  // biases and the step's loss sums included) into `grads`; PART2 = the same for bucket 2
+  // (arena [0, grad_split)).  The caller all-reduces bucket 1 while PART2 runs.
+  const bool bucketed = part != 0 && use_chain3(p, batch, Bp3) && Bp3 % (256 * p->bucket_splits) == 0 &&
+                        std::getenv("INF_FUSED_UPDATE") == nullptr;
+  if (part == 2 && !bucketed) return INF_OK;  // PART1 reduced the whole gradient
+  if (part == 2) {
+    INF_CHECK_ARG(p->stepped && p->last_chain == 3 && p->saved_bp == Bp3, "train_step: PART2 without its PART1");
+    if ((rc = run_weight_grads(p, Bp3, st, 3, nullptr, 2))) return rc;
+    AdamArgs a = update_args(p, Bp3);
+    a.segs = p->W<AdamSeg>(p->o_tables_b);
+    a.items += p->n_items_b1;
+    a.num_items -= p->n_items_b1;
+    a.grad_src = GRAD_SLABS;
+    a.write_grads = 1;
+    return launch_update(a, p->mode, st);
+  }
   // the update launch's arguments for a step whose gradient partials are complete
   auto step_update = [&](int Bp_, int nloss_) {
     AdamArgs a = update_args(p, Bp_);
@@ -1268,6 +1342,15 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       if ((rc = run_weight_grads(p, Bp, st, 3, &a))) return rc;
       note_shadow_write(p, a, st);
       return INF_OK;
+    }
+    if (bucketed) {  // PART1
+      p->last_chain = 3;
+      if ((rc = run_weight_grads(p, Bp, st, 3, nullptr, 1))) return rc;
+      if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
+      AdamArgs a = step_update(Bp, nloss);
+      a.segs = p->W<AdamSeg>(p->o_tables_b);
+      a.num_items = p->n_items_b1;
+      return launch_update(a, p->mode, st);
     }
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
   } else if (chain) {
@@ -1530,7 +1613,8 @@ int inf_prefetch_batch(inf_plan* p, const inf_batch* b, int slot, inf_stream_t s
   hipStream_t st = (hipStream_t)stream;
   if ((rc = launch_gather(b->table, b->table_dtype, b->num_vertices, p->k_pad, p->k_pad, b->vids, b->vid_dtype,
                           b->bary, b->ray_idx, b->idx_dtype, b->idx_offset,
-                          b->offset_from_ctrl ? &p->ctrl->prefetch_index : nullptr, b->num_rays, b->batch,
+                          b->offset_from_ctrl ? &p->ctrl->prefetch_index : nullptr, b->num_rays,
+                          b->num_source_rays, b->batch,
                           p->W(p->o_xp[slot]), INF_DTYPE_BF16, p->k_pad, Bp, nullptr, 0, st)))
     return rc;
   if (b->offset_from_ctrl) {
@@ -1539,6 +1623,8 @@ int inf_prefetch_batch(inf_plan* p, const inf_batch* b, int slot, inf_stream_t s
   }
   return INF_OK;
 }
+
+int64_t inf_plan_grad_split(const inf_plan* p) { return p == nullptr ? -1 : p->grad_split; }
 
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;

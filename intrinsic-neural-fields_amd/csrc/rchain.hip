@@ -100,8 +100,8 @@ __global__ __launch_bounds__(CW * 64) void rchain_kernel(const RchainArgs a) {
     const int b = b0 + rl;
     int v = 0, ok = 0;
     float w = 0.f;
-    if (b < a.batch && ray_in_range(a.idx_offset, b, a.num_rays)) {
-      const int64_t rr = a.ray_idx != nullptr ? ray_row(a.ray_idx, a.idx_dtype, a.idx_offset, b) : a.idx_offset + b;
+    const int64_t rr = b < a.batch ? source_row(a.ray_idx, a.idx_dtype, a.idx_offset, b, a.num_rays, a.num_src) : -1;
+    if (rr >= 0) {
       const int64_t e = vid_at(a.vids, a.vid_dtype, 3 * rr + i);
       ok = (uint64_t)e < (uint64_t)a.num_vertices;  // out-of-range ids read as zero rows (gather.hip)
       v = ok ? (int)e : 0;

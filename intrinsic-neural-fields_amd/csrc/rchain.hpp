@@ -25,6 +25,7 @@ struct RchainArgs {
   int32_t idx_dtype;
   int64_t idx_offset;
   int64_t num_rays;  // bound on idx_offset + b (0 = unchecked)
+  int64_t num_src;   // rows of vids / bary / rgb (inf_batch::num_source_rays; 0 = unchecked)
   // weight stream (C3Block; flags C3F_SWAP / C3F_GATHER as in the chunked chain3 schedule)
   C3Block blk[RC_MAX_BLOCKS];
   int32_t nblk, nphase, nchunk;

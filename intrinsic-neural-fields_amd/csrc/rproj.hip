@@ -153,8 +153,8 @@ __global__ __launch_bounds__((LP<H, CW_>::THREADS)) void rproj_kernel(const Rcha
     Rec r{0, 0, 0.f};
     if (x < BM * 3) {
       const int b = tile * BM + x / 3, i = x % 3;
-      if (b < a.batch && ray_in_range(a.idx_offset, b, a.num_rays)) {
-        const int64_t rr = a.ray_idx != nullptr ? ray_row(a.ray_idx, a.idx_dtype, a.idx_offset, b) : a.idx_offset + b;
+      const int64_t rr = b < a.batch ? source_row(a.ray_idx, a.idx_dtype, a.idx_offset, b, a.num_rays, a.num_src) : -1;
+      if (rr >= 0) {
         const int64_t e = vid_at(a.vids, a.vid_dtype, 3 * rr + i);
         r.ok = (uint64_t)e < (uint64_t)a.num_vertices;  // out-of-range ids read as zero rows (gather.hip)
         r.v = r.ok ? (int)e : 0;

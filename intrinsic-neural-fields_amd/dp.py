@@ -50,6 +50,38 @@ def allreduce_grads(flat_grads: torch.Tensor, group=None) -> torch.Tensor:
     return flat_grads
 
 
+def any_rank(flag: bool, device, group=None) -> bool:
+    """True on every rank when `flag` is True on at least one (one MAX all-reduce).  Used for
+    decisions that change which collectives a rank issues: they must be taken together."""
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(int(t.item()))
+
+
+def replica_checksum(arena: torch.Tensor) -> torch.Tensor:
+    """Bit-exact fingerprint of an fp32 arena: [sum of the int32 bit patterns, the same
+    weighted by position mod 65521] as int64 (any flipped bit changes the first)."""
+    bits = arena.detach().reshape(-1).view(torch.int32).to(torch.int64)
+    pos = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([bits.sum(), (bits * pos).sum()])
+
+
+def check_replicas(arena: torch.Tensor, group=None, what="parameters"):
+    """Raise when the replicas' `what` differ on any rank (MIN vs MAX of the fingerprint):
+    data parallelism here keeps replicas bitwise equal without broadcasts, so a difference
+    means the ranks' collectives or updates went out of step."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    hi = replica_checksum(arena)
+    lo = hi.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    if not torch.equal(hi, lo):
+        raise RuntimeError(f"data-parallel replicas diverged: {what} differ across ranks "
+                           f"(fingerprint min {lo.tolist()} / max {hi.tolist()})")
+
+
 def allreduce_scalars(values, device, group=None) -> list:
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -96,9 +128,27 @@ class DataParallelEpoch:
     the flat-gradient all-reduce over RCCL, then Adam and the batch advance -- GRAPH_STEPS
     steps per graph replay, the collective captured inside (no host round trip per step).
     Replicas stay bitwise equal without parameter broadcasts.  A partial last batch
-    (drop_last=False) runs eagerly."""
+    (drop_last=False) runs eagerly.
+
+    Re-capture is decided collectively: a rank whose plan changed (rank 0 alone renders the
+    validation views, and a render can grow its model's plan) would otherwise capture on
+    its own, and its capture's eager warm-up step would issue an all-reduce the other ranks
+    never match -- every later gradient all-reduce would then pair steps of different ranks.
+    After every epoch the replicas' parameters are compared bit for bit across ranks
+    (check_replicas; INF_DP_CHECK=0 turns it off)."""
 
     GRAPH_STEPS = 8  # even: the pre-gather slots alternate
+    # step shapes (how the gradient all-reduce sits in the step):
+    #   serial   -- fused step -> all-reduce of the flat gradient -> Adam + batch advance;
+    #   prefetch -- serial, plus the next batch's gather on a side stream beside the
+    #               all-reduce (runtime.StepPipeline lead 0: the chain reads pre-gathered rows);
+    #   bucketed -- the dW GEMM and gradient reduction in two halves (inf_train_step PART1 /
+    #               PART2): bucket 1 (Ly and the layers after it) is all-reduced on a side
+    #               stream while the second half's GEMM runs, then bucket 2, then Adam.
+    # INF_DP_SHAPE picks one; "auto" (default at world > 1 over RCCL) captures every shape,
+    # times a few replays of each on the same saved state and keeps the fastest -- the
+    # decision is the MAX over ranks of each shape's time, so every rank picks the same one.
+    SHAPES = ("serial", "prefetch", "bucketed")
 
     def __init__(self, group=None):
         self.group = group
@@ -109,6 +159,9 @@ class DataParallelEpoch:
         self.idx = None
         self.steps_done = 0
         self.pipe = None
+        self.side = None
+        self.shape = "serial"
+        self.shape_times = None  # {shape: ms per step} of the last autotune
 
     def graph_collective(self) -> bool:
         """The all-reduce can be captured into the step graphs (RCCL; not gloo)."""
@@ -122,39 +175,114 @@ class DataParallelEpoch:
         plan.train_step(batch, None, apply_adam=False, xslot=xslot)
         self._tail_all_reduce(rt, plan)
 
+    def _step_bucketed(self, rt, plan, batch):
+        """One step with the gradient all-reduced in two buckets: bucket 1 on a side stream
+        beside the second half of the dW GEMM, then bucket 2 (after bucket 1: one
+        communicator, used in order), then Adam + advance."""
+        split = plan.grad_split()
+        plan.train_step(batch, None, apply_adam=False, part=1)
+        main = torch.cuda.current_stream()
+        if self.side is None:
+            self.side = torch.cuda.Stream(device=rt.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            allreduce_grads(rt.grads[split:], self.group)
+        plan.train_step(batch, None, apply_adam=False, part=2)
+        main.wait_stream(self.side)
+        allreduce_grads(rt.grads[:split], self.group)
+        plan.adam(0, 0.0, advance=True)
+
     def _pipelined(self, count, rt, plan, batch):
         self.pipe.run(count, lambda xs: plan.train_step(batch, None, apply_adam=False, xslot=xs),
                       tail_fn=lambda: self._tail_all_reduce(rt, plan))
 
-    def _capture(self, plan, rt, batch):
+    def _steps(self, shape, count, rt, plan, batch):
+        if shape == "prefetch" and self.pipe is not None:
+            self._pipelined(count, rt, plan, batch)
+        elif shape == "bucketed":
+            for _ in range(count):
+                self._step_bucketed(rt, plan, batch)
+        else:
+            for _ in range(count):
+                self._step(rt, plan, batch)
+
+    def _candidate_shapes(self):
+        want = os.environ.get("INF_DP_SHAPE", "auto")
+        if want != "auto":
+            if want not in self.SHAPES:
+                raise ValueError(f"INF_DP_SHAPE must be one of {self.SHAPES} or auto")
+            return [want]
+        # one GPU: nothing to hide behind, the plain step is the fastest (bench.py INF_BENCH_DP)
+        return list(self.SHAPES) if self.world > 1 else ["serial"]
+
+    def _capture_shape(self, shape, plan, rt, batch, s):
         from inf_hip import runtime
+        pipe = None
+        if shape == "prefetch":
+            pipe = runtime.StepPipeline(plan, batch, lead=0)
+            if not pipe.start():
+                return None
+        self.pipe = pipe
+        g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                self._steps("bucketed" if shape == "bucketed" else "serial", 1, rt, plan, batch)
+            with torch.cuda.graph(gm, stream=s):
+                self._steps(shape, self.GRAPH_STEPS, rt, plan, batch)
+        torch.cuda.current_stream().wait_stream(s)
+        return (g1, gm, pipe)
+
+    def _time_graphs(self, g, plan, full):
+        """ms per step of replays of one shape's graphs (batch index from 0, within the
+        epoch's full batches)."""
+        g1, gm, pipe = g
+        plan.set_batch_index(0)
+        if pipe is not None:
+            pipe.start()
+        n = min(full, self.GRAPH_STEPS)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if n == self.GRAPH_STEPS:
+            gm.replay()  # warm
+            plan.set_batch_index(0)
+            if pipe is not None:
+                pipe.start()
+            e0.record()
+            gm.replay()
+            e1.record()
+        else:
+            e0.record()
+            for _ in range(n):
+                g1.replay()
+            e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    def _capture(self, plan, rt, batch, full=2):
         saved = [x.clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl)]
         plan.set_batch_index(0)
         plan.train_step(batch, None, apply_adam=False)  # settles the plan's tables before capture
         self._tail_all_reduce(rt, plan)
-        # the next batch's gather on a side stream, beside the all-reduce (StepPipeline)
-        # INF_PREFETCH=1: the next batch's gather beside the all-reduce (off by default, see
-        # runtime.StepPipeline and bench.py for the world-1 measurement)
-        self.pipe = runtime.StepPipeline(plan, batch, lead=0) if os.environ.get("INF_PREFETCH", "0") != "0" else None
-        if self.pipe is not None and not self.pipe.start():
-            self.pipe = None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s):
-                plan.train_step(batch, None, apply_adam=False)
-                self._tail_all_reduce(rt, plan)
-            with torch.cuda.graph(gm, stream=s):
-                if self.pipe is not None:
-                    self._pipelined(self.GRAPH_STEPS, rt, plan, batch)
-                else:
-                    for _ in range(self.GRAPH_STEPS):
-                        self._step(rt, plan, batch)
-        torch.cuda.current_stream().wait_stream(s)
+        graphs = {}
+        for shape in self._candidate_shapes():
+            g = self._capture_shape(shape, plan, rt, batch, s)
+            if g is not None:
+                graphs[shape] = g
+        names = list(graphs)
+        chosen = names[0]
+        if len(names) > 1:
+            ms = torch.tensor([self._time_graphs(graphs[n], plan, full) for n in names], dtype=torch.float64,
+                              device=rt.device)
+            if self.world > 1:
+                dist.all_reduce(ms, op=dist.ReduceOp.MAX, group=self.group)
+            self.shape_times = dict(zip(names, ms.tolist()))
+            chosen = names[int(torch.argmin(ms))]
         for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
             dst.copy_(src)
         plan.sync_shadow()
+        g1, gm, pipe = graphs[chosen]
+        self.shape, self.pipe = chosen, pipe
         self.graph = (g1, gm)
 
     def run(self, trainer, loader):
@@ -191,10 +319,12 @@ class DataParallelEpoch:
                                     offset_from_ctrl=True, loss_count=3 * B, loss=loss_type)
             if use_graph:
                 key = (plan, bs, full, loss_type, loader.source, self.idx.data_ptr())
-                stale = self.key is None or self.key[0] is not plan or self.key[4] is not loader.source or \
-                    self.key[1:4] != key[1:4] or self.key[5] != key[5]
-                if self.graph is None or stale:
-                    self._capture(plan, rt, batch)
+                stale = self.graph is None or self.key is None or self.key[0] is not plan or \
+                    self.key[4] is not loader.source or self.key[1:4] != key[1:4] or self.key[5] != key[5]
+                if self.world > 1:  # every rank re-captures (and warms up) together
+                    stale = any_rank(stale, rt.device, self.group)
+                if stale:
+                    self._capture(plan, rt, batch, full)
                     self.key = key
                 optim.sync_runtime_state(model, rt, plan, group)
                 plan.reset_epoch_sums()
@@ -211,9 +341,8 @@ class DataParallelEpoch:
                         g1.replay()
             else:
                 plan.set_batch_index(0)
-                for _ in range(full):
-                    plan.train_step(batch, None, apply_adam=False)
-                    self._tail_all_reduce(rt, plan)
+                shape = os.environ.get("INF_DP_SHAPE", "serial")
+                self._steps("bucketed" if shape == "bucketed" else "serial", full, rt, plan, batch)
             steps = full
         if nb > full:  # partial last batch (drop_last=False), eager
             gb = N - full * B
@@ -230,6 +359,8 @@ class DataParallelEpoch:
             steps += 1
         optim.after_fused_steps(model, rt, group, steps)
         self.steps_done += steps
+        if os.environ.get("INF_DP_CHECK", "1") != "0":
+            check_replicas(rt.arena, self.group)
         c = plan.read_ctrl()
         loss_sum, sse = allreduce_scalars([c["epoch_loss"], c["epoch_sse"]], rt.device, self.group)
         return loss_sum / (3 * N if nb > full else 3 * full * B), sse / (N if nb > full else full * B)

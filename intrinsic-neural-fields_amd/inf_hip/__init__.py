@@ -21,7 +21,7 @@ LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
 LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
-STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1 = 1, 2, 4, 8  # inf_train_step flags
+STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, STEP_PART1, STEP_PART2 = 1, 2, 4, 8, 16, 32  # inf_train_step
 ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF, ENC_PROJECTED = 0, 1, 2, 3, 4
 ENC_CODES = {"xyz": ENC_XYZ, "rff": ENC_RFF, "ff": ENC_FF}
 
@@ -46,7 +46,8 @@ class Batch(ctypes.Structure):
                 ("ray_idx", c_void_p), ("idx_dtype", c_int32), ("idx_offset", c_int64),
                 ("offset_from_ctrl", c_int32), ("features", c_void_p), ("ld_features", c_int64),
                 ("batch", c_int32), ("loss_count", c_int64), ("loss", c_int32), ("num_rays", c_int64),
-                ("encoding", c_int32), ("enc_k", c_int32), ("enc_proj", c_void_p), ("enc_include_input", c_int32)]
+                ("encoding", c_int32), ("enc_k", c_int32), ("enc_proj", c_void_p), ("enc_include_input", c_int32),
+                ("num_source_rays", c_int64)]
 
 
 class Ctrl(ctypes.Structure):
@@ -61,10 +62,11 @@ assert CTRL_BYTES == 48
 _SIGNATURES = {
     "inf_last_error": (ctypes.c_char_p, []),
     "inf_abi_version": (c_int, []),
+    "inf_build_id": (ctypes.c_char_p, []),
     "inf_gather": (c_int, [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int,
-                           c_int64, c_int, c_void_p, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p]),
-    "inf_encode": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int64, c_int, c_int, c_int,
-                           c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_void_p]),
+                           c_int64, c_int, c_int64, c_void_p, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p]),
+    "inf_encode": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int64, c_int, c_int64,
+                           c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int64, c_int, c_void_p]),
     "inf_encoded_dim": (c_int, [c_int, c_int, c_int]),
     "inf_ssim_workspace_bytes": (c_int64, [c_int, c_int, c_int]),
     "inf_ssim": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, ctypes.c_double, c_void_p, c_void_p, c_void_p]),
@@ -100,6 +102,7 @@ _SIGNATURES = {
     "inf_project_table": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_plan_last_step_path": (c_int, [c_void_p]),
+    "inf_plan_grad_split": (c_int64, [c_void_p]),
     "inf_plan_weight_generation": (c_int64, [c_void_p]),
     "inf_prefetch_batch": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
@@ -135,7 +138,40 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    _check_provenance(lib)
     return lib
+
+
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+BUILD_ID = None       # inf_build_id() of the loaded library
+BUILD_VERIFIED = None  # True: recomputed from the sources beside it; None: sources absent
+
+
+def source_hash(files, base=CSRC) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(base, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _check_provenance(lib):
+    """The library must have been linked from the sources next to it (csrc/Makefile writes
+    the hash of their bytes into inf_build_id): a stale or foreign libinf_hip.so raises
+    here instead of running other kernels than the tree's.  INF_ALLOW_STALE_LIB=1 skips
+    the refusal (tuning experiments on variant builds)."""
+    global BUILD_ID, BUILD_VERIFIED
+    BUILD_ID = lib.inf_build_id().decode()
+    want, *files = BUILD_ID.split()
+    if not files or not all(os.path.exists(os.path.join(CSRC, f)) for f in files):
+        BUILD_VERIFIED = None
+        return
+    got = source_hash(files)
+    BUILD_VERIFIED = got == want
+    if not BUILD_VERIFIED and os.environ.get("INF_ALLOW_STALE_LIB", "0") == "0":
+        raise ImportError(f"{LIB_PATH} was built from other sources (build id {want}, sources hash {got}): "
+                          "rebuild it (make -C intrinsic-neural-fields_amd/csrc)")
 
 
 lib = _load()

@@ -11,7 +11,8 @@ import ctypes
 import torch
 
 from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, ENC_PROJECTED, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
-               MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo, c_int64, c_void_p,
+               MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_PART1, STEP_PART2, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo,
+               c_int64, c_void_p,
                check, lib)
 
 _TORCH_DTYPE = {DTYPE_F32: torch.float32, DTYPE_BF16: torch.bfloat16}
@@ -67,7 +68,7 @@ def gather(E: torch.Tensor, vids: torch.Tensor, bary: torch.Tensor, ray_idx: tor
         return out
     check(lib.inf_gather(ptr(E), dtype_code(E), E.shape[0], k, E.stride(0), ptr(vids), dtype_code(vids), ptr(bary),
                          ptr(ray_idx), dtype_code(ray_idx) if ray_idx is not None else DTYPE_I64, offset, batch,
-                         ptr(out), dtype_code(out), out.stride(0), out.shape[0], None, 0, stream_handle()), "gather")
+                         vids.shape[0], ptr(out), dtype_code(out), out.stride(0), out.shape[0], None, 0, stream_handle()), "gather")
     return out
 
 
@@ -116,7 +117,7 @@ def encode(enc: Encoding, points: torch.Tensor, vids: torch.Tensor | None = None
         return out
     check(lib.inf_encode(ptr(points), points.shape[0], ptr(vids), dtype_code(vids) if vids is not None else DTYPE_I32,
                          ptr(bary), ptr(ray_idx), dtype_code(ray_idx) if ray_idx is not None else DTYPE_I64, offset,
-                         batch, enc.code, enc.k, ptr(enc.proj), int(enc.include_input), ptr(out), DTYPE_F32,
+                         batch, vids.shape[0] if vids is not None else points.shape[0], enc.code, enc.k, ptr(enc.proj), int(enc.include_input), ptr(out), DTYPE_F32,
                          out.stride(0), out.shape[0], stream_handle()), "encode")
     return out
 
@@ -339,6 +340,7 @@ class Plan:
             b.vids = None
             b.batch = xyz.shape[0] if batch is None else int(batch)
             b.num_rays = xyz.shape[0]
+            b.num_source_rays = xyz.shape[0]
         elif features is not None:
             require_hip(features)
             if features.dtype != torch.float32 or features.dim() != 2 or features.stride(1) != 1:
@@ -363,6 +365,8 @@ class Plan:
             b.vid_dtype = DTYPE_I32
             b.bary = src.bary.data_ptr()
             b.rgb = src.rgbs.data_ptr() if src.rgbs is not None else None
+            # rows the permutation may name: an entry outside them reads as a zero row
+            b.num_source_rays = src.vids32.shape[0]
             if ray_idx is not None:
                 b.ray_idx = ray_idx.data_ptr()
                 b.idx_dtype = dtype_code(ray_idx)
@@ -394,12 +398,15 @@ class Plan:
         check(lib.inf_backward(self.handle, ptr(dpred), ptr(grads), stream_handle()), "backward")
 
     def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool, advance: bool = False,
-                   xslot: int | None = None):
+                   xslot: int | None = None, part: int | None = None):
         """inf_train_step; advance=True also moves ctrl.batch_index on (graph-replayed epochs);
-        xslot: the batch's features were gathered into that pre-gather slot (prefetch)."""
+        xslot: the batch's features were gathered into that pre-gather slot (prefetch);
+        part 1 / 2: the bucketed halves of a gradient-only step (grad_split())."""
         flags = (STEP_ADAM if apply_adam else 0) | (STEP_ADVANCE if advance else 0)
         if xslot is not None:
             flags |= STEP_XSLOT0 if xslot == 0 else STEP_XSLOT1
+        if part is not None:
+            flags |= STEP_PART1 if part == 1 else STEP_PART2
         check(lib.inf_train_step(self.handle, ctypes.byref(b), ptr(pred), flags, stream_handle()), "train_step")
 
     def prefetch(self, b: Batch, slot: int) -> bool:
@@ -455,6 +462,10 @@ class Plan:
         """inf_plan_weight_generation: changes whenever an update launch may have moved the
         weights; -1 once one was graph-captured (then nothing derived may be cached)."""
         return int(lib.inf_plan_weight_generation(self.handle))
+
+    def grad_split(self) -> int:
+        """inf_plan_grad_split: gradient bucket 1 = arena [split, P), bucket 2 = [0, split)."""
+        return int(lib.inf_plan_grad_split(self.handle))
 
     def ctrl_advance(self):
         check(lib.inf_ctrl_advance(self.handle, stream_handle()), "ctrl_advance")

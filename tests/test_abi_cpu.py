@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(inf_hip.lib, name), name
         assert name in inf_hip.EXPORTED, f"{name} has no ctypes signature"
-    assert inf_hip.lib.inf_abi_version() == 1
+    assert inf_hip.lib.inf_abi_version() == 2
 
 
 def reference_layout(k, H, L, s):

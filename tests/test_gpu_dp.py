@@ -171,3 +171,138 @@ def test_train_data_parallel_two_ranks_one_gpu_gloo(tmp_path, mode, w_rel, loss_
         assert d.max() <= 2 * lr * 200 and rel <= w_rel, (k, float(d.max()), rel)
     assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
     np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=loss_rtol)
+
+
+def _bucket_rays(k, V, N, seed):
+    rng = np.random.default_rng(seed)
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= E.max(0) - E.min(0)
+    return (torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (N, 3))).cuda(),
+            torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32)).cuda(),
+            torch.from_numpy(rng.random((N, 3)).astype(np.float32)).cuda())
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_bucketed_step_bitwise_unbucketed(monkeypatch, graph):
+    """The data-parallel step in two gradient buckets (inf_train_step PART1 / PART2: the dW
+    GEMM of Ly and the layers after it, their reduction, then the rest; the caller's
+    all-reduce of bucket 1 on a side stream between them) leaves exactly the parameters,
+    Adam moments and loss sums of the one-bucket step (fused step, all-reduce, Adam) when
+    both sum the same number of split-K partials -- eager and graph-captured, config B's
+    MLP at 4096 rays."""
+    from inf_hip import runtime
+    import model as M
+    k, H, L, s, B = 1024, 256, 8, 4, 4096
+    N = 3 * B
+    E, vids, bary, rgb = _bucket_rays(k, 3000, N, seed=4)
+    monkeypatch.setenv("INF_DW_SPLITS", "4")
+    monkeypatch.setenv("INF_BUCKET_SPLITS", "4")
+    out = {}
+    for shape in ("serial", "bucketed"):
+        torch.manual_seed(0)
+        m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()
+        rt = m.hip_runtime()
+        rt.ensure_optimizer_arenas()
+        plan = runtime.Plan(k, H, L, s, "bf16", "L2", B, rt.arena, rt.grads, rt.exp_avg, rt.exp_avg_sq)
+        plan.set_lr(1e-3)
+        src = runtime.RaySource(E, vids, bary, rgb)
+        perm = torch.randperm(N, generator=torch.Generator().manual_seed(2)).cuda()
+        b = plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B, offset_from_ctrl=True)
+        side = torch.cuda.Stream()
+        split = plan.grad_split()
+        assert 0 < split < plan.info.num_params
+
+        def step():
+            if shape == "serial":
+                plan.train_step(b, None, apply_adam=False)
+            else:
+                plan.train_step(b, None, apply_adam=False, part=1)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    rt.grads[split:].mul_(1.0)  # stands in for the bucket-1 all-reduce
+                plan.train_step(b, None, apply_adam=False, part=2)
+                torch.cuda.current_stream().wait_stream(side)
+            plan.adam(0, 0.0, advance=True)
+
+        plan.set_batch_index(0)
+        if graph:
+            step()  # settles the plan's tables
+            plan.set_batch_index(0)
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            saved = [x.clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl)]
+            with torch.cuda.stream(st):
+                with torch.cuda.graph(g, stream=st):
+                    step()
+            torch.cuda.current_stream().wait_stream(st)
+            for dst, srcv in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
+                dst.copy_(srcv)
+            plan.sync_shadow()
+            plan.set_batch_index(0)
+            for _ in range(3):
+                g.replay()
+        else:
+            for _ in range(3):
+                step()
+        torch.cuda.synchronize()
+        assert plan.last_step_path() == "chain3"
+        c = plan.read_ctrl()
+        out[shape] = [x.detach().cpu().clone() for x in (plan.params, plan.exp_avg, plan.exp_avg_sq)] + \
+            [c["epoch_loss"], c["epoch_sse"], c["batch_index"]]
+    a, bb = out["serial"], out["bucketed"]
+    for x, y in zip(a[:3], bb[:3]):
+        assert torch.equal(x, y)
+    assert a[3:] == bb[3:] and a[5] == 3
+
+
+@pytest.mark.parametrize("mode,w_rel,loss_rtol", [("bf16", 5e-2, 2e-3), ("fp32", 1e-6, 1e-6)])
+def test_config_c_data_parallel_two_ranks_gloo(tmp_path, mode, w_rel, loss_rtol):
+    """Config C -- the human k=1024, 8 x 256 (skip 4), L2, lr 1e-4, batch 4096 MLP of
+    configs/texture_reconstruction/intrinsic_human_k1024_8x256.yaml -- through
+    `torchrun --nproc-per-node 2 train.py <cfg> --data_parallel` (two ranks on the one GPU
+    over gloo, 2048 rays per rank per step) against the single-process run of the same
+    YAML on a synthetic dataset in the reference's layout (a torus, 1024 eigenfunction
+    columns): same files, logged scalars up to the two half-batch gradients' summation
+    order, weights close (bounds as test_train_data_parallel_two_ranks_one_gpu_gloo)."""
+    import synthetic_views as S
+    S.build(str(tmp_path), H=128, W=128, kmax=1024, views=(4, 1, 1))
+    with open(os.path.join(ROOT, "configs", "texture_reconstruction", "intrinsic_human_k1024_8x256.yaml")) as fh:
+        cfg = yaml.safe_load(fh)
+    base = S.intrinsic_config(epochs=2, batch=4096, H=128, W=128)
+    cfg["data"] = base["data"]  # the synthetic dataset's paths; the MLP / training keys stay C's
+    cfg["model"]["kernels"]["mode"] = mode
+    cfg["training"].update(epochs=2, render_every=100)
+    assert (cfg["model"]["k"], cfg["model"]["num_layers"], cfg["model"]["mlp_hidden_dim"],
+            cfg["model"]["skip_layer_idx"], cfg["training"]["batch_size"]) == (1024, 8, 256, 4, 4096)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", INF_DP_BACKEND="gloo")
+    results = {}
+    for tag in ("single", "dp2"):
+        cfg["training"]["out_dir"] = f"out/{tag}"
+        path = tmp_path / f"{tag}.yaml"
+        with open(path, "w") as fh:
+            yaml.safe_dump(cfg, fh)
+        if tag == "single":
+            cmd = [sys.executable, os.path.join(PKG, "train.py"), str(path)]
+        else:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(PKG, "train.py"),
+                   str(path), "--data_parallel"]
+        r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        print(tag, r.stdout[-2000:], r.stderr[-3000:])
+        assert r.returncode == 0, tag
+        out = tmp_path / "out" / tag
+        sd = torch.load(out / "model_last_epoch.pt", map_location="cpu", weights_only=True)
+        rows = [json.loads(x) for x in open(out / "logs" / "scalars.jsonl")]
+        results[tag] = (sorted(os.listdir(out)), sd, rows)
+    (fs, ws, rs), (fd, wd, rd) = results["single"], results["dp2"]
+    assert fs == fd
+    assert ws["layers.4.Ly.weight"].shape == (256, 1024)
+    lr = float(cfg["training"]["lr"])
+    for key in ws:
+        a, b = ws[key].float().numpy().reshape(-1), wd[key].float().numpy().reshape(-1)
+        rel = float(np.linalg.norm(a - b) / max(np.linalg.norm(a), 1e-12))
+        print(key, "max", float(np.abs(a - b).max()), "rel", rel)
+        assert np.abs(a - b).max() <= 2 * lr * 200 and rel <= w_rel, (key, rel)
+    assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
+    np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=loss_rtol)

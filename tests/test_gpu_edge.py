@@ -199,3 +199,72 @@ def test_out_of_range_rays_and_vertices_read_as_zero():
         x[5] = 0.0
         p_ref, _ = O.mlp_forward(w0, x, L, s)
         assert np.abs(pred.cpu().numpy() - p_ref).max() < tol, mode
+
+
+def test_out_of_range_permutation_values_read_as_zero_rows():
+    """A permutation ENTRY naming a row outside the ray arrays (negative, >= N, the int32
+    limit) reads as a zero feature row and a zero target on every kernel path that reads
+    ray records -- gather + layered head (fp32), the register chain (bf16 forward), the
+    fused training chain (bf16, <= 8192 rays), the LDS-ring chain (bf16, > 8192 rays) and
+    the projected-table render -- instead of loading outside vids / bary / rgb
+    (inf_batch.num_source_rays; the cause of the illegal access recorded in f1fb648)."""
+    k, H, L, s = 64, 128, 4, 2
+    w0 = init_weights(k, H, L, s, seed=13)
+    N = 9100
+    E, vids, bary, rgb = synth_rays(k, 50, N, seed=21)
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda())
+    bad = {3: N + 1000, 7: -5, 11: 2 ** 31 - 1, 40: N}
+
+    def perm_for(B):
+        p = np.arange(B, dtype=np.int64)
+        for i, v in bad.items():
+            p[i] = v
+        return p
+
+    def oracle(B, w):
+        x = O.gather(E, vids[:B], bary[:B])
+        t = rgb[:B].copy()
+        for i in bad:
+            x[i] = 0.0
+            t[i] = 0.0
+        return x, t
+
+    for mode, B in (("fp32", 64), ("bf16", 64), ("bf16", 256), ("bf16", 9000)):
+        perm = torch.from_numpy(perm_for(B)).cuda()
+        x, t = oracle(B, w0)
+        p_ref, _ = O.mlp_forward(w0, x, L, s)
+        tol = 1e-5 if mode == "fp32" else 2e-2
+        plan, _ = plan_for(k, H, L, s, w0, mode, "L2", B)
+        pred = torch.empty((B, 3), device="cuda")
+        plan.forward(plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B), pred, save=False)
+        torch.cuda.synchronize()
+        assert np.abs(pred.cpu().numpy() - p_ref).max() < tol, ("forward", mode, B)
+        # a training step (loss against zero targets on the bad rows)
+        plan.set_lr(0.0)
+        plan.train_step(plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B), pred, apply_adam=True)
+        torch.cuda.synchronize()
+        assert np.abs(pred.cpu().numpy() - p_ref).max() < tol, ("train", mode, B, plan.last_step_path())
+        loss_ref = float(((p_ref - t) ** 2).sum())
+        loss = plan.read_ctrl()["loss_sum"]
+        assert abs(loss - loss_ref) < (1e-5 if mode == "fp32" else 2e-2) * max(1.0, loss_ref), (mode, B, loss, loss_ref)
+    # the projected-table render (bf16)
+    import model as M
+    m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()
+    m.kernel_mode = "bf16"
+    bplan = m.hip_plan(256)
+    wm = {n: p.detach().cpu().numpy() for n, p in m.named_parameters()}
+    B = 256
+    perm = torch.from_numpy(perm_for(B)).cuda()
+    P = bplan.project_table(src.table_for(bplan))
+    rpred = torch.empty((B, 3), device="cuda")
+    bplan.forward(bplan.make_batch(source=src, ray_idx=perm, offset=0, batch=B, projected=P), rpred, save=False)
+    torch.cuda.synchronize()
+    x, _ = oracle(B, wm)
+    r_ref, _ = O.mlp_forward(wm, x, L, s)
+    assert np.abs(rpred.cpu().numpy() - r_ref).max() < 2e-2
+    # the standalone gather (mesh.get_k_eigenfunc_vec_vals with the loader's index select)
+    T = torch.from_numpy(E).cuda()
+    got = rt().gather(T, src.vids32, src.bary, ray_idx=perm, offset=0, batch=B)
+    torch.cuda.synchronize()
+    assert np.abs(got.cpu().numpy() - x).max() < 1e-6
