@@ -693,23 +693,33 @@ def rff_bench(args, device, B=4096, reps=6):
             "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s"}
 
 
-def psnr_vs_ref(mode):
+PSNR_RUNS = {
+    # fixture: (workload, model keys, loss)
+    "g8_train_curve.npz": ("reference synthetic run G8 (k=64 4x128 skip 2, L1, lr 1e-3, 12 epochs)",
+                           {"k": 64, "num_layers": 4, "mlp_hidden_dim": 128, "skip_layer_idx": 2}, "L1"),
+    "g13_train_curve_B_L2.npz": ("reference synthetic run G13 on config B's MLP (k=1024 8x256 skip 4, L2, lr 1e-4, "
+                                 "12 epochs)",
+                                 {"k": 1024, "num_layers": 8, "mlp_hidden_dim": 256, "skip_layer_idx": 4}, "L2"),
+}
+
+
+def psnr_vs_ref(mode, fixture="g8_train_curve.npz"):
     """'PSNR vs ref' of BASELINE.json's metric: the reference's own 12-epoch synthetic
-    training run (tests/golden/g8_train_curve.npz, produced by importing the reference:
-    k=64 4x128 skip 2, L1, Adam; no dataset is available offline) re-run through this
-    framework's Trainer (trainer.py mirror, fused HIP steps) -- validation epoch-PSNR curve
-    against the reference's."""
+    training runs (tests/golden/g8_train_curve.npz and, on the benchmarked MLP,
+    g13_train_curve_B_L2.npz, produced by importing the reference; no dataset is available
+    offline) re-run through this framework's Trainer (trainer.py mirror, fused HIP steps)
+    -- validation epoch-PSNR curve against the reference's."""
     import tempfile
 
     import config
     from ray_dataloader import RayDataLoader
     from trainer import Trainer
-    d = np.load(os.path.join(ROOT, "tests", "golden", "g8_train_curve.npz"))
+    workload, mkeys, loss = PSNR_RUNS[fixture]
+    d = np.load(os.path.join(ROOT, "tests", "golden", fixture))
     with tempfile.TemporaryDirectory() as out:
         cfg = {"seed": 0, "data": {"img_height": 8, "img_width": 8},
-               "model": {"k": 64, "num_layers": 4, "mlp_hidden_dim": 128, "skip_layer_idx": 2,
-                         "kernels": {"mode": mode}},
-               "training": {"out_dir": out, "batch_size": int(d["batch"]), "lr": float(d["lr"]), "loss_type": "L1",
+               "model": dict(mkeys, kernels={"mode": mode}),
+               "training": {"out_dir": out, "batch_size": int(d["batch"]), "lr": float(d["lr"]), "loss_type": loss,
                             "render_every": 1000, "print_every": 1000, "epochs": len(d["val_psnr"]),
                             "checkpoint_every": 1000}}
         E = torch.from_numpy(d["E"])
@@ -725,7 +735,7 @@ def psnr_vs_ref(mode):
         rows = [json.loads(x) for x in open(os.path.join(out, "logs", "scalars.jsonl"))]
     val = np.array([r["value"] for r in rows if r["tag"] == "Val Epoch-PSNR"])
     ref = np.asarray(d["val_psnr"], dtype=np.float64)
-    return {"workload": "reference synthetic run G8 (k=64 4x128 skip 2, L1, 12 epochs)", "mode": mode,
+    return {"workload": workload, "mode": mode,
             "ref_final_db": float(ref[-1]), "final_db": float(val[-1]), "delta_final_db": float(val[-1] - ref[-1]),
             "max_abs_delta_db": float(np.abs(val - ref).max())}
 
@@ -930,7 +940,7 @@ def main():
     psnr = None
     if rank == 0 and world == 1 and not args.no_render and want("psnr"):
         try:
-            psnr = [psnr_vs_ref(m) for m in ("bf16", "fp32")]
+            psnr = [psnr_vs_ref(m, f) for f in PSNR_RUNS for m in ("bf16", "fp32")]
         except Exception as exc:  # reported, never fatal to the throughput line
             psnr = {"error": repr(exc)}
 

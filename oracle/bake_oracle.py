@@ -6,10 +6,13 @@ the GPU (csrc/bake.hip + the plan's render path).
 A float64 numpy restatement of bake_texture_field.py's texel search (point_in_tri
 :37-63 strict-interior test, clean_tris :96-112, nearest-centroid choice of
 get_tris_fast :134-161 without its 10-candidate horizon), bary_matched (:196-228) and
-uv_fill_holes (:245-264, scipy.signal.convolve2d as in the reference).  The reference
-needs trimesh + cv2 + a trained model on real data, none of which exist here, so this
-restatement is PARITY UNPINNED: it is checked by known answers in
-tests/test_oracle_raycast.py only.
+uv_fill_holes (:245-264, scipy.signal.convolve2d as in the reference).  PINNED against the
+reference's own get_tris_fast / bary_matched / uv_fill_holes run by
+tests/golden/make_golden.py (G14: a regular and a jittered UV triangulation, the
+reference's float128 arithmetic): identical texel -> triangle assignment, barycentrics
+within 1e-12, hole filling within 1e-12 (tests/test_oracle_fixtures_f.py); plus known
+answers in tests/test_oracle_raycast.py.  The reference's whole bake_texture still needs
+trimesh (mesh + material loading) and cv2, absent here.
 """
 from __future__ import annotations
 

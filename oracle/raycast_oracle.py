@@ -7,9 +7,12 @@ A numpy float64 restatement of the reference's camera rays and closest-hit ray-m
 intersection.  The reference intersects with trimesh + pyembree (closest hit,
 `multiple_hits=False`, two-sided, t > 0) and then computes the hit point's barycentric
 coordinates with `trimesh.triangles.points_to_barycentric(..., method='cramer')`.
-Neither trimesh nor embree is installed here and the reference's own tests hold no
-fixture for this path, so this restatement is PARITY UNPINNED: it is checked by
-known-answer cases (tests/test_oracle_raycast.py) and by analytic geometry only.
+Neither trimesh nor embree is installed here, so the INTERSECTION (closest_hits,
+points_to_barycentric_cramer) is PARITY UNPINNED: checked by known-answer cases
+(tests/test_oracle_raycast.py) and analytic geometry only.  The camera-ray generation is
+PINNED: create_ray_origins_and_directions matches the reference's own (pure torch,
+mesh.py:171-207) run by tests/golden/make_golden.py (G15) within 2e-7
+(tests/test_oracle_fixtures_f.py).
 """
 from __future__ import annotations
 

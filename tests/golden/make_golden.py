@@ -26,6 +26,11 @@ Fixtures:
   g10_rff_curve.npz                  12-epoch synthetic run, rff strategy  trainer.py:164-187,232-283 + the above
   g11_viewdep_{intrinsic,extrinsic}.npz  view-dependent field fwd + 1 step model.py:115-191,240-256
   g12_train_curve_B.npz              G8's run on config B's MLP (k=1024, 8x256, skip 4)
+  g13_train_curve_B_L2.npz           the same MLP with config B/C's own L2 loss and lr 1e-4
+                                     (a non-chaotic trajectory: the bf16 PSNR bar)
+  g14_bake_{grid,jitter}.npz         texel search + barycentrics + hole filling
+                                     (get_tris_fast, bary_matched, uv_fill_holes)  bake_texture_field.py:96-264,360-397
+  g15_raygen.npz                     create_ray_origins_and_directions         mesh.py:171-207
 
 Run:  python tests/golden/make_golden.py
 """
@@ -74,6 +79,7 @@ def _install_stubs():
             pass
 
     mod("tensorboardX", SummaryWriter=_Writer)
+    mod("cv2")  # bake_texture_field.py imports it for image writing only
     sk = mod("skimage")
     sk.metrics = mod("skimage.metrics", structural_similarity=lambda *a, **k: 0.0)
     return _Writer
@@ -536,6 +542,117 @@ def g12_train_curve_B():
          batch=np.int64(batch))
 
 
+def g13_train_curve_B_L2():
+    """G12's synthetic run on config B's MLP with the loss and learning rate config B / C
+    use (configs/texture_reconstruction/intrinsic_human_k1024_8x256.yaml: L2, lr 1e-4).
+    Unlike L1 at 2e-4 this trajectory is insensitive to summation order: the reference
+    itself run with 8 vs 3 CPU threads gives curves within 0.0013 dB (L1 / 2e-4: 0.18 dB),
+    so a per-epoch PSNR bar on it measures the arithmetic, not chaos."""
+    rng = np.random.default_rng(13)
+    V, k = 1000, in_dim("B")
+    E = rescaled_table(rng, V, k)
+    proj = rng.standard_normal((16, 3)).astype(np.float32) * 2.0
+    vert_rgb = 1.0 / (1.0 + np.exp(-(E[:, :16] * 4.0) @ proj))
+    def rays(n):
+        vids, bary = synthetic_rays(rng, V, n, include_edges=False)
+        rgb = np.einsum("ni,nic->nc", bary, vert_rgb[vids]).astype(np.float32)
+        return vids, bary, rgb
+    tr_v, tr_b, tr_rgb = rays(16384)
+    va_v, va_b, va_rgb = rays(2048)
+    batch, lr = 1024, 1e-4
+    cfg = {"model": model_cfg("B"), "training": {"lr": lr, "loss_type": "L2"}}
+    curves = []
+    for threads in (8, 3):  # two summation orders of the reference itself
+        torch.set_num_threads(threads)
+        torch.manual_seed(0)
+        model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+        tr = _bare_trainer(model, optim, ref_config.get_loss_fn(cfg))
+        Et = torch.from_numpy(E)
+        train_ld = ref_loader.RayDataLoader(Et, "efuncs", torch.from_numpy(tr_v), torch.from_numpy(tr_b),
+                                            torch.from_numpy(tr_rgb), None, None, batch, False, True, device="cpu")
+        tr.val_data_loader = ref_loader.RayDataLoader(Et, "efuncs", torch.from_numpy(va_v), torch.from_numpy(va_b),
+                                                      torch.from_numpy(va_rgb), None, None, batch, False, False,
+                                                      device="cpu")
+        val_psnr = []
+        for epoch in range(12):
+            for b in train_ld:  # shuffle=False: deterministic batch order
+                tr._train_step(b)
+            val_psnr.append(tr.evaluate(epoch)[1])
+        curves.append(val_psnr)
+    torch.set_num_threads(8)
+    save("g13_train_curve_B_L2.npz", E=E, tr_vids=tr_v, tr_bary=tr_b, tr_rgb=tr_rgb, va_vids=va_v, va_bary=va_b,
+         va_rgb=va_rgb, val_psnr=np.array(curves[0]), val_psnr_threads3=np.array(curves[1]), lr=np.float32(lr),
+         batch=np.int64(batch))
+
+
+def _uv_grid(nu, nv, jitter, rng):
+    """A UV triangulation of the unit square's [0.02, 0.98]^2 (a torus's seamed grid, as
+    tests/synthetic_views.py bakes), interior vertices jittered by `jitter` cells."""
+    gu, gv = np.meshgrid(np.arange(nu + 1) / nu, np.arange(nv + 1) / nv, indexing="ij")
+    VT = np.stack([0.02 + 0.96 * gu, 0.02 + 0.96 * gv], -1)
+    if jitter:
+        VT[1:-1, 1:-1] += (rng.random(VT[1:-1, 1:-1].shape) - 0.5) * jitter * 0.96 / np.array([nu, nv])
+    VT = VT.reshape(-1, 2)
+    i, j = np.meshgrid(np.arange(nu), np.arange(nv), indexing="ij")
+    a, b = i * (nv + 1) + j, (i + 1) * (nv + 1) + j
+    c, d = (i + 1) * (nv + 1) + j + 1, i * (nv + 1) + j + 1
+    F = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+    return VT, F
+
+
+def g14_bake():
+    """bake_texture's reverse texture lookup (bake_texture_field.py:356-397): texel centres
+    p of an H x W texture against the UV triangles in texel units ((W-1) u, (H-1)(1-v)),
+    the reference's float128 arithmetic; get_tris_fast (10 nearest centroids, strict
+    interior, min_area 1e-4), bary_matched, and uv_fill_holes of a texture with holes."""
+    import bake_texture_field as ref_bake
+    rng = np.random.default_rng(14)
+    for tag, (nu, nv, jit, H, W) in {"grid": (12, 8, 0.0, 40, 56), "jitter": (20, 14, 0.6, 64, 80)}.items():
+        VT, F = _uv_grid(nu, nv, jit, rng)
+        dtype = np.float128
+        pu = (W - 1) * VT[:, 0].astype(dtype)
+        pv = (H - 1) * (1 - VT[:, 1]).astype(dtype)
+        puvs = np.stack([pu, pv], -1)
+        a, b, c = puvs[F[:, 0]], puvs[F[:, 1]], puvs[F[:, 2]]
+        PX, PY = np.meshgrid(np.arange(W), np.arange(H))
+        p = np.stack([PX.ravel(), PY.ravel()], -1).astype(dtype)
+        idx = np.concatenate([ref_bake.get_tris_fast(p=ch, a=a, b=b, c=c)
+                              for ch in np.split(p, np.arange(1 << 15, p.shape[0], 1 << 15), axis=0)])
+        iv = idx[idx >= 0]
+        u, v, w = ref_bake.bary_matched(p=p[idx >= 0], a=a[iv], b=b[iv], c=c[iv])
+        bari = np.zeros((H * W, 3), np.float64)
+        bari[idx >= 0] = np.stack([u, v, w], -1).astype(np.float64)
+        # a texture with holes: colours on the covered texels, zero elsewhere (as bake_texture)
+        cols = np.zeros((H * W, 3))
+        cols[idx >= 0] = rng.random((int((idx >= 0).sum()), 3))
+        CC = cols.reshape(H, W, 3)
+        filled = ref_bake.uv_fill_holes(CC)
+        save(f"g14_bake_{tag}.npz", uv=VT, faces=F.astype(np.int64), H=np.int64(H), W=np.int64(W),
+             texel_face=idx.astype(np.int64), texel_bary=bari, tex=CC, tex_filled=filled,
+             tex_u8=(255 * filled).astype(np.uint8))
+
+
+def g15_raygen():
+    """mesh.create_ray_origins_and_directions (mesh.py:171-207): the rays of the masked
+    pixels of a view, R K^-1 [x y 1] normalised, from the camera centre."""
+    rng = np.random.default_rng(15)
+    H, W = 37, 53
+    ang = rng.standard_normal(3)
+    th = np.linalg.norm(ang)
+    kx = np.array([[0, -ang[2], ang[1]], [ang[2], 0, -ang[0]], [-ang[1], ang[0], 0]]) / th
+    R = np.eye(3) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+    cam = np.concatenate([R, rng.standard_normal((3, 1)) * 2.0], 1).astype(np.float32)
+    K = np.array([[W * 1.3, 0, W / 2 + 0.7], [0, H * 1.2, H / 2 - 0.4], [0, 0, 1]], np.float32)
+    res = {"cam": cam, "K": K, "H": np.int64(H), "W": np.int64(W)}
+    for tag, mask in (("full", np.ones(H * W, bool)), ("mask", rng.random(H * W) < 0.6)):
+        o, d = ref_mesh.create_ray_origins_and_directions(torch.from_numpy(cam), torch.from_numpy(K),
+                                                          torch.from_numpy(mask), H=H, W=W)
+        res[f"mask_{tag}"] = mask
+        res[f"origins_{tag}"] = o.numpy()
+        res[f"dirs_{tag}"] = d.numpy()
+    save("g15_raygen.npz", **res)
+
+
 if __name__ == "__main__":
     import tempfile
     torch.set_num_threads(8)
@@ -557,3 +674,6 @@ if __name__ == "__main__":
         g10_rff_curve()
         g11_viewdep()
         g12_train_curve_B()
+        g13_train_curve_B_L2()
+        g14_bake()
+        g15_raygen()

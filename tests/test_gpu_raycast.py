@@ -189,3 +189,19 @@ def test_row_sharded_render_assembles_to_full_frame():
     torch.testing.assert_close(torch.cat(parts), full, atol=0, rtol=0)
     torch.testing.assert_close(dp.render_distributed(r, c, Kt), full, atol=0, rtol=0)
     np.testing.assert_array_equal(r.render(c, Kt), full.cpu().numpy())
+
+
+@pytest.mark.parametrize("tag", ["full", "mask"])
+def test_camera_rays_match_reference_g15(g, tag):
+    """The device's camera rays (R K^-1 [x y 1] per masked pixel, normalised) against the
+    reference's own create_ray_origins_and_directions (mesh.py:171-207, fixture G15 made by
+    importing the reference): a rotated camera, off-centre principal point."""
+    import mesh as MS
+    d = g("g15_raygen.npz")
+    H, W = int(d["H"]), int(d["W"])
+    V, F = R.icosphere(2)
+    bvh = MS.get_ray_mesh_intersector(MS.TriMesh(V + 5.0, F))
+    mask = d[f"mask_{tag}"]
+    pix = torch.from_numpy(np.nonzero(mask)[0]).cuda()
+    face, bary, dirs = bvh.cast(torch.from_numpy(d["cam"]), torch.from_numpy(d["K"]), H, W, pixel_idx=pix)
+    np.testing.assert_allclose(dirs.cpu().numpy(), d[f"dirs_{tag}"], atol=1e-6)
