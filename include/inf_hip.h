@@ -36,7 +36,11 @@ enum {
 };
 
 enum { INF_DTYPE_F32 = 0, INF_DTYPE_BF16 = 1, INF_DTYPE_I32 = 2, INF_DTYPE_I64 = 3 };
-enum { INF_MODE_FP32 = 0, INF_MODE_BF16 = 1 };             /* GEMM arithmetic          */
+/* GEMM arithmetic: FP32 exact f32 MFMA; BF16 bf16 operands (fp32 accumulation, fp32
+ * master weights); BF16X3 fp32 operands multiplied as split bf16 (hi*hi + hi*lo + lo*hi,
+ * ~2^-16 relative per product) -- every buffer and kernel of the fp32 mode, only the
+ * GEMMs' inner products on bf16 matrix cores */
+enum { INF_MODE_FP32 = 0, INF_MODE_BF16 = 1, INF_MODE_BF16X3 = 2 };
 enum { INF_LOSS_L2 = 0, INF_LOSS_L1 = 1, INF_LOSS_CAUCHY = 2 }; /* config.py:113-122   */
 /* Input front-end of a batch (TextureField.input_feature_embed, model.py:33-40,98-104).
  * NONE: the table rows are the features (efuncs).  XYZ/RFF/FF: the table is the fp32

@@ -6,6 +6,12 @@
 //   fp32 mode: v_mfma_f32_16x16x4_f32 (exact f32 FMA chain), k-tile BK = 32 (128-byte
 //              rows); a lane's 16-byte fragment read holds 4 consecutive k that feed 4
 //              consecutive MFMAs, so every operand read is one ds_read_b128 in both modes.
+//   bf16x3 mode (SPLIT): fp32 operands in memory and LDS exactly as the fp32 mode; each
+//              lane splits its 8 k of a 32-k tile into x = hi + lo (hi = bf16(x),
+//              lo = bf16(x - hi)) and the product is hi*hi + hi*lo + lo*hi on
+//              v_mfma_f32_16x16x32_bf16 with fp32 accumulation: ~2^-16 relative per product
+//              (the dropped lo*lo), at 3 bf16 MFMAs per 32 k instead of 8 fp32 ones of 4x the
+//              cycles (SURVEY.md §0.3's split-bf16 parity mode).
 // Operand tiles are staged global -> registers -> LDS with a double buffer: the loads
 // for k-tile t+1 are issued before the MFMAs of tile t and written to the other LDS
 // buffer afterwards (one barrier per k-tile).  LDS rows are 8 x 16-byte chunks stored
@@ -88,14 +94,50 @@ struct Tile {
   static constexpr int TM = WM / 16, TN = WN / 16;
 };
 
-template <typename T, int BM, int BN>
+// x = hi + lo + O(2^-17 |x|): hi, lo round to nearest (bf16 conversions)
+__device__ __forceinline__ void split_bf16(const f32x4& x0, const f32x4& x1, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = (bf16)x0[e];
+    hi[4 + e] = (bf16)x1[e];
+    lo[e] = (bf16)(x0[e] - (float)hi[e]);
+    lo[4 + e] = (bf16)(x1[e] - (float)hi[4 + e]);
+  }
+}
+
+template <typename T, int BM, int BN, bool SPLIT = false>
 __device__ __forceinline__ void compute_tile(const char* __restrict__ As, const char* __restrict__ Bs, int wm0,
                                              int wn0, int lane, f32x4 (&acc)[Tile<T, BM, BN>::TM][Tile<T, BM, BN>::TN]) {
   using TL = Tile<T, BM, BN>;
   constexpr int TM = TL::TM, TN = TL::TN;
   const int r16 = lane & 15;
   const int g = lane >> 4;
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (SPLIT) {
+    // lane (r16, g) holds k = 8 g .. 8 g + 7 of the 32-k tile (chunks 2 g, 2 g + 1) for A
+    // and B alike -- one 16x16x32 MFMA per term covers the whole fp32 k-tile
+    static_assert(sizeof(T) == 4, "bf16x3 splits fp32 operands");
+    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm0 + i * 16 + r16;
+      split_bf16(*reinterpret_cast<const f32x4*>(As + swz(row, 2 * g)),
+                 *reinterpret_cast<const f32x4*>(As + swz(row, 2 * g + 1)), ah[i], al[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn0 + j * 16 + r16;
+      split_bf16(*reinterpret_cast<const f32x4*>(Bs + swz(row, 2 * g)),
+                 *reinterpret_cast<const f32x4*>(Bs + swz(row, 2 * g + 1)), bh[j], bl[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+  } else if constexpr (sizeof(T) == 2) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 a[TM], b[TN];
@@ -143,7 +185,7 @@ __device__ __forceinline__ float ld_elem(const void* p, int64_t i) {
   return (float)reinterpret_cast<const T*>(p)[i];
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool SPLIT = false>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) {
   using TL = Tile<T, BM, BN>;
   constexpr int BK = TL::BK;
@@ -240,7 +282,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
       wait_ahead_barrier<STAGES - 2, PER>(ahead);
       if (t + STAGES - 1 < t_end) issue(t + STAGES - 1);
       const char* As = smem + ((t - t_begin) % STAGES) * TL::STAGE_BYTES;
-      compute_tile<T, BM, BN>(As, As + BM * 128, wm0, wn0, lane, acc);
+      compute_tile<T, BM, BN, SPLIT>(As, As + BM * 128, wm0, wn0, lane, acc);
     }
   }
   __syncthreads();
@@ -332,16 +374,16 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
   }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool SPLIT = false>
 int launch_typed(const GemmBatch& b, hipStream_t stream) {
   constexpr int lds = Tile<T, BM, BN>::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN, SPLIT>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
-  gemm_nt_kernel<T, BM, BN><<<dim3((unsigned)b.total_blocks), dim3(256), lds, stream>>>(b);
+  gemm_nt_kernel<T, BM, BN, SPLIT><<<dim3((unsigned)b.total_blocks), dim3(256), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -377,6 +419,11 @@ int launch_gemm(GemmBatch& b, int mode, GemmTile tile, hipStream_t stream) {
     if (tile == TILE_128x128) return launch_typed<bf16, 128, 128>(b, stream);
     if (tile == TILE_128x64) return launch_typed<bf16, 128, 64>(b, stream);
     return launch_typed<bf16, 64, 64>(b, stream);
+  }
+  if (mode == INF_MODE_BF16X3) {
+    if (tile == TILE_128x128) return launch_typed<float, 128, 128, true>(b, stream);
+    if (tile == TILE_128x64) return launch_typed<float, 128, 64, true>(b, stream);
+    return launch_typed<float, 64, 64, true>(b, stream);
   }
   if (tile == TILE_128x128) return launch_typed<float, 128, 128>(b, stream);
   if (tile == TILE_128x64) return launch_typed<float, 128, 64>(b, stream);

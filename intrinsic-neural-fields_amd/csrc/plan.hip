@@ -1076,7 +1076,7 @@ int inf_plan_create(const inf_mlp_desc* desc, int max_batch, inf_plan** plan) {
   INF_CHECK_ARG(d.hidden >= 64 && d.hidden % 64 == 0 && d.hidden <= 512,
                 "mlp_hidden_dim must be a multiple of 64 in [64, 512]");
   INF_CHECK_ARG(d.out_dim == 3, "out_dim must be 3 (RGB head)");
-  INF_CHECK_ARG(d.mode == INF_MODE_FP32 || d.mode == INF_MODE_BF16, "mode");
+  INF_CHECK_ARG(d.mode == INF_MODE_FP32 || d.mode == INF_MODE_BF16 || d.mode == INF_MODE_BF16X3, "mode");
   INF_CHECK_ARG(d.loss >= INF_LOSS_L2 && d.loss <= INF_LOSS_CAUCHY, "loss type");
   INF_CHECK_ARG(max_batch >= 1, "max_batch");
   inf_plan* p = new inf_plan();

@@ -16,10 +16,10 @@ LIB_PATH = os.environ.get("INF_LIB") or os.path.join(_HERE, "libinf_hip.so")
 # ---- constants (inf_hip.h) ---------------------------------------------------------
 INF_OK = 0
 DTYPE_F32, DTYPE_BF16, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
-MODE_FP32, MODE_BF16 = 0, 1
+MODE_FP32, MODE_BF16, MODE_BF16X3 = 0, 1, 2
 LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
 LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
-MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16}
+MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16, "bf16x3": MODE_BF16X3}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
 STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, STEP_PART1, STEP_PART2 = 1, 2, 4, 8, 16, 32  # inf_train_step
 ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF, ENC_PROJECTED = 0, 1, 2, 3, 4
