@@ -22,6 +22,7 @@
 #include "lgemm.hpp"
 #include "rchain.hpp"
 #include "blaslt.hpp"
+#include "ptab.hpp"
 
 namespace inf {
 
@@ -1418,10 +1419,12 @@ int inf_render(inf_plan* p, const inf_batch* batch, const int64_t* hit, const in
 int64_t inf_projected_rows(int64_t num_vertices) { return num_vertices <= 0 ? 0 : round_up(num_vertices, 128); }
 
 // out[v] = (W_0 E[v], W_y E[v]) in bf16: one plain NT GEMM over the packed table (A = E
-// [V][k_pad], B = [W_0; W_y] [2H][k_pad] bf16, C = out [.][2H]) through hipBLASLt; with
-// INF_PROJECT_GEMM=own the plan's grouped GEMM in 2^24-row slices.  The
-// last partial 128-row tile is staged through X0 (the GEMM reads whole tiles; out has
-// inf_projected_rows(V) rows, so its stores stay in bounds).
+// [V][k_pad], B = [W_0; W_y] [2H][k_pad] bf16, C = out [.][2H]) by the hand-written
+// 256 x 256-tile GEMM of ptab.hip (2H a multiple of 256); INF_PROJECT_GEMM=blaslt takes
+// hipBLASLt instead (and so does a 2H ptab.hip cannot tile), INF_PROJECT_GEMM=own the
+// plan's grouped GEMM in 2^24-row slices, the last partial 128-row tile staged through X0
+// (the GEMM reads whole tiles; out has inf_projected_rows(V) rows, so its stores stay in
+// bounds).
 int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void* out, inf_stream_t stream) {
   if (p == nullptr || !p->bound) {
     set_error("plan not bound");
@@ -1442,7 +1445,11 @@ int inf_project_table(inf_plan* p, const void* table, int64_t num_vertices, void
   for (int h = 0; h < 2; ++h)
     INF_HIP_TRY(hipMemcpyAsync(pcat + h * wbytes, p->shadow + w[h]->w_off, wbytes, hipMemcpyDeviceToDevice, st));
   const char* gsel = std::getenv("INF_PROJECT_GEMM");
-  const bool own = gsel != nullptr && std::string(gsel) == "own";
+  const std::string sel = gsel != nullptr ? gsel : "";
+  if (sel.empty() && (2 * H) % 256 == 0)  // ptab.hip: any row count, rows past V untouched
+    return launch_proj_gemm(reinterpret_cast<const bf16*>(table), num_vertices, k_pad,
+                            reinterpret_cast<const bf16*>(pcat), 2 * H, k_pad, reinterpret_cast<bf16*>(out), 2 * H, st);
+  const bool own = sel == "own";
   if (!own)  // hipBLASLt: any row count, rows past V untouched
     return blaslt_gemm_nt_bf16(table, k_pad, pcat, k_pad, out, 2 * H, num_vertices, 2 * H, k_pad, st);
   const int64_t full = num_vertices / 128 * 128, tail = num_vertices - full;

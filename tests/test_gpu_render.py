@@ -140,17 +140,19 @@ def test_render_projected_config_e():
     assert np.abs(img[hit_np[sample]] - p_ref).max() < 2e-2
 
 
-@pytest.mark.parametrize("gemm", ["hipblaslt", "own"])
-@pytest.mark.parametrize("V", [100, 256, 1000])
-def test_project_table_vs_torch(V, gemm, monkeypatch):
-    """inf_project_table against torch fp32 on the bf16 operands: whole tiles, a staged
-    tail tile (V % 128 != 0) and a table smaller than one tile; through hipBLASLt and
-    through the plan's own grouped GEMM (INF_PROJECT_GEMM=own)."""
-    if gemm == "own":
-        monkeypatch.setenv("INF_PROJECT_GEMM", "own")
+@pytest.mark.parametrize("gemm", ["ptab", "hipblaslt", "own"])
+@pytest.mark.parametrize("V,H", [(100, 256), (256, 256), (1000, 256), (5000, 256), (777, 128)])
+def test_project_table_vs_torch(V, H, gemm, monkeypatch):
+    """inf_project_table against torch fp32 on the bf16 operands: whole tiles, tail tiles
+    (V % 256 != 0) and a table smaller than one tile; through the hand-written 256 x 256
+    GEMM (csrc/ptab.hip, the default), hipBLASLt (INF_PROJECT_GEMM=blaslt) and the plan's
+    own grouped GEMM (INF_PROJECT_GEMM=own).  Every element within the bf16 rounding of
+    the fp32 product (2^-9 relative) plus summation-order slack; rows past V untouched."""
+    if gemm != "ptab":
+        monkeypatch.setenv("INF_PROJECT_GEMM", "own" if gemm == "own" else "blaslt")
     import model as M
     torch.manual_seed(1)
-    k, H = 512, 256
+    k = 512
     m = M.make_model({"k": k, "num_layers": 8, "mlp_hidden_dim": H, "skip_layer_idx": 4}).cuda()
     m.kernel_mode = "bf16"
     plan = m.hip_plan(1024)
@@ -166,8 +168,15 @@ def test_project_table_vs_torch(V, gemm, monkeypatch):
     Eb = T[:, :k].float()
     ref = torch.cat([Eb @ W.bfloat16().float().t() for W in W0], 1)
     got = P[:V].float()
-    err = (got - ref).abs().max().item()
-    assert err <= 1e-2 * ref.abs().max().item(), err
+    err = (got - ref).abs()
+    bound = 4e-3 * ref.abs() + 1e-4 * ref.abs().max()
+    assert bool((err <= bound).all()), (err - bound).max().item()
+    if gemm == "ptab" and P.shape[0] > V:  # rows past V keep what the caller put there
+        P2 = torch.full_like(P, 7.0)
+        plan.project_table(T, out=P2)
+        torch.cuda.synchronize()
+        assert bool((P2[V:] == 7.0).all())
+        assert torch.equal(P2[:V], P[:V])
 
 
 def test_render_projected_small_models(monkeypatch):
