@@ -6,12 +6,15 @@
 //   fp32 mode: v_mfma_f32_16x16x4_f32 (exact f32 FMA chain), k-tile BK = 32 (128-byte
 //              rows); a lane's 16-byte fragment read holds 4 consecutive k that feed 4
 //              consecutive MFMAs, so every operand read is one ds_read_b128 in both modes.
-//   bf16x3 mode (SPLIT): fp32 operands in memory and LDS exactly as the fp32 mode; each
-//              lane splits its 8 k of a 32-k tile into x = hi + lo (hi = bf16(x),
-//              lo = bf16(x - hi)) and the product is hi*hi + hi*lo + lo*hi on
-//              v_mfma_f32_16x16x32_bf16 with fp32 accumulation: ~2^-16 relative per product
-//              (the dropped lo*lo), at 3 bf16 MFMAs per 32 k instead of 8 fp32 ones of 4x the
-//              cycles (SURVEY.md §0.3's split-bf16 parity mode).
+//   split-bf16 modes (SPLIT 3 / 6): fp32 operands in memory and LDS exactly as the fp32
+//              mode; each lane splits its 8 k of a 32-k tile into bf16 parts and sums the
+//              significant cross products on v_mfma_f32_16x16x32_bf16 (fp32 accumulation,
+//              smallest terms first):
+//                3: x = hi + lo (+ 2^-16 |x|), hi*hi + hi*lo + lo*hi       -- ~2^-16 per product
+//                6: x = hi + mid + lo (+ 2^-24 |x|), the six terms down to
+//                   2^-16: hi*lo + lo*hi + mid*mid + hi*mid + mid*hi + hi*hi -- fp32-class
+//              at 3 / 6 bf16 MFMAs per 32 k instead of 8 fp32 ones of twice the cycles each
+//              (SURVEY.md §0.3's split-bf16 parity mode).
 // Operand tiles are staged global -> registers -> LDS with a double buffer: the loads
 // for k-tile t+1 are issued before the MFMAs of tile t and written to the other LDS
 // buffer afterwards (one barrier per k-tile).  LDS rows are 8 x 16-byte chunks stored
@@ -94,48 +97,60 @@ struct Tile {
   static constexpr int TM = WM / 16, TN = WN / 16;
 };
 
-// x = hi + lo + O(2^-17 |x|): hi, lo round to nearest (bf16 conversions)
-__device__ __forceinline__ void split_bf16(const f32x4& x0, const f32x4& x1, bf16x8& hi, bf16x8& lo) {
+// x = hi + lo + O(2^-16 |x|) (SPLIT 3) or hi + mid + lo + O(2^-24 |x|) (SPLIT 6); every
+// part rounds to nearest (bf16 conversions)
+template <int SPLIT>
+__device__ __forceinline__ void split_bf16(const f32x4& x0, const f32x4& x1, bf16x8 (&part)[SPLIT == 6 ? 3 : 2]) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    hi[e] = (bf16)x0[e];
-    hi[4 + e] = (bf16)x1[e];
-    lo[e] = (bf16)(x0[e] - (float)hi[e]);
-    lo[4 + e] = (bf16)(x1[e] - (float)hi[4 + e]);
+  for (int e = 0; e < 8; ++e) {
+    const float x = e < 4 ? x0[e] : x1[e - 4];
+    const bf16 h = (bf16)x;
+    const float r = x - (float)h;
+    const bf16 m = (bf16)r;
+    part[0][e] = h;
+    part[1][e] = m;
+    if constexpr (SPLIT == 6) part[2][e] = (bf16)(r - (float)m);
   }
 }
 
-template <typename T, int BM, int BN, bool SPLIT = false>
+template <typename T, int BM, int BN, int SPLIT = 0>
 __device__ __forceinline__ void compute_tile(const char* __restrict__ As, const char* __restrict__ Bs, int wm0,
                                              int wn0, int lane, f32x4 (&acc)[Tile<T, BM, BN>::TM][Tile<T, BM, BN>::TN]) {
   using TL = Tile<T, BM, BN>;
   constexpr int TM = TL::TM, TN = TL::TN;
   const int r16 = lane & 15;
   const int g = lane >> 4;
-  if constexpr (SPLIT) {
+  if constexpr (SPLIT != 0) {
     // lane (r16, g) holds k = 8 g .. 8 g + 7 of the 32-k tile (chunks 2 g, 2 g + 1) for A
     // and B alike -- one 16x16x32 MFMA per term covers the whole fp32 k-tile
-    static_assert(sizeof(T) == 4, "bf16x3 splits fp32 operands");
-    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+    static_assert(sizeof(T) == 4 && (SPLIT == 3 || SPLIT == 6), "split-bf16 of fp32 operands");
+    constexpr int NP = SPLIT == 6 ? 3 : 2;
+    bf16x8 ap[TM][NP], bp[TN][NP];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wm0 + i * 16 + r16;
-      split_bf16(*reinterpret_cast<const f32x4*>(As + swz(row, 2 * g)),
-                 *reinterpret_cast<const f32x4*>(As + swz(row, 2 * g + 1)), ah[i], al[i]);
+      split_bf16<SPLIT>(*reinterpret_cast<const f32x4*>(As + swz(row, 2 * g)),
+                        *reinterpret_cast<const f32x4*>(As + swz(row, 2 * g + 1)), ap[i]);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int row = wn0 + j * 16 + r16;
-      split_bf16(*reinterpret_cast<const f32x4*>(Bs + swz(row, 2 * g)),
-                 *reinterpret_cast<const f32x4*>(Bs + swz(row, 2 * g + 1)), bh[j], bl[j]);
+      split_bf16<SPLIT>(*reinterpret_cast<const f32x4*>(Bs + swz(row, 2 * g)),
+                        *reinterpret_cast<const f32x4*>(Bs + swz(row, 2 * g + 1)), bp[j]);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        f32x4 c = acc[i][j];
+        if constexpr (SPLIT == 6) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[i][0], bp[j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[i][2], bp[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[i][1], bp[j][1], c, 0, 0, 0);
+        }
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[i][1], bp[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[i][0], bp[j][1], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[i][0], bp[j][0], c, 0, 0, 0);
       }
   } else if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -185,7 +200,7 @@ __device__ __forceinline__ float ld_elem(const void* p, int64_t i) {
   return (float)reinterpret_cast<const T*>(p)[i];
 }
 
-template <typename T, int BM, int BN, bool SPLIT = false>
+template <typename T, int BM, int BN, int SPLIT = 0>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) {
   using TL = Tile<T, BM, BN>;
   constexpr int BK = TL::BK;
@@ -374,7 +389,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
   }
 }
 
-template <typename T, int BM, int BN, bool SPLIT = false>
+template <typename T, int BM, int BN, int SPLIT = 0>
 int launch_typed(const GemmBatch& b, hipStream_t stream) {
   constexpr int lds = Tile<T, BM, BN>::LDS_BYTES;
   static bool attr = false;
@@ -392,7 +407,7 @@ int launch_typed(const GemmBatch& b, hipStream_t stream) {
 
 int launch_gemm(GemmBatch& b, int mode, GemmTile tile, hipStream_t stream) {
   const int BM = tile_bm(tile), BN = tile_bn(tile);
-  const int BK = mode == INF_MODE_BF16 ? 64 : 32;
+  const int BK = mode == INF_MODE_BF16 ? 64 : 32;  // split modes stage fp32 tiles
   INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= GEMM_MAX_PROBLEMS, "gemm: problem count");
   int blocks = 0;
   for (int i = 0; i < b.nprob; ++i) {
@@ -421,9 +436,14 @@ int launch_gemm(GemmBatch& b, int mode, GemmTile tile, hipStream_t stream) {
     return launch_typed<bf16, 64, 64>(b, stream);
   }
   if (mode == INF_MODE_BF16X3) {
-    if (tile == TILE_128x128) return launch_typed<float, 128, 128, true>(b, stream);
-    if (tile == TILE_128x64) return launch_typed<float, 128, 64, true>(b, stream);
-    return launch_typed<float, 64, 64, true>(b, stream);
+    if (tile == TILE_128x128) return launch_typed<float, 128, 128, 3>(b, stream);
+    if (tile == TILE_128x64) return launch_typed<float, 128, 64, 3>(b, stream);
+    return launch_typed<float, 64, 64, 3>(b, stream);
+  }
+  if (mode == GEMM_MODE_BF16X6) {
+    if (tile == TILE_128x128) return launch_typed<float, 128, 128, 6>(b, stream);
+    if (tile == TILE_128x64) return launch_typed<float, 128, 64, 6>(b, stream);
+    return launch_typed<float, 64, 64, 6>(b, stream);
   }
   if (tile == TILE_128x128) return launch_typed<float, 128, 128>(b, stream);
   if (tile == TILE_128x64) return launch_typed<float, 128, 64>(b, stream);

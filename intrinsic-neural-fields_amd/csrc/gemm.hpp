@@ -59,7 +59,12 @@ enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_128x64 = 2 };
 inline int tile_bm(GemmTile t) { return t == TILE_64x64 ? 64 : 128; }
 inline int tile_bn(GemmTile t) { return t == TILE_128x128 ? 128 : 64; }
 
-// Fills tiles_m/tiles_n/block_begin/total_blocks and launches.  mode = INF_MODE_*.
+// GEMM arithmetic beyond the plan modes: fp32 operands as three bf16 parts, six products
+// (fp32-class; the split-bf16 plan mode's GEMMs that need it, plan.hip split_gemm_mode)
+constexpr int GEMM_MODE_BF16X6 = 16;
+
+// Fills tiles_m/tiles_n/block_begin/total_blocks and launches.  mode = INF_MODE_* or
+// GEMM_MODE_BF16X6.
 int launch_gemm(GemmBatch& batch, int mode, GemmTile tile, hipStream_t stream);
 
 }  // namespace inf

@@ -320,6 +320,21 @@ GemmProblem blank_problem() {
 
 int dtype_of(const inf_plan* p) { return p->mode == INF_MODE_BF16 ? INF_DTYPE_BF16 : INF_DTYPE_F32; }
 
+// GEMM arithmetic of a layered GEMM.  The split-bf16 plan mode runs the forward GEMMs on
+// 3 products (hi*hi + hi*lo + lo*hi: RGB ~1e-6 of the reference) and the backward ones on
+// 6 (three-part split): the dX chain sums long, cancelling dot products through every
+// layer, which amplifies a 2^-16 product error to ~1e-2 of a gradient's max at config B
+// (tests/test_gpu_bf16x3.py); INF_X3_{FWD,DX,DW}=3|6 override for experiments.
+enum GemmRole { ROLE_FWD = 0, ROLE_DX = 1, ROLE_DW = 2 };
+int gemm_mode(const inf_plan* p, GemmRole role) {
+  if (p->mode != INF_MODE_BF16X3) return p->mode;
+  static const char* names[3] = {"INF_X3_FWD", "INF_X3_DX", "INF_X3_DW"};
+  static const int defaults[3] = {3, 6, 6};
+  int terms = defaults[role];
+  if (const char* e = std::getenv(names[role])) terms = std::atoi(e) == 6 ? 6 : 3;
+  return terms == 6 ? GEMM_MODE_BF16X6 : INF_MODE_BF16X3;
+}
+
 // ---------------------------------------------------------------------------------
 int ensure_rowmajor(inf_plan* p, hipStream_t st);
 
@@ -396,7 +411,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
       q.CT = p->W(p->o_yt[l]);
       q.ldct = Bp;
     }
-    int rc = launch_gemm(gb, p->mode, tile, st);
+    int rc = launch_gemm(gb, gemm_mode(p, ROLE_FWD), tile, st);
     if (rc) return rc;
   }
   return INF_OK;
@@ -433,7 +448,7 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
     q.CT = p->W(p->o_dZT[l - 1]);
     q.ldct = Bp;
     q.colsum = p->W<float>(p->o_colsum[l - 1]);
-    int rc = launch_gemm(gb, p->mode, tile, st);
+    int rc = launch_gemm(gb, gemm_mode(p, ROLE_DX), tile, st);
     if (rc) return rc;
   }
   return run_weight_grads(p, Bp, st);
@@ -520,7 +535,7 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     std::memset(&gb, 0, sizeof(gb));
     gb.nprob = (int)std::min<size_t>(GEMM_MAX_PROBLEMS, probs.size() - i0);
     for (int j = 0; j < gb.nprob; ++j) gb.p[j] = probs[i0 + j];
-    int rc = launch_gemm(gb, p->mode, wtile, st);
+    int rc = launch_gemm(gb, gemm_mode(p, ROLE_DW), wtile, st);
     if (rc) return rc;
   }
   return INF_OK;
