@@ -25,6 +25,8 @@
 // chunks) and written out with 16-byte coalesced stores, rows past V skipped.
 // XCD-aware order: the 2 column tiles of a row panel are consecutive on one XCD (the
 // panel's table rows are read once from HBM and once from that XCD's L2).
+#include <cstdlib>
+
 #include "ptab.hpp"
 #include "c3common.hpp"
 
@@ -35,15 +37,24 @@ using c3::pack_bf16x2;
 using c3::u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int PT_BM = 256, PT_BN = 256, PT_BK = 32;
-constexpr int PT_THREADS = 512;
-constexpr int PT_STAGES = 4;
-constexpr int PT_STAGE_BYTES = (PT_BM + PT_BN) * PT_BK * 2;  // 32 KB
-constexpr int PT_LDS = PT_STAGES * PT_STAGE_BYTES;             // 128 KB (epilogue image: 128 KB)
-constexpr int PT_GLDS = PT_STAGE_BYTES / (PT_THREADS * 16);    // 4 per thread per stage
-static_assert(PT_BM * PT_BN * 2 <= PT_LDS, "epilogue image");
-
-__device__ __forceinline__ int pt_swz(int row) { return ((row >> 3) & 1) * 3; }
+template <int BM_, int BN_, int BK_, int STAGES_, int WAVES_M_>
+struct PT {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, STAGES = STAGES_;
+  static constexpr int THREADS = 512;                    // 8 waves
+  static constexpr int WAVES_M = WAVES_M_, WAVES_N = 8 / WAVES_M_;
+  static constexpr int WROWS = BM / WAVES_M, WCOLS = BN / WAVES_N;  // per wave: vertex rows, output columns
+  static constexpr int TI = WROWS / 16, TJ = WCOLS / 16;            // MFMA tiles per wave
+  static constexpr int ROWB = BK * 2;                    // stage row bytes (64 / 128)
+  static constexpr int CPR = ROWB / 16;                  // 16-byte chunks per stage row
+  static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
+  static constexpr int LDS = STAGES * STAGE_BYTES > BM * BN * 2 ? STAGES * STAGE_BYTES : BM * BN * 2;
+  static constexpr int GLDS = STAGE_BYTES / (THREADS * 16);  // direct-to-LDS loads per thread per stage
+  static_assert(STAGE_BYTES % (THREADS * 16) == 0 && LDS <= 160 * 1024 && TI >= 1 && TJ >= 1, "tile");
+  static_assert(BN % 8 == 0 && (BN / 8) <= 64, "epilogue image rows of at most 64 chunks");
+  // chunk swizzle of a stage row: 64-B rows c ^ 3 ((r >> 3) & 1) (chain.hip), 128-B rows
+  // c ^ ((r >> 1) & 7) (gemm.hip): conflict-free 16-row ds_read_b128 groups either way
+  __device__ static int swz(int row) { return BK == 32 ? ((row >> 3) & 1) * 3 : (row >> 1) & 7; }
+};
 
 // wait until at most N of this wave's direct-to-LDS loads are in flight, then the
 // workgroup barrier (one asm statement: no LDS access moves across it)
@@ -51,98 +62,115 @@ template <int N>
 __device__ __forceinline__ void pt_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// at most `ahead` stages (each G loads) in flight after the oldest, ahead <= A
+template <int A, int G>
+__device__ __forceinline__ void pt_wait_ahead(int ahead) {
+  if constexpr (A <= 0) {
+    pt_wait_barrier<0>();
+  } else {
+    if (ahead >= A) pt_wait_barrier<A * G>();
+    else pt_wait_ahead<A - 1, G>(ahead);
+  }
+}
 
-__global__ __launch_bounds__(PT_THREADS, 1) void proj_gemm_kernel(const bf16* __restrict__ A, int64_t M, int64_t lda,
-                                                                  const bf16* __restrict__ B, int N, int K,
-                                                                  bf16* __restrict__ C, int64_t ldc, int tiles_n,
-                                                                  int nblocks) {
+template <class P>
+__global__ __launch_bounds__(512, 1) void proj_gemm_kernel(const bf16* __restrict__ A, int64_t M, int64_t lda,
+                                                           const bf16* __restrict__ B, int N, int K,
+                                                           bf16* __restrict__ C, int64_t ldc, int tiles_n,
+                                                           int nblocks) {
+  constexpr int BM = P::BM, BN = P::BN, BK = P::BK, ROWB = P::ROWB, CPR = P::CPR, TI = P::TI, TJ = P::TJ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // bijective XCD remap: the blocks one XCD receives (orig % 8 equal) take consecutive tiles
   const int orig = (int)blockIdx.x;
   const int q = nblocks / 8, rr = nblocks % 8, xcd = orig % 8;
   const int bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
-  const int64_t m0 = (int64_t)tm * PT_BM;
-  const int n0 = tn * PT_BN;
+  const int64_t m0 = (int64_t)tm * BM;
+  const int n0 = tn * BN;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;  // rows 128 wr .., columns 64 wc ..
+  const int wr = wave / P::WAVES_N, wc = wave % P::WAVES_N;
   const int r16 = lane & 15, g4 = lane >> 4;
 
-  // ---- stage fill: thread t loads 16-byte pieces p = t + 512 i (i < 4) of the stage image:
-  // rows 0..255 = W rows n0.., 256..511 = table rows m0..; piece p is row p / 4, LDS chunk
-  // p % 4 holding source chunk (p % 4) ^ swz(row).  Table rows past M are clamped (their
+  // ---- stage fill: thread t loads 16-byte pieces p = t + 512 i of the stage image: rows
+  // 0..BN-1 = W rows n0.., BN.. = table rows m0..; piece p is row p / CPR, LDS chunk
+  // p % CPR holding source chunk (p % CPR) ^ swz(row).  Table rows past M are clamped (their
   // outputs are never stored).
-  const int KT = K / PT_BK;
-  const char* srcp[PT_GLDS];
+  const int KT = K / BK;
+  const char* srcp[P::GLDS];
 #pragma unroll
-  for (int i = 0; i < PT_GLDS; ++i) {
-    const int p = tid + PT_THREADS * i;
-    const int row = p >> 2, ch = (p & 3) ^ pt_swz(row & 255);
-    if (row < PT_BN) {
-      srcp[i] = reinterpret_cast<const char*>(B + (int64_t)(n0 + row) * K) + ch * 16;
+  for (int i = 0; i < P::GLDS; ++i) {
+    const int p = tid + P::THREADS * i;
+    const int row = p / CPR;
+    if (row < BN) {
+      srcp[i] = reinterpret_cast<const char*>(B + (int64_t)(n0 + row) * K) + (((p % CPR) ^ P::swz(row)) << 4);
     } else {
-      int64_t m = m0 + (row - PT_BN);
+      const int lr = row - BN;
+      int64_t m = m0 + lr;
       if (m >= M) m = M - 1;
-      srcp[i] = reinterpret_cast<const char*>(A + m * lda) + ch * 16;
+      srcp[i] = reinterpret_cast<const char*>(A + m * lda) + (((p % CPR) ^ P::swz(lr)) << 4);
     }
   }
   auto issue = [&](int t) {
-    char* st = smem + (t % PT_STAGES) * PT_STAGE_BYTES;
+    char* st = smem + (t % P::STAGES) * P::STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < PT_GLDS; ++i)
-      __builtin_amdgcn_global_load_lds(srcp[i] + (int64_t)t * PT_BK * 2, (lds_void*)(st + (wave + 8 * i) * 1024),
-                                       16, 0, 0);
+    for (int i = 0; i < P::GLDS; ++i)
+      __builtin_amdgcn_global_load_lds(srcp[i] + (int64_t)t * ROWB, (lds_void*)(st + (wave + 8 * i) * 1024), 16, 0, 0);
   };
 
-  f32x4 acc[4][8];  // [column tile j][row tile i]
+  f32x4 acc[TJ][TI];  // [output-column tile j][vertex-row tile i]
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < TJ; ++j)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < TI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-  for (int t = 0; t < PT_STAGES - 1; ++t)
+  for (int t = 0; t < P::STAGES - 1; ++t)
     if (t < KT) issue(t);
 
-  // a lane's operand: 16-byte chunk g4 of row (tile row + r16)
-  const int aw0 = wc * 64, bt0 = PT_BN + wr * 128;
+  const int aw0 = wc * P::WCOLS, bt0 = BN + wr * P::WROWS;
 #pragma unroll 1
   for (int t = 0; t < KT; ++t) {
-    const int ahead = KT - 1 - t;  // stages issued after t (at most 2 in flight here)
-    if (ahead >= 2) pt_wait_barrier<2 * PT_GLDS>();
-    else if (ahead == 1) pt_wait_barrier<PT_GLDS>();
-    else pt_wait_barrier<0>();
-    if (t + PT_STAGES - 1 < KT) issue(t + PT_STAGES - 1);
-    const char* st = smem + (t % PT_STAGES) * PT_STAGE_BYTES;
-    bf16x8 wf[4], ef[8];
+    // stage t landed (each wave's own loads, then the barrier); at most STAGES - 2 newer ones
+    // stay in flight across it
+    pt_wait_ahead<P::STAGES - 2, P::GLDS>(KT - 1 - t);
+    if (t + P::STAGES - 1 < KT) issue(t + P::STAGES - 1);
+    const char* st = smem + (t % P::STAGES) * P::STAGE_BYTES;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = aw0 + 16 * j + r16;
-      wf[j] = *reinterpret_cast<const bf16x8*>(st + row * 64 + ((g4 ^ pt_swz(row)) << 4));
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 wf[TJ], ef[TI];
+      const int c = kk * 4 + g4;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int row = aw0 + 16 * j + r16;
+        wf[j] = *reinterpret_cast<const bf16x8*>(st + row * ROWB + ((c ^ P::swz(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int lr = wr * P::WROWS + 16 * i + r16;
+        ef[i] = *reinterpret_cast<const bf16x8*>(st + (BN + lr) * ROWB + ((c ^ P::swz(lr)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], ef[i], acc[j][i], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = bt0 + 16 * i + r16;
-      ef[i] = *reinterpret_cast<const bf16x8*>(st + row * 64 + ((g4 ^ pt_swz(row & 255)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], ef[i], acc[j][i], 0, 0, 0);
   }
+  (void)bt0;
   __syncthreads();  // every wave's last fragment reads done before the image overwrites the ring
 
-  // ---- epilogue: lane holds output columns 64 wc + 16 j + 4 g4 + (0..3) of table row
-  // 128 wr + 16 i + r16; bf16 image [256][256], chunk c of row r at c ^ (r & 31)
-  auto img_off = [](int row, int col) { return row * 512 + ((((col >> 3) ^ (row & 31))) << 4) + ((col & 7) << 1); };
+  // ---- epilogue: lane holds output columns aw0 + 16 j + 4 g4 + (0..3) of tile row
+  // wr WROWS + 16 i + r16; bf16 image [BM][BN], chunk c of row r at c ^ (r & (BN/8 - 1))
+  constexpr int RB = BN * 2, RC = BN / 8;
+  auto img_off = [&](int row, int col) { return row * RB + ((((col >> 3) ^ (row & (RC - 1)))) << 4) + ((col & 7) << 1); };
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < TJ; ++j)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = wr * 128 + 16 * i + r16, col = wc * 64 + 16 * j + 4 * g4;
+    for (int i = 0; i < TI; ++i) {
+      const int row = wr * P::WROWS + 16 * i + r16, col = aw0 + 16 * j + 4 * g4;
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
       u32x2 w;
       w[0] = pack_bf16x2(acc[j][i][0], acc[j][i][1]);
@@ -151,13 +179,33 @@ __global__ __launch_bounds__(PT_THREADS, 1) void proj_gemm_kernel(const bf16* __
     }
   __syncthreads();
 #pragma unroll 4
-  for (int p = tid; p < PT_BM * (PT_BN / 8); p += PT_THREADS) {
-    const int row = p >> 5, c = p & 31;
+  for (int p = tid; p < BM * RC; p += P::THREADS) {
+    const int row = p / RC, c = p % RC;
     if (m0 + row < M) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(smem + row * 512 + ((c ^ (row & 31)) << 4));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(smem + row * RB + ((c ^ (row & (RC - 1))) << 4));
       *reinterpret_cast<u32x4*>(C + (m0 + row) * ldc + n0 + c * 8) = v;
     }
   }
+}
+
+template <class P>
+int launch_pt(const bf16* A, int64_t M, int64_t lda, const bf16* B, int N, int K, bf16* C, int64_t ldc,
+              hipStream_t stream) {
+  INF_CHECK_ARG(N % P::BN == 0 && K % P::BK == 0 && K >= P::BK, "proj_gemm: N / K not tile multiples");
+  const int64_t tiles_m = ceil_div(M, P::BM);
+  const int tiles_n = N / P::BN;
+  INF_CHECK_ARG(tiles_m * tiles_n < (int64_t)1 << 31, "proj_gemm: too many tiles");
+  const int nblocks = (int)(tiles_m * tiles_n);
+  static bool attr = false;
+  if (!attr) {
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)proj_gemm_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    P::LDS));
+    attr = true;
+  }
+  proj_gemm_kernel<P><<<dim3((unsigned)nblocks), dim3(P::THREADS), P::LDS, stream>>>(A, M, lda, B, N, K, C, ldc,
+                                                                                     tiles_n, nblocks);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
 }
 
 }  // namespace
@@ -165,22 +213,16 @@ __global__ __launch_bounds__(PT_THREADS, 1) void proj_gemm_kernel(const bf16* __
 int launch_proj_gemm(const bf16* A, int64_t M, int64_t lda, const bf16* B, int N, int K, bf16* C, int64_t ldc,
                      hipStream_t stream) {
   INF_CHECK_ARG(A != nullptr && B != nullptr && C != nullptr && M >= 1, "proj_gemm: operands");
-  INF_CHECK_ARG(N % PT_BN == 0 && K % PT_BK == 0 && K >= PT_BK, "proj_gemm: N must be a multiple of 256, K of 32");
   INF_CHECK_ARG(lda % 8 == 0 && ldc % 8 == 0 && lda >= K && ldc >= N, "proj_gemm: 16-byte aligned rows");
   INF_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "proj_gemm: 16-byte aligned operands");
-  const int64_t tiles_m = ceil_div(M, PT_BM);
-  const int tiles_n = N / PT_BN;
-  INF_CHECK_ARG(tiles_m * tiles_n < (int64_t)1 << 31, "proj_gemm: too many tiles");
-  const int nblocks = (int)(tiles_m * tiles_n);
-  static bool attr = false;
-  if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)proj_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, PT_LDS));
-    attr = true;
-  }
-  proj_gemm_kernel<<<dim3((unsigned)nblocks), dim3(PT_THREADS), PT_LDS, stream>>>(A, M, lda, B, N, K, C, ldc, tiles_n,
-                                                                                  nblocks);
-  INF_LAUNCH_CHECK();
-  return INF_OK;
+  // tile variants (INF_PTAB_TILE, tools/ptab_sweep.py): 0 = 256 x 256 x 32, 4 stages (default)
+  int v = 0;
+  if (const char* e = std::getenv("INF_PTAB_TILE")) v = std::atoi(e);
+  if (v == 1 && N % 256 == 0 && K % 64 == 0) return launch_pt<PT<256, 256, 64, 2, 2>>(A, M, lda, B, N, K, C, ldc, stream);
+  if (v == 2 && N % 128 == 0 && K % 64 == 0) return launch_pt<PT<256, 128, 64, 3, 4>>(A, M, lda, B, N, K, C, ldc, stream);
+  if (v == 3 && N % 256 == 0 && K % 64 == 0) return launch_pt<PT<128, 256, 64, 3, 2>>(A, M, lda, B, N, K, C, ldc, stream);
+  if (v == 4 && N % 128 == 0 && K % 32 == 0) return launch_pt<PT<256, 128, 32, 4, 4>>(A, M, lda, B, N, K, C, ldc, stream);
+  return launch_pt<PT<256, 256, 32, 4, 2>>(A, M, lda, B, N, K, C, ldc, stream);
 }
 
 }  // namespace inf
