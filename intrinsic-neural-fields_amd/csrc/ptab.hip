@@ -73,11 +73,14 @@ __device__ __forceinline__ void pt_wait_ahead(int ahead) {
   }
 }
 
-template <class P>
+// (a kernel template over an internal-linkage type gets no host stub from hipcc: the tile
+// parameters are template ints and the traits struct is named inside)
+template <int BM_, int BN_, int BK_, int STAGES_, int WAVES_M_>
 __global__ __launch_bounds__(512, 1) void proj_gemm_kernel(const bf16* __restrict__ A, int64_t M, int64_t lda,
                                                            const bf16* __restrict__ B, int N, int K,
                                                            bf16* __restrict__ C, int64_t ldc, int tiles_n,
                                                            int nblocks) {
+  using P = PT<BM_, BN_, BK_, STAGES_, WAVES_M_>;
   constexpr int BM = P::BM, BN = P::BN, BK = P::BK, ROWB = P::ROWB, CPR = P::CPR, TI = P::TI, TJ = P::TJ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // bijective XCD remap: the blocks one XCD receives (orig % 8 equal) take consecutive tiles
@@ -117,7 +120,13 @@ __global__ __launch_bounds__(512, 1) void proj_gemm_kernel(const bf16* __restric
     char* st = smem + (t % P::STAGES) * P::STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < P::GLDS; ++i)
-      __builtin_amdgcn_global_load_lds(srcp[i] + (int64_t)t * ROWB, (lds_void*)(st + (wave + 8 * i) * 1024), 16, 0, 0);
+    {
+      // (the source as its own variable: with the pointer arithmetic inside the builtin's
+      // argument list hipcc's host pass drops this kernel template's stub -- an undefined
+      // symbol at load time)
+      const char* src = srcp[i] + (int64_t)t * ROWB;
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(st + (wave + 8 * i) * 1024), 16, 0, 0);
+    }
   };
 
   f32x4 acc[TJ][TI];  // [output-column tile j][vertex-row tile i]
@@ -198,12 +207,12 @@ int launch_pt(const bf16* A, int64_t M, int64_t lda, const bf16* B, int N, int K
   const int nblocks = (int)(tiles_m * tiles_n);
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)proj_gemm_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    P::LDS));
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)proj_gemm_kernel<P::BM, P::BN, P::BK, P::STAGES, P::WAVES_M>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS));
     attr = true;
   }
-  proj_gemm_kernel<P><<<dim3((unsigned)nblocks), dim3(P::THREADS), P::LDS, stream>>>(A, M, lda, B, N, K, C, ldc,
-                                                                                     tiles_n, nblocks);
+  proj_gemm_kernel<P::BM, P::BN, P::BK, P::STAGES, P::WAVES_M>
+      <<<dim3((unsigned)nblocks), dim3(P::THREADS), P::LDS, stream>>>(A, M, lda, B, N, K, C, ldc, tiles_n, nblocks);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
