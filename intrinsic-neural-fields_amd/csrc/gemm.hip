@@ -22,6 +22,7 @@
 // over all bank slots of a 256-byte bank row pair (2-way at worst).
 // Epilogue: accumulators -> padded fp32 LDS tile -> bias / ReLU / ReLU-mask ->
 // coalesced row-major store, transposed store and per-tile column sums.
+#include <algorithm>
 #include <cstdlib>
 
 #include "gemm.hpp"
@@ -391,12 +392,15 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const GemmBatch batch) 
 
 template <typename T, int BM, int BN, int SPLIT = 0>
 int launch_typed(const GemmBatch& b, hipStream_t stream) {
-  constexpr int lds = Tile<T, BM, BN>::LDS_BYTES;
-  static bool attr = false;
-  if (!attr) {
+  int lds = Tile<T, BM, BN>::LDS_BYTES;
+  // INF_GEMM_LDS (experiments): reserve at least this much LDS per workgroup, e.g. > 80 KiB
+  // for one workgroup per CU
+  if (const char* e = std::getenv("INF_GEMM_LDS")) lds = std::max(lds, std::min(std::atoi(e), 160 * 1024));
+  static int attr = 0;
+  if (attr < lds) {
     INF_HIP_TRY(hipFuncSetAttribute((const void*)gemm_nt_kernel<T, BM, BN, SPLIT>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    attr = true;
+    attr = lds;
   }
   gemm_nt_kernel<T, BM, BN, SPLIT><<<dim3((unsigned)b.total_blocks), dim3(256), lds, stream>>>(b);
   INF_LAUNCH_CHECK();

@@ -324,14 +324,15 @@ int dtype_of(const inf_plan* p) { return p->mode == INF_MODE_BF16 ? INF_DTYPE_BF
 // hi*lo + lo*hi) put RGB within 1e-6 of the reference, but at config B a forward on them
 // leaves a gradient of layers.0 8.4e-3 of its max from the reference's (pre-activations
 // at rounding distance from the ReLU kink change their mask; measured with the backward on
-// 6 products too), while 6 products everywhere hold 1e-6 (tests/test_gpu_bf16x3.py,
-// profiles/r03/bf16x3_*_tests.log).  Default 6 for every role; INF_X3_{FWD,DX,DW}=3|6
-// override for experiments.
+// 6 products too), while a forward on 6 holds every gradient within 1.4e-5 of its max with
+// the backward GEMMs (dX, dW) on 3 (7.9e-6 with dX on 6; 8.7e-7 with all on 6:
+// tests/test_gpu_bf16x3.py, profiles/r03/bf16x3_*_tests.log).  Default: forward 6, dX 3,
+// dW 3; INF_X3_{FWD,DX,DW}=3|6 override for experiments.
 enum GemmRole { ROLE_FWD = 0, ROLE_DX = 1, ROLE_DW = 2 };
 int gemm_mode(const inf_plan* p, GemmRole role) {
   if (p->mode != INF_MODE_BF16X3) return p->mode;
   static const char* names[3] = {"INF_X3_FWD", "INF_X3_DX", "INF_X3_DW"};
-  static const int defaults[3] = {6, 6, 6};
+  static const int defaults[3] = {6, 3, 3};
   int terms = defaults[role];
   if (const char* e = std::getenv(names[role])) terms = std::atoi(e) == 6 ? 6 : 3;
   return terms == 6 ? GEMM_MODE_BF16X6 : INF_MODE_BF16X3;

@@ -224,14 +224,20 @@ int launch_proj_gemm(const bf16* A, int64_t M, int64_t lda, const bf16* B, int N
   INF_CHECK_ARG(A != nullptr && B != nullptr && C != nullptr && M >= 1, "proj_gemm: operands");
   INF_CHECK_ARG(lda % 8 == 0 && ldc % 8 == 0 && lda >= K && ldc >= N, "proj_gemm: 16-byte aligned rows");
   INF_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "proj_gemm: 16-byte aligned operands");
-  // tile variants (INF_PTAB_TILE, tools/ptab_sweep.py): 0 = 256 x 256 x 32, 4 stages (default)
-  int v = 0;
+  // tile variants (INF_PTAB_TILE, tools/ptab_sweep.py; 400k x 512 x 1024 on one MI355X,
+  // profiles/r03/ptab_sweep.log): 1 = 256 x 256 x 64, 2 stages (default: 0.442 ms, hipBLASLt
+  // 0.430), 0 = 256 x 256 x 32, 4 stages (0.489), 2 = 256 x 128 x 64, 3 stages (0.512),
+  // 3 = 128 x 256 x 64, 3 stages (0.496), 4 = 256 x 128 x 32, 4 stages (0.612)
+  int v = 1;
   if (const char* e = std::getenv("INF_PTAB_TILE")) v = std::atoi(e);
+  if (v == 5 && N % 256 == 0 && K % 64 == 0) return launch_pt<PT<256, 256, 64, 2, 4>>(A, M, lda, B, N, K, C, ldc, stream);
   if (v == 1 && N % 256 == 0 && K % 64 == 0) return launch_pt<PT<256, 256, 64, 2, 2>>(A, M, lda, B, N, K, C, ldc, stream);
   if (v == 2 && N % 128 == 0 && K % 64 == 0) return launch_pt<PT<256, 128, 64, 3, 4>>(A, M, lda, B, N, K, C, ldc, stream);
   if (v == 3 && N % 256 == 0 && K % 64 == 0) return launch_pt<PT<128, 256, 64, 3, 2>>(A, M, lda, B, N, K, C, ldc, stream);
   if (v == 4 && N % 128 == 0 && K % 32 == 0) return launch_pt<PT<256, 128, 32, 4, 4>>(A, M, lda, B, N, K, C, ldc, stream);
-  return launch_pt<PT<256, 256, 32, 4, 2>>(A, M, lda, B, N, K, C, ldc, stream);
+  if (v == 0 && N % 256 == 0) return launch_pt<PT<256, 256, 32, 4, 2>>(A, M, lda, B, N, K, C, ldc, stream);
+  INF_CHECK_ARG(N % 256 == 0 && K % 64 == 0, "proj_gemm: N must be a multiple of 256, K of 64");
+  return launch_pt<PT<256, 256, 64, 2, 2>>(A, M, lda, B, N, K, C, ldc, stream);
 }
 
 }  // namespace inf

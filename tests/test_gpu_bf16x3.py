@@ -1,6 +1,7 @@
 """The split-bf16 parity mode (INF_MODE_BF16X3): fp32 buffers and kernels
 of the fp32 mode, every GEMM inner product from bf16 parts of its operands on bf16 matrix
-cores (plan.hip gemm_mode: six products of a three-part split, ~2^-24 relative).  Held to the north_star's exact bar against the
+cores (plan.hip gemm_mode: the forward GEMMs on six products of a three-part split,
+~2^-24 relative; the backward ones on three of a two-part split, ~2^-16).  Held to the north_star's exact bar against the
 reference's own fixtures (G2 forward, G3 gradients / one Adam step, G4 20 Adam steps) and
 the fp32 oracle on device-resident rays: predicted RGB within 1e-4 abs, reduced gradients
 within 1e-4 of each tensor's max, Adam weights as the fp32 mode's tests hold them (a
@@ -53,7 +54,7 @@ def test_backward_bf16x3_golden(name, loss):
     print(name, loss, "grad err (of max)", worst)
 
 
-@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("R", "L1"), ("R", "L2")])
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1")])
 def test_fused_step_bf16x3_golden(name, loss):
     d = golden(f"g3_step_{name}_{loss}.npz")
     k, H, L, s = CFG[name]

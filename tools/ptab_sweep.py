@@ -22,7 +22,7 @@ E = torch.randn((V, k), generator=g, device="cuda")
 E /= E.max(0, keepdim=True).values - E.min(0, keepdim=True).values
 T = runtime.pack_table(E, plan.in_pad, torch.bfloat16)
 del E
-variants = ["0", "1", "2", "3", "4", "blaslt"]
+variants = ["1", "5", "0", "blaslt"]
 outs = {}
 times = {v: [] for v in variants}
 
@@ -40,7 +40,7 @@ for v in variants:
     setv(v)
     outs[v] = plan.project_table(T)
 torch.cuda.synchronize()
-ref = outs["0"][:V].float()
+ref = outs["1"][:V].float()
 for v in variants:
     d = (outs[v][:V].float() - ref).abs()
     print(v, "max |d| vs variant 0", float(d.max()), "rel", float((d / ref.abs().clamp_min(1e-3)).max()), flush=True)
