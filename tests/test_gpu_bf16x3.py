@@ -116,5 +116,9 @@ def test_train_step_rays_bf16x3_matches_oracle():
         np.testing.assert_allclose(pred.cpu().numpy(), p_ref, atol=1e-4)
         assert abs(plan.read_ctrl()["loss_sum"] / (3 * B) - loss) < 1e-5
     got = arena_to_dict(params, w, L, s)
+    # gradients agree to ~1e-5 of each tensor's max (test_backward_bf16x3_golden), so elements
+    # whose gradient is smaller than that may take Adam's opposite step (m / sqrt(v) = +-1 on
+    # step 1): seen 539 of layers.0.0.weight's 262,144 elements (0.2 %) moved by up to lr,
+    # every element within 2 lr steps
     for n in O.layer_names(L, s):
-        assert_adam_close(got[n], tr.w[n], lr=1e-4, steps=2, name=n)
+        assert_adam_close(got[n], tr.w[n], lr=1e-4, steps=2, name=n, frac=5e-3)
