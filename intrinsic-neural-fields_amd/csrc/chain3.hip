@@ -55,7 +55,15 @@ constexpr int C3_LDS_CAP = 160 * 1024;
 #ifndef C3_DEPTH
 #define C3_DEPTH 8
 #endif
-constexpr int C3BM = 16;  // rays per workgroup
+constexpr int C3BM = 16;  // rays per 16-row MFMA tile (= per workgroup at NR = 1)
+// Wide tiles (NR = C3_NR_WIDE ray tiles per workgroup, batches above CHAIN3_MAX_ROWS):
+// each fetched weight fragment feeds NR MFMAs instead of one, so the L2 -> CU weight
+// stream per ray drops NR-fold; the feature tile is streamed in C3_KC_WIDE-column chunks
+// (64 x 1024 bf16 would not fit beside the activation tiles) and the fragment ring is
+// shallower (each k block now carries NR times the MFMA work)
+#ifndef C3_DEPTH_WIDE
+#define C3_DEPTH_WIDE 3
+#endif
 // Cache policy of the table-row loads: non-temporal for tables larger than the MALL (rows
 // read once per step would evict the weight stream's L2 lines; config D's 4.1 GB table),
 // the default policy below it -- a MALL-resident table (config B's 102 MB) measured 0.8-1.0
@@ -64,34 +72,56 @@ constexpr int C3BM = 16;  // rays per workgroup
 constexpr int C3_CPOL_NT = 2;
 constexpr size_t C3_NT_TABLE_BYTES = (size_t)256 << 20;
 
-template <int H>
+// 1 if x != 0 else 0, as one v_min_u32 (asm: the compiler turns min(x, 1) back into a
+// compare whose lane mask lives in an SGPR pair)
+__device__ __forceinline__ unsigned nz1(unsigned x) {
+  unsigned r;
+  asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+template <int H, int NR>
 struct L3 {
-  static constexpr int BM = C3BM;
+  static constexpr int BM = C3BM * NR;          // rays per workgroup
   static constexpr int TN = H / (16 * C3_CW);  // 16-feature tiles per wave (2: H = 256, 1: H = 128)
   static constexpr int WN = H / C3_CW;          // features per wave
   static constexpr int UPL = H / 32;            // 32-deep k blocks per hidden layer (= per stream block)
   static constexpr int NT = H / 16;             // 16-row tiles per k block of a weight image
-  static constexpr int ACT_BYTES = BM * H * 2;
-  // activation / dZ tiles (act_off layout), double-buffered: epilogue p writes tile
-  // (p + 1) & 1, phase p reads tile p & 1, so one barrier per phase suffices
+  static constexpr int TILE_BYTES = C3BM * H * 2;  // one 16-ray activation tile
+  static constexpr int ACT_BYTES = NR * TILE_BYTES;
+  static constexpr int KC = NR == 1 ? C3_KC : C3_KC_WIDE;  // feature columns per chunk (XC)
+  // activation / dZ tiles (act_off layout per 16-ray tile), double-buffered: epilogue p
+  // writes tile (p + 1) & 1, phase p reads tile p & 1, so one barrier per phase suffices
+  // per-workgroup partials (sums over all BM rays) of the bias / output-layer gradients
+  // and the loss
   static constexpr int OFF_ACT = 0;
   static constexpr int OFF_CS = OFF_ACT + 2 * ACT_BYTES;  // [2][H] bias-gradient partials (epilogue p: p & 1)
   static constexpr int OFF_HW = OFF_CS + 2 * H * 4;       // [3][H] output-layer weight grad
   static constexpr int OFF_HB = OFF_HW + 3 * H * 4;       // [4]
   static constexpr int OFF_LS = OFF_HB + 16;              // [2] f64 loss / SSE
   static constexpr int OFF_PRED = OFF_LS + 16;            // [BM][3]
-  static constexpr int OFF_DZ = OFF_PRED + BM * 12;       // [waves][BM][3] head gradient
-  static constexpr int OFF_TGT = OFF_DZ + C3_CW * BM * 12;  // [BM][3] targets
+  // [waves][BM][3] head gradient; wide tiles: in the head phase's input activation tile,
+  // idle from barrier Bh1 on (all MFMAs of the phase and its Y^T copy are done)
+  static constexpr int OFF_DZ = OFF_PRED + BM * 12;
+  static constexpr int DZ_BYTES = NR == 1 ? C3_CW * BM * 12 : 0;
+  static constexpr int OFF_TGT = OFF_DZ + DZ_BYTES;       // [BM][3] targets
   static constexpr int OFF_ZP = OFF_TGT + BM * 12;        // [waves][BM][3] head partial sums
   static constexpr int OFF_RAY = OFF_ZP + C3_CW * BM * 12;  // [BM][4] vertex ids, [BM][3] ok
   static constexpr int OFF_RBARY = OFF_RAY + BM * 16 + BM * 12 + 16;  // [BM][3] barycentrics
   static constexpr int OFF_W7 = OFF_RBARY + BM * 12 + 16;  // [3][H] then b7[3]
   static constexpr int OFF_VEC = OFF_W7 + 3 * H * 4 + 16;  // biases [L-1][H], then Ly.bias [H]
-  // the feature tile holds kx columns: k_pad, or C3_KC when it is streamed in chunks
+  // the feature tile holds kx columns: k_pad, or KC when it is streamed in chunks.  Wide
+  // chunked tiles park the W_y x accumulators of phase 0 in the same region from barrier
+  // B2(0) on ([wave][NR TN][lane] 16-byte slots), when the last chunk is done with
+  static constexpr int ACCY_BYTES = C3_CW * 64 * NR * TN * 16;
   __host__ __device__ static int off_x(int L) { return OFF_VEC + L * H * 4; }
-  __host__ __device__ static int off_stamp(int L, int kx) { return off_x(L) + BM * kx * 2; }
-  static int lds_bytes(int L, int kx) { return off_stamp(L, kx) + (7 * C3_MAX_PHASES + 8) * 8; }
+  __host__ __device__ static int x_region(int kx, bool xc) {
+    return (NR > 1 && xc && ACCY_BYTES > BM * kx * 2) ? ACCY_BYTES : BM * kx * 2;
+  }
+  __host__ __device__ static int off_stamp(int L, int kx, bool xc) { return off_x(L) + x_region(kx, xc); }
+  static int lds_bytes(int L, int kx, bool xc) { return off_stamp(L, kx, xc) + (7 * C3_MAX_PHASES + 8) * 8; }
   static_assert(TN >= 1 && TN * 4 <= 8, "ReLU bits of a lane: at most 8 per layer");
+  static_assert(TN * 4 * NR <= 32, "ReLU bits of a lane: one 32-bit word per layer (wide tiles)");
   static_assert(OFF_LS % 8 == 0 && OFF_W7 % 16 == 0 && OFF_VEC % 16 == 0, "LDS alignment");
 };
 
@@ -103,11 +133,13 @@ struct L3 {
 // the chunk is resident and added in the skip layer's epilogue; each chunk is gathered
 // once, at its first block (two barriers: everyone is done with the previous chunk /
 // the new one is in LDS), and the store wave copies its X^T between them.
-template <int H, int LOSS, bool ENC, bool XC>
+// NR: 16-ray tiles per workgroup (1, or C3_NR_WIDE for large batches; not with ENC).
+template <int H, int LOSS, bool ENC, bool XC, int NR>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
-  using C = L3<H>;
+  using C = L3<H, NR>;
   constexpr int BM = C::BM, TN = C::TN, UPL = C::UPL;
-  constexpr int NV = TN * 4;  // accumulator values per lane
+  constexpr int NV = TN * 4;  // accumulator values per lane and ray tile
+  static_assert(NR == 1 || !ENC, "wide tiles: eigenfunction tables only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = a.L;
   const int k_pad = a.k_pad;
@@ -117,7 +149,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   float* hbs = reinterpret_cast<float*>(smem + C::OFF_HB);
   double* lss = reinterpret_cast<double*>(smem + C::OFF_LS);
   float* preds = reinterpret_cast<float*>(smem + C::OFF_PRED);
-  float* dzs = reinterpret_cast<float*>(smem + C::OFF_DZ);
+  float* dzs = reinterpret_cast<float*>(NR == 1 ? smem + C::OFF_DZ : smem + C::OFF_ACT + ((L - 2) & 1) * C::ACT_BYTES);
   float* tgs = reinterpret_cast<float*>(smem + C::OFF_TGT);
   float* zps = reinterpret_cast<float*>(smem + C::OFF_ZP);
   int* rvid = reinterpret_cast<int*>(smem + C::OFF_RAY);          // [BM][4]
@@ -125,7 +157,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   float* w7s = reinterpret_cast<float*>(smem + C::OFF_W7);
   float* vecs = reinterpret_cast<float*>(smem + C::OFF_VEC);
   char* xs = smem + C::off_x(L);  // gathered features [BM][kx] bf16 (tile_off layout)
-  const int kx = XC ? C3_KC : k_pad;  // columns resident in LDS
+  const int kx = XC ? C::KC : k_pad;  // columns resident in LDS
   const int xrow = kx * 2;
 
   const int tid = threadIdx.x;
@@ -140,7 +172,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   // wave 0 records everything; the last compute wave and the store wave their B1 arrivals
   const bool stamp_wg = a.stamps != nullptr && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
   if (stamp_wg && (wave == 0 || wave == C3_CW - 1 || wave == C3_CW))
-    stl = reinterpret_cast<unsigned long long*>(smem + C::off_stamp(L, kx));
+    stl = reinterpret_cast<unsigned long long*>(smem + C::off_stamp(L, kx, XC));
   const unsigned long long t_entry = stl != nullptr ? wall_clock64() : 0ull;
   auto stamp = [&](int i) {
     if (stl != nullptr) {
@@ -156,7 +188,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     const int wc = wave;
     const int t0 = wc * TN;  // the wave's first 16-feature tile
     // fragment ring: D k-blocks (D * TN KiB per wave) in flight
-    constexpr int D = C3_DEPTH < UPL ? C3_DEPTH : UPL;
+    constexpr int D0 = NR == 1 ? C3_DEPTH : C3_DEPTH_WIDE;
+    constexpr int D = D0 < UPL ? D0 : UPL;
     bf16x8 fr[D][TN];
     // buffer loads: descriptor per image in SGPRs, k-block offset in soffset, tile offset
     // as the immediate, one VGPR of lane offset -- no 64-bit address registers
@@ -370,9 +403,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
       }
     } else {
-      const int n0 = XC ? min(C3_KC, k_pad) : k_pad;
+      const int n0 = XC ? min(C::KC, k_pad) : k_pad;
       if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, std::true_type{}, 0, n0);
-      else if (a.gather_nt || XC) gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, std::true_type{}, 0, n0);
+      else if (a.gather_nt || (XC && NR == 1)) gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, std::true_type{}, 0, n0);
       else gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, std::false_type{}, 0, n0);
     }
     // every load issued so far has landed (the gather's data is in LDS and the fragment
@@ -385,17 +418,24 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     stamp(3 * nphase + 5);
 
     // ReLU bits of the lane's NV accumulator elements for layers 0..L-3 (bit j 4 + r), in
-    // registers: 64 / NV layers per word
+    // registers: 64 / NV layers per word.  Wide tiles (NR > 1): NR NV <= 32 bits per layer
+    // (tile n at bit n NV), kept as a stack -- the forward pushes layers 0..L-3 in order
+    // and the backward pops them in reverse (dX of layer l masks by Y_{l-1}), so every
+    // access is a static register index
     constexpr int MPW = 64 / NV;
     static_assert(2 * MPW >= CHAIN_MAX_HIDDEN - 1, "ReLU bit words");
     unsigned long long mbits[2] = {0ull, 0ull};
+    constexpr int MST = NR == 1 ? 1 : CHAIN_MAX_HIDDEN - 1;
+    unsigned mst[MST];
+#pragma unroll
+    for (int i = 0; i < MST; ++i) mst[i] = 0u;
     // B-operand slot offsets of this lane inside a k block of the activation tile (the
     // swizzle repeats every 4 k blocks)
     int aoffs[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) aoffs[q] = act_off(q, r16, g4) - q * 1024;
     const char* xlane = xs + r16 * xrow;
-    // the lane's accumulator element (j, r) is ray r16, feature feat(j) + r
+    // the lane's accumulator element (j, r) is ray r16 (of each ray tile), feature feat(j) + r
     auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
     // activations / dZ -> the LDS tile: one 16-byte write per k block (tile pair), 8 bytes
     // for a lone tile (H = 128: a wave owns half a k block)
@@ -423,6 +463,32 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       }
     };
+    // the inverse of put_act for this lane's own slots
+    auto get_act = [&](float (&v)[TN][4], const char* act) {
+      auto unpack = [](unsigned w, float& lo, float& hi) {
+        lo = __builtin_bit_cast(float, w << 16);
+        hi = __builtin_bit_cast(float, w & 0xFFFF0000u);
+      };
+      if constexpr (TN % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; j += 2) {
+          const u32x4 w = *reinterpret_cast<const u32x4*>(act + act_off((t0 + j) >> 1, r16, g4));
+          unpack(w[0], v[j][0], v[j][1]);
+          unpack(w[1], v[j][2], v[j][3]);
+          unpack(w[2], v[j + 1][0], v[j + 1][1]);
+          unpack(w[3], v[j + 1][2], v[j + 1][3]);
+        }
+      } else {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int t = t0 + j;
+          const u32x2 w = *reinterpret_cast<const u32x2*>(act + act_off(t >> 1, r16, g4) + 8 * (t & 1));
+          unpack(w[0], v[j][0], v[j][1]);
+          unpack(w[1], v[j][2], v[j][3]);
+        }
+      }
+    };
     // sums over the 16 rays of per-lane values v[j][r] -> dst[feature] (lane r16 < NV
     // holds value r16 after the reduce-scatter)
     auto ray_sums_to = [&](const float (&v)[TN][4], float* dst) {
@@ -436,14 +502,35 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (r16 < NV) dst[feat(idx >> 2) + (idx & 3)] = s;
     };
 
-    f32x4 acc[TN], accy[TN];  // accy: W_y x of the chunked schedule (XC)
+    // The chunked schedule's second accumulator set (W_y x, phase 0 .. the skip layer):
+    // ACCY -- in registers (accy, NR = 1); PARK -- wide tiles, whose NR-fold sets leave no
+    // registers for it: during phase 0 the set not being accumulated waits in the lane's
+    // own slots of the two activation tiles (unused until phase 0's epilogue; slot (j, n)
+    // = tile j, ray tile n, the wave's k block -- exactly the slots the wave's own
+    // epilogue writes later), exchanged at every C3F_SWAP block; at the end of phase 0
+    // W_y x moves to the feature-tile region (free once every wave and the store wave are
+    // past the last chunk: barrier BX) until the skip layer's epilogue reads it back
+    constexpr bool ACCY = XC && NR == 1;
+    constexpr bool PARK = XC && NR > 1;
+    static_assert(!PARK || TN == 2, "wide chunked tiles: one 16-byte slot per ray tile and tile pair");
+    auto park_slot = [&](int n, int j) -> char* { return act + j * C::ACT_BYTES + n * C::TILE_BYTES + wc * 1024 + lane * 16; };
+    auto wy_slot = [&](int n, int j) -> char* { return xs + ((wc * NR * TN + n * TN + j) * 64 + lane) * 16; };
+    f32x4 acc[NR][TN], accy[ACCY ? NR : 1][TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NR; ++n)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) accy[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TN; ++j) acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < TN; ++j) accy[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PARK) {
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) *reinterpret_cast<f32x4*>(park_slot(n, j)) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
-#pragma unroll 1
-    for (int i = 0; i < a.nblk; ++i) {
+    // one block of the weight stream (and the epilogue of the phase it ends)
+    auto run_block = [&](int i) {
       const C3Block& B = a.blk[i];
       const C3Block& Bn = a.blk[i + 1 < a.nblk ? i + 1 : i];
       if (i == 0 || a.blk[i - 1].last) stamp(1 + 3 * B.phase);
@@ -453,19 +540,38 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         if (B.flags & C3F_GATHER) {
           const int c = B.flags >> C3F_CHUNK_SHIFT;
           lbar();  // G1: every wave is done with the previous chunk (and the store wave with its X^T)
-          const int nc = min(C3_KC, k_pad - c * C3_KC);
-          // chunked tiles (k_pad > C3_KC) are the large tables: non-temporal rows
-          if (a.table_big) gather_cols(std::integral_constant<int, 2>{}, std::true_type{}, std::true_type{}, c * C3_KC, nc);
-          else gather_cols(std::integral_constant<int, 2>{}, std::false_type{}, std::true_type{}, c * C3_KC, nc);
+          const int nc = min(C::KC, k_pad - c * C::KC);
+          // chunked tiles (k_pad > C3_KC) are the large tables: non-temporal rows (wide
+          // tiles: the MALL policy decides, as for the whole-tile gather); one load set
+          // per thread in the wide variant (four accumulator sets are live)
+          constexpr int GRX = NR == 1 ? 2 : 1;
+#ifdef EXP_NOGATHER
+          if (NR > 1) {} else
+#endif
+          if (a.table_big)
+            gather_cols(std::integral_constant<int, GRX>{}, std::true_type{}, std::true_type{}, c * C::KC, nc);
+          else if (NR == 1 || a.gather_nt)
+            gather_cols(std::integral_constant<int, GRX>{}, std::false_type{}, std::true_type{}, c * C::KC, nc);
+          else
+            gather_cols(std::integral_constant<int, GRX>{}, std::false_type{}, std::false_type{}, c * C::KC, nc);
           lbar();  // G2: chunk c in LDS
         }
         if (B.flags & C3F_SWAP) {
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const f32x4 t = acc[j];
-            acc[j] = accy[j];
-            accy[j] = t;
-          }
+          for (int n = 0; n < NR; ++n)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              if constexpr (PARK) {
+                f32x4* q = reinterpret_cast<f32x4*>(park_slot(n, j));
+                const f32x4 t = *q;
+                *q = acc[n][j];
+                acc[n][j] = t;
+              } else {
+                const f32x4 t = acc[n][j];
+                acc[n][j] = accy[n][j];
+                accy[n][j] = t;
+              }
+            }
         }
       }
       const __amdgpu_buffer_rsrc_t crs = rsrc_of(B.img);
@@ -478,34 +584,70 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       // a pointer ternary inside the unrolled loop had compiled to scalar branches between
       // the MFMAs.  X: chunk (m 4 + g4) ^ r16 of row r16 with m = ak0 + kb, and ak0 a
       // multiple of UPL keeps the xor inside the k-block's 32-chunk (UPL = 8) / 16-chunk
-      // (UPL = 4) span: xlane + 64 ak0 + ((kb 4 + g4) ^ r16) 16
+      // (UPL = 4) span: xlane + 64 ak0 + ((kb 4 + g4) ^ r16) 16.  Ray tile n: 16 rows of X
+      // / one activation tile further
       const int fx = from_x ? 1 : 0;
       const char* bbase = from_x ? xlane + ak0 * 64 : act_in;
-      auto bread = [&](int kb) -> bf16x8 {
+      const int nstride = from_x ? 16 * xrow : C::TILE_BYTES;
+      auto bread = [&](int kb, int n) -> bf16x8 {
         const int xo = ((kb * 4 + g4) ^ r16) << 4;
         const int ao = kb * 1024 + aoffs[kb & 3];
-        return *reinterpret_cast<const bf16x8*>(bbase + ao + fx * (xo - ao));
+        return *reinterpret_cast<const bf16x8*>(bbase + n * nstride + ao + fx * (xo - ao));
       };
-      // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
-      // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
-      // latency is exposed at every k-block, behind only TN MFMAs)
-      // (not in the chunked variant: its second accumulator set leaves no room -- it spills)
-      constexpr bool BPF = !XC;
-      bf16x8 bq[2];
-      if constexpr (BPF) bq[0] = bread(0);
+      if constexpr (NR == 1) {
+        // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
+        // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
+        // latency is exposed at every k-block, behind only TN MFMAs)
+        // (not in the chunked variant: its second accumulator set leaves no room -- it spills)
+        constexpr bool BPF = !XC;
+        bf16x8 bq[2];
+        if constexpr (BPF) bq[0] = bread(0, 0);
 #pragma unroll
-      for (int kb = 0; kb < UPL; ++kb) {
-        if constexpr (BPF) {
-          if (kb + 1 < UPL) bq[(kb + 1) & 1] = bread(kb + 1);
+        for (int kb = 0; kb < UPL; ++kb) {
+          if constexpr (BPF) {
+            if (kb + 1 < UPL) bq[(kb + 1) & 1] = bread(kb + 1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          const bf16x8 bv = BPF ? bq[kb & 1] : bread(kb, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[0][j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
           __builtin_amdgcn_sched_barrier(0);
         }
-        const bf16x8 bv = BPF ? bq[kb & 1] : bread(kb);
+      } else {
+        // wide tiles: NR TN MFMAs per k block; ray tile n's operand for k block kb + 1 is
+        // read right after its MFMAs of kb (one operand register set, rolling)
+#ifdef C3_WIDE_NOBQ
+        constexpr bool RB = false;
+#else
+        constexpr bool RB = true;
+#endif
+        auto mfma_block = [&](f32x4 (&tgt)[NR][TN]) {
+          bf16x8 bq[NR];
+          if constexpr (RB) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[j], 0, 0, 0);
+            for (int n = 0; n < NR; ++n) bq[n] = bread(0, n);
+          }
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
-        __builtin_amdgcn_sched_barrier(0);
+          for (int kb = 0; kb < UPL; ++kb) {
+#pragma unroll
+            for (int n = 0; n < NR; ++n) {
+              const bf16x8 bv = RB ? bq[n] : bread(kb, n);
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                tgt[n][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, tgt[n][j], 0, 0, 0);
+              if (RB && kb + 1 < UPL) bq[n] = bread(kb + 1, n);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        };
+        mfma_block(acc);
       }
 #ifdef C3_STREAM_ONLY  // diagnostics: the weight stream and MFMAs alone (wrong results);
                       // with C3_STREAM_BARRIERS also the two barriers per phase
@@ -516,9 +658,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         lbar();
 #endif
       }
-      continue;
+      return;
 #endif
-      if (!B.last) continue;
+      if (!B.last) return;
 
       // ---- epilogue of phase p ---------------------------------------------------------
       const int p = B.phase;
@@ -527,98 +669,146 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       // were last read in phase p - 1 / copied by the store wave before B2(p - 1)
       char* act_out = act + ((p + 1) & 1) * C::ACT_BYTES;
       float* cs_out = csb + (p & 1) * H;
+      if constexpr (PARK) {
+        if (p == 0) {
+          lbar();  // BX: every wave and the store wave are done with the last feature chunk
+#pragma unroll
+          for (int n = 0; n < NR; ++n)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              *reinterpret_cast<f32x4*>(wy_slot(n, j)) = *reinterpret_cast<const f32x4*>(park_slot(n, j));
+        }
+      }
       if (p < nfwd) {
-        // forward of layer l: bias (+ Ly.bias at the skip layer) + ReLU -> tile, bits
+        // forward of layer l: bias (+ Ly.bias at the skip layer) + ReLU -> tile, bits; one
+        // ray tile at a time (wide tiles: keeps one tile's activations live, not NR)
         const int l = p;
         const bool skip = l == a.s;
         const bool last = l == L - 2;
-        // + bias (+ the chunked schedule's W_y x and Ly.bias at the skip layer), in the
-        // layered GEMM epilogue's order (the bias last: the fp32 sums match it)
+        unsigned bits = 0;
+        float hq1[TN][4];  // NR = 1: the head's activations stay in registers
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
-          if (skip) {
-            const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
+        for (int n = 0; n < NR; ++n) {
+          // + bias (+ the chunked schedule's W_y x and Ly.bias at the skip layer), in the
+          // layered GEMM epilogue's order (the bias last: the fp32 sums match it).  Wide
+          // chunked tiles read W_y x back from this lane's own LDS slots
+          float hq[TN][4];  // bf16-rounded activations as f32
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float v = acc[j][r];
-              if constexpr (XC) v += accy[j][r];
-              acc[j][r] = (v + bv[r]) + yv[r];
+          for (int j = 0; j < TN; ++j) {
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+            f32x4 z = acc[n][j];
+            if (skip) {
+              const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (L - 1) * H + feat(j));
+              f32x4 wy = f32x4{0.f, 0.f, 0.f, 0.f};
+              if constexpr (ACCY) wy = accy[n][j];
+              else if constexpr (PARK) wy = *reinterpret_cast<const f32x4*>(wy_slot(n, j));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float v = z[r];
+                if constexpr (XC) v += wy[r];
+                z[r] = (v + bv[r]) + yv[r];
+              }
+            } else {
+              z += bv;
             }
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+              const unsigned w = pack_bf16x2(relu1(z[r]), relu1(z[r + 1]));
+              hq[j][r] = __builtin_bit_cast(float, w << 16);
+              hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
+              // h > 0 <=> the bf16 bits without the sign are nonzero (ReLU left no negatives
+              // but possibly a -0)
+              if constexpr (NR == 1) {
+                bits |= ((w & 0x7FFFu) != 0u ? 1u : 0u) << (n * NV + j * 4 + r);
+                bits |= ((w & 0x7FFF0000u) != 0u ? 1u : 0u) << (n * NV + j * 4 + r + 1);
+              } else {  // v_min_u32 x, 1: the flag in a VGPR (NR TN 8 compares would each
+                        // take an SGPR pair, and spill)
+                bits |= nz1(w & 0x7FFFu) << (n * NV + j * 4 + r);
+                bits |= nz1(w & 0x7FFF0000u) << (n * NV + j * 4 + r + 1);
+              }
+            }
+          }
+          if (!last) {
+            put_act(hq, act_out + n * C::TILE_BYTES);
           } else {
-            acc[j] += bv;
+            // ---- head on the registers of the last hidden layer (model.py:89-94) --------
+            // z partials over this lane's features, then over the 4 row groups (a wave's WN
+            // features), then over the waves through LDS
+#pragma unroll
+            for (int o = 0; o < 3; ++o) {
+              float z = 0.f;
+#pragma unroll
+              for (int j = 0; j < TN; ++j) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
+              }
+              z = col_sum4(z);
+              if (g4 == 0) zps[(wc * BM + 16 * n + r16) * 3 + o] = z;
+            }
+            // wide tiles: the activations wait in this lane's own slots of the output tile
+            // (bf16, exact: they are bf16-rounded) until the head backward overwrites them
+            if constexpr (NR == 1) {
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hq1[j][r] = hq[j][r];
+            } else {
+              put_act(hq, act_out + n * C::TILE_BYTES);
+            }
           }
         }
-        float hq[TN][4];  // bf16-rounded activations as f32
-        unsigned bits = 0;
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            const unsigned w = pack_bf16x2(relu1(acc[j][r]), relu1(acc[j][r + 1]));
-            hq[j][r] = __builtin_bit_cast(float, w << 16);
-            hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
-            // h > 0 <=> the bf16 bits without the sign are nonzero (ReLU left no negatives
-            // but possibly a -0)
-            bits |= ((w & 0x7FFFu) != 0u ? 1u : 0u) << (j * 4 + r);
-            bits |= ((w & 0x7FFF0000u) != 0u ? 1u : 0u) << (j * 4 + r + 1);
-          }
         if (!last) {
-          if (l < MPW) mbits[0] |= (unsigned long long)bits << (NV * l);
-          else mbits[1] |= (unsigned long long)bits << (NV * (l - MPW));
-          put_act(hq, act_out);
-        } else {
-          // ---- head on the registers of the last hidden layer (model.py:89-94) ----------
-          // z partials over this lane's features, then over the 4 row groups (a wave's WN
-          // features), then over the waves through LDS
+          if constexpr (NR == 1) {
+            if (l < MPW) mbits[0] |= (unsigned long long)bits << (NV * l);
+            else mbits[1] |= (unsigned long long)bits << (NV * (l - MPW));
+          } else {
 #pragma unroll
-          for (int o = 0; o < 3; ++o) {
-            float z = 0.f;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
-#pragma unroll
-              for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
-            }
-            z = col_sum4(z);
-            if (g4 == 0) zps[(wc * BM + r16) * 3 + o] = z;
+            for (int i = MST - 1; i > 0; --i) mst[i] = mst[i - 1];
+            mst[0] = bits;
           }
+        } else {
           lbar();  // Bh1: per-wave head partial sums complete
           // sigmoid, loss and dL/dz (model.py:89-94, config.py:113-122, trainer.py:76):
-          // every compute wave computes all BM x 3 of them (one lane each) into its own
-          // copy of dz, so only same-wave LDS ordering is needed, no second barrier
+          // every compute wave computes all BM x 3 of them (one lane each per 64) into its
+          // own copy of dz, so only same-wave LDS ordering is needed, no second barrier
           {
             float* dzw = dzs + wc * BM * 3;
             float lsum = 0.f, ssum = 0.f;
-            if (lane < BM * 3) {
-              const int b = b0 + lane / 3, o = lane % 3;
-              float z = w7s[3 * H + o];
+            // (not unrolled: the unrolled copies' LDS addresses were hoisted to the kernel
+            // entry and spilled -- a scratch reload drains the fragment queue)
+#pragma unroll 1
+            for (int e0 = 0; e0 < BM * 3; e0 += 64) {
+              const int e = e0 + lane;
+              if (e < BM * 3) {
+                const int b = b0 + e / 3, o = e % 3;
+                float z = w7s[3 * H + o];
 #pragma unroll
-              for (int w = 0; w < C3_CW; ++w) z += zps[w * BM * 3 + lane];
-              const float pv = 1.f / (1.f + expf(-z));
-              float dz = 0.f;
-              if (b < a.batch) {
-                const float d = pv - tgs[lane];
-                float lv, g;
-                if constexpr (LOSS == INF_LOSS_L2) {
-                  lv = d * d;
-                  g = 2.f * d;
-                } else if constexpr (LOSS == INF_LOSS_L1) {
-                  lv = fabsf(d);
-                  g = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-                } else {
-                  const float qq = d * d / C3_CAUCHY_C2;
-                  lv = C3_CAUCHY_C2 * logf(1.f + qq);
-                  g = 2.f * d / (1.f + qq);
+                for (int w = 0; w < C3_CW; ++w) z += zps[w * BM * 3 + e];
+                const float pv = 1.f / (1.f + expf(-z));
+                float dz = 0.f;
+                if (b < a.batch) {
+                  const float d = pv - tgs[e];
+                  float lv, g;
+                  if constexpr (LOSS == INF_LOSS_L2) {
+                    lv = d * d;
+                    g = 2.f * d;
+                  } else if constexpr (LOSS == INF_LOSS_L1) {
+                    lv = fabsf(d);
+                    g = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+                  } else {
+                    const float qq = d * d / C3_CAUCHY_C2;
+                    lv = C3_CAUCHY_C2 * logf(1.f + qq);
+                    g = 2.f * d / (1.f + qq);
+                  }
+                  dz = (g * a.inv_count) * (1.f - pv) * pv;
+                  lsum += lv;
+                  ssum += d * d;
                 }
-                dz = (g * a.inv_count) * (1.f - pv) * pv;
-                lsum = lv;
-                ssum = d * d;
+                dzw[e] = dz;
+                if (wc == 0) preds[e] = pv;
               }
-              dzw[lane] = dz;
-              if (wc == 0) preds[lane] = pv;
             }
-            static_assert(C3BM * 3 <= 64, "one lane per (ray, output)");
             if (wc == 0) {  // all 64 lanes active for the cross-lane sums
               lsum = col_sum4(row_sum16(lsum));
               ssum = col_sum4(row_sum16(ssum));
@@ -630,64 +820,100 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's dz writes
           }
           // head backward in registers: dZ_{L-2} = (dz W7) * (h > 0), its ray sums, and the
-          // output layer's weight-gradient partials sum_rays dz_o * h
-          float dzr[3];
+          // output layer's weight-gradient partials sum_rays dz_o * h (the ray tiles summed
+          // in registers first: one partial per workgroup)
+          float cst[TN][4], hst[3][TN][4], dbs[3];
 #pragma unroll
-          for (int o = 0; o < 3; ++o) dzr[o] = dzs[wc * BM * 3 + r16 * 3 + o];
-          // the output bias partials (sum over the 16 rays of dz_o): a DPP row sum in wave 0
+          for (int n = 0; n < NR; ++n) {
+            float dzr[3];
+#pragma unroll
+            for (int o = 0; o < 3; ++o) dzr[o] = dzs[wc * BM * 3 + (16 * n + r16) * 3 + o];
+#pragma unroll
+            for (int o = 0; o < 3; ++o) dbs[o] = n == 0 ? dzr[o] : dbs[o] + dzr[o];
+            float hq[TN][4];
+            if constexpr (NR == 1) {
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hq[j][r] = hq1[j][r];
+            } else {
+              get_act(hq, act_out + n * C::TILE_BYTES);
+            }
+            float gv[TN][4];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const f32x4 w0 = *reinterpret_cast<const f32x4*>(w7s + 0 * H + feat(j));
+              const f32x4 w1 = *reinterpret_cast<const f32x4*>(w7s + 1 * H + feat(j));
+              const f32x4 w2 = *reinterpret_cast<const f32x4*>(w7s + 2 * H + feat(j));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float g = fmaf(dzr[2], w2[r], fmaf(dzr[1], w1[r], dzr[0] * w0[r]));
+                gv[j][r] = hq[j][r] > 0.f ? g : 0.f;
+              }
+            }
+            put_act(gv, act_out + n * C::TILE_BYTES);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                cst[j][r] = n == 0 ? gv[j][r] : cst[j][r] + gv[j][r];
+#pragma unroll
+                for (int o = 0; o < 3; ++o)
+                  hst[o][j][r] = n == 0 ? dzr[o] * hq[j][r] : fmaf(dzr[o], hq[j][r], hst[o][j][r]);
+              }
+          }
+          // the output bias partials (sum over the rays of dz_o): a DPP row sum in wave 0
           // (lane r16 holds ray r16's dz) instead of a 16-deep dependent LDS loop
           if (wc == 0) {
 #pragma unroll
             for (int o = 0; o < 3; ++o) {
-              const float db = row_sum16(dzr[o]);
+              const float db = row_sum16(dbs[o]);
               if (lane == 0) hbs[o] = db;
             }
           }
-          float gv[TN][4];
+          ray_sums_to(cst, cs_out);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const f32x4 w0 = *reinterpret_cast<const f32x4*>(w7s + 0 * H + feat(j));
-            const f32x4 w1 = *reinterpret_cast<const f32x4*>(w7s + 1 * H + feat(j));
-            const f32x4 w2 = *reinterpret_cast<const f32x4*>(w7s + 2 * H + feat(j));
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float g = fmaf(dzr[2], w2[r], fmaf(dzr[1], w1[r], dzr[0] * w0[r]));
-              gv[j][r] = hq[j][r] > 0.f ? g : 0.f;
-            }
-          }
-          put_act(gv, act_out);
-          ray_sums_to(gv, cs_out);
-#pragma unroll
-          for (int o = 0; o < 3; ++o) {
-            float hv[TN][4];
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) hv[j][r] = dzr[o] * hq[j][r];
-            ray_sums_to(hv, hws + o * H);
-          }
+          for (int o = 0; o < 3; ++o) ray_sums_to(hst[o], hws + o * H);
         }
       } else {
         // dX of layer l masked by Y_{l-1} > 0 -> dZ_{l-1} (tile, bias partial)
         const int l = (L - 2) - (p - nfwd);
-        const unsigned bits = (unsigned)((l - 1 < MPW ? mbits[0] >> (NV * (l - 1)) : mbits[1] >> (NV * (l - 1 - MPW))) &
-                                         ((1u << NV) - 1));
-        float v[TN][4];
+        unsigned bits;
+        if constexpr (NR == 1) {
+          bits = (unsigned)((l - 1 < MPW ? mbits[0] >> (NV * (l - 1)) : mbits[1] >> (NV * (l - 1 - MPW))) &
+                            ((1u << NV) - 1));
+        } else {
+          bits = mst[0];
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+          for (int i = 0; i + 1 < MST; ++i) mst[i] = mst[i + 1];
+        }
+        float cst[TN][4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[j][r] = ((bits >> (j * 4 + r)) & 1u) ? acc[j][r] : 0.f;
-        put_act(v, act_out);
-        ray_sums_to(v, cs_out);
+        for (int n = 0; n < NR; ++n) {
+          float v[TN][4];
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[j][r] = ((bits >> (n * NV + j * 4 + r)) & 1u) ? acc[n][j][r] : 0.f;
+              cst[j][r] = n == 0 ? v[j][r] : cst[j][r] + v[j][r];
+            }
+          put_act(v, act_out + n * C::TILE_BYTES);
+        }
+        ray_sums_to(cst, cs_out);
       }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < NR; ++n)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       stamp(wave == 0 ? 4 * nphase + 6 + p : 6 * nphase + 6 + p);
       lbar();  // B2: tile of the next phase and this phase's partials complete
       stamp(3 + 3 * p);
-    }
+    };
+#pragma unroll 1
+    for (int i = 0; i < a.nblk; ++i) run_block(i);
 #ifdef C3_STREAM_ONLY
-    if (acc[0][0] == 1234.5f) act[lane] = 1;  // keep the MFMAs (and their loads) alive
+    if (acc[0][0][0] == 1234.5f) act[lane] = 1;  // keep the MFMAs (and their loads) alive
 #endif
     stamp(2 + 3 * nphase);
     if (stl != nullptr && wave == 0) {
@@ -729,15 +955,19 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     {
       int64_t offset = a.idx_offset;
       if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
-      const int bt = b0 + lane / 3;
-      float tt = 0.f;
-      const int64_t trow =
-          lane < BM * 3 && bt < a.batch ? source_row(a.ray_idx, a.idx_dtype, offset, bt, a.num_rays, a.num_src) : -1;
-      if (trow >= 0) tt = a.rgb[trow * 3 + lane % 3];
-      if (lane < BM * 3) tgs[lane] = tt;
+#pragma unroll
+      for (int e0 = 0; e0 < BM * 3; e0 += 64) {
+        const int e = e0 + lane;
+        const int bt = b0 + e / 3;
+        float tt = 0.f;
+        const int64_t trow =
+            e < BM * 3 && bt < a.batch ? source_row(a.ray_idx, a.idx_dtype, offset, bt, a.num_rays, a.num_src) : -1;
+        if (trow >= 0) tt = a.rgb[trow * 3 + e % 3];
+        if (e < BM * 3) tgs[e] = tt;
+      }
     }
     // ---- fragment images for the dW GEMM (lgemm.hpp: rows = features, k = rays) ----------
-    // The workgroup's 16 rays are half (b0 / 16) % 2 of k block b0 / 32: per 16-feature
+    // A 16-ray tile at b0n = b0 + 16 n is half (b0n / 16) % 2 of k block b0n / 32: per 16-feature
     // tile t one 512-byte piece, lane slot i + 16 rh = feature 16 t + i, rays 8 rh .. 8 rh + 7.
     // One store instruction writes the pieces of tiles 2 s and 2 s + 1 (2 x 512 contiguous
     // bytes, whole lines); the feature-major transpose comes from ds_read_b64_tr_b16: a
@@ -747,16 +977,17 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     const int ti = lane & 15;                 // slot in the piece = feature within the tile
     const int tq = ti >> 2, tp = ti & 3;      // this lane's address: ray row tq, feature quad tp
     const int trh = tg & 1;
-    const int64_t half_off = ((b0 >> 4) & 1) * 512 + (int64_t)(ti + 16 * trh) * 16;
+    const int64_t lane_off = (int64_t)(ti + 16 * trh) * 16;
     typedef short s16x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
     auto tr_read = [&](const char* p8) -> s16x4 {
       return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p8));
     };
-    // tiles: R / 16 of an image with R rows; addr(t, ray, quad) -> the 8-byte LDS address of
-    // features 16 t + 4 quad .. + 3 of `ray`
-    auto copy_image = [&](auto addr, int R, bf16* img, int s_begin, int s_end) {
-      char* d = reinterpret_cast<char*>(img) + (int64_t)(b0 >> 5) * (R / 16) * 1024 + half_off;
+    // tiles: R / 16 of an image with R rows; addr(t, n, ray, quad) -> the 8-byte LDS address
+    // of features 16 t + 4 quad .. + 3 of `ray` of ray tile n
+    auto copy_image = [&](auto addr, int R, bf16* img, int s_begin, int s_end, int n) {
+      const int b0n = b0 + 16 * n;
+      char* d = reinterpret_cast<char*>(img) + (int64_t)(b0n >> 5) * (R / 16) * 1024 + ((b0n >> 4) & 1) * 512 + lane_off;
       // batches of 4 instructions: all 8 transposing reads issued before the first store
       // waits on them (counted lgkmcnt), so LDS latency is paid once per batch
       constexpr int NB = 4;
@@ -766,8 +997,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
           const int t = 2 * min(s0 + u, s_end - 1) + (tg >> 1);
-          lo[u] = tr_read(addr(t, 8 * trh + tq, tp));
-          hi[u] = tr_read(addr(t, 8 * trh + 4 + tq, tp));
+          lo[u] = tr_read(addr(t, n, 8 * trh + tq, tp));
+          hi[u] = tr_read(addr(t, n, 8 * trh + 4 + tq, tp));
         }
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
@@ -785,8 +1016,13 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       }
     };
     int x_tile0 = 0;  // first 16-feature tile held in LDS (chunked tile)
-    auto x_addr = [&](int t, int r, int q) -> const char* {
-      return xs + r * xrow + (((2 * (t - x_tile0) + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
+    auto x_addr = [&](int t, int n, int r, int q) -> const char* {
+      return xs + (16 * n + r) * xrow + (((2 * (t - x_tile0) + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
+    };
+    // every ray tile's piece of an image
+    auto copy_tiles = [&](auto addr, int R, bf16* img, int s_begin, int s_end) {
+#pragma unroll 1
+      for (int n = 0; n < NR; ++n) copy_image(addr, R, img, s_begin, s_end, n);
     };
     // X^T for the dW GEMMs of layer 0 and Ly, copied while the compute waves stream the
     // long input-layer phases (W_0: phase 0, W_y: the skip phase s), half in each
@@ -800,11 +1036,12 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           lbar();  // G1(c)
           lbar();  // G2(c)
         }
-        x_tile0 = c * (C3_KC / 16);
-        copy_image(x_addr, k_pad, a.XT, c * (C3_KC / 32), min((c + 1) * C3_KC, k_pad) / 32);
+        x_tile0 = c * (C::KC / 16);
+        copy_tiles(x_addr, k_pad, a.XT, c * (C::KC / 32), min((c + 1) * C::KC, k_pad) / 32);
       }
+      if (NR > 1) lbar();  // BX: the feature-tile region takes the parked W_y x
     } else {
-      copy_image(x_addr, k_pad, a.XT, 0, xs_mid);
+      copy_tiles(x_addr, k_pad, a.XT, 0, xs_mid);
     }
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
@@ -829,71 +1066,93 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       lbar();  // B2
       // phase p's outputs: act tile (p + 1) & 1, colsum p & 1 -- to be copied before B2(p + 1)
       const char* act_p = act + ((p + 1) & 1) * C::ACT_BYTES;
-      auto act_addr = [&](int t, int r, int q) -> const char* { return act_p + act_off(t >> 1, r, q) + 8 * (t & 1); };
+      auto act_addr = [&](int t, int n, int r, int q) -> const char* {
+        return act_p + n * C::TILE_BYTES + act_off(t >> 1, r, q) + 8 * (t & 1);
+      };
       const char* cs = reinterpret_cast<const char*>(csb + (p & 1) * H);
+      // one partial per workgroup (Bp / BM of them: refresh_tables)
+      const int64_t part0 = blockIdx.x;
       if (p < nfwd) {
         const int l = p;
-        if (!head_phase) copy_image(act_addr, H, a.YT[l], 0, H / 32);
-        if (!XC && p == a.s - 1) copy_image(x_addr, k_pad, a.XT, xs_mid, xs_total);
+        if (!head_phase) copy_tiles(act_addr, H, a.YT[l], 0, H / 32);
+        if (!XC && p == a.s - 1) copy_tiles(x_addr, k_pad, a.XT, xs_mid, xs_total);
         if (head_phase) {
-          copy_image(act_addr, H, a.dZT[L - 2], 0, H / 32);
-          copy_out(cs, a.colsum[L - 2] + (int64_t)blockIdx.x * H, H * 4);
-          copy_out(reinterpret_cast<const char*>(hws), a.hw_part + (int64_t)blockIdx.x * 3 * H, 3 * H * 4);
-          if (lane < 3) a.hb_part[(int64_t)blockIdx.x * 3 + lane] = hbs[lane];
-          if (lane < 2 && a.loss_part != nullptr) a.loss_part[2 * (int64_t)blockIdx.x + lane] = lss[lane];
+          copy_tiles(act_addr, H, a.dZT[L - 2], 0, H / 32);
+          copy_out(cs, a.colsum[L - 2] + part0 * H, H * 4);
+          copy_out(reinterpret_cast<const char*>(hws), a.hw_part + part0 * 3 * H, 3 * H * 4);
+          if (lane < 3) a.hb_part[part0 * 3 + lane] = hbs[lane];
+          if (lane < 2 && a.loss_part != nullptr) a.loss_part[2 * part0 + lane] = lss[lane];
           if (a.pred != nullptr)
             for (int c = lane; c < BM * 3; c += 64)
               if (b0 + c / 3 < a.batch) a.pred[(int64_t)b0 * 3 + c] = preds[c];
         }
       } else {
         const int l = (L - 2) - (p - nfwd);
-        copy_image(act_addr, H, a.dZT[l - 1], 0, H / 32);
-        copy_out(cs, a.colsum[l - 1] + (int64_t)blockIdx.x * H, H * 4);
+        copy_tiles(act_addr, H, a.dZT[l - 1], 0, H / 32);
+        copy_out(cs, a.colsum[l - 1] + part0 * H, H * 4);
       }
     }
   }
 }
 
-template <int H, int LOSS, bool ENC, bool XC>
+template <int H, int LOSS, bool ENC, bool XC, int NR>
 int launch3_enc(const Chain3Args& a, hipStream_t stream) {
-  using C = L3<H>;
-  const int lds = C::lds_bytes(a.L, a.kc);
+  using C = L3<H, NR>;
+  const int lds = C::lds_bytes(a.L, a.kc, XC);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC, NR>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
-  chain3_kernel<H, LOSS, ENC, XC><<<dim3((unsigned)(a.rows / C3BM)), dim3(C3_THREADS), lds, stream>>>(a);
+  chain3_kernel<H, LOSS, ENC, XC, NR><<<dim3((unsigned)(a.rows / C::BM)), dim3(C3_THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
 
 template <int H, int LOSS>
-int launch3_loss(const Chain3Args& a, hipStream_t stream) {
-  if (a.encoding != INF_ENC_NONE) return launch3_enc<H, LOSS, true, false>(a, stream);
-  if (a.kc < a.k_pad) return launch3_enc<H, LOSS, false, true>(a, stream);
-  return launch3_enc<H, LOSS, false, false>(a, stream);
+int launch3_loss(const Chain3Args& a, int bm, hipStream_t stream) {
+  if (bm != C3BM) {
+    if constexpr (H == 256) {  // chain3_supported: chunked wide tiles need H = 256
+      if (a.kc < a.k_pad) return launch3_enc<H, LOSS, false, true, C3_NR_WIDE>(a, stream);
+    }
+    INF_CHECK_ARG(a.kc == a.k_pad, "chain3: chunked wide tiles need H = 256");
+    return launch3_enc<H, LOSS, false, false, C3_NR_WIDE>(a, stream);
+  }
+  if (a.encoding != INF_ENC_NONE) return launch3_enc<H, LOSS, true, false, 1>(a, stream);
+  if (a.kc < a.k_pad) return launch3_enc<H, LOSS, false, true, 1>(a, stream);
+  return launch3_enc<H, LOSS, false, false, 1>(a, stream);
 }
 
 // the loss is a template parameter: one branch-free head per loss type keeps the compute
 // waves inside their VGPR budget (a spill would drain the weight queue)
 template <int H>
-int launch3_typed(const Chain3Args& a, hipStream_t stream) {
-  if (a.loss == INF_LOSS_L2) return launch3_loss<H, INF_LOSS_L2>(a, stream);
-  if (a.loss == INF_LOSS_L1) return launch3_loss<H, INF_LOSS_L1>(a, stream);
-  return launch3_loss<H, INF_LOSS_CAUCHY>(a, stream);
+int launch3_typed(const Chain3Args& a, int bm, hipStream_t stream) {
+  if (a.loss == INF_LOSS_L2) return launch3_loss<H, INF_LOSS_L2>(a, bm, stream);
+  if (a.loss == INF_LOSS_L1) return launch3_loss<H, INF_LOSS_L1>(a, bm, stream);
+  return launch3_loss<H, INF_LOSS_CAUCHY>(a, bm, stream);
 }
 
 }  // namespace
+
+bool chain3_lds_fits(int H, int L, int k_pad, int64_t rows) {
+  if (H != 128 && H != 256) return false;
+  const int kc = chain3_kc(k_pad, rows);
+  const bool xc = kc < k_pad;
+  int lds;
+  if (chain3_bm(rows) == C3BM) lds = H == 256 ? L3<256, 1>::lds_bytes(L, kc, xc) : L3<128, 1>::lds_bytes(L, kc, xc);
+  else lds = H == 256 ? L3<256, C3_NR_WIDE>::lds_bytes(L, kc, xc) : L3<128, C3_NR_WIDE>::lds_bytes(L, kc, xc);
+  return lds <= C3_LDS_CAP;
+}
 
 int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
   Chain3Args a = a_in;
   a.table_big = a.encoding == INF_ENC_NONE && a.num_vertices * (int64_t)a.k_pad * 2 >= ((int64_t)1 << 32);
   a.gather_nt = a.encoding == INF_ENC_NONE && (size_t)a.num_vertices * (size_t)a.k_pad * 2 > C3_NT_TABLE_BYTES;
   INF_CHECK_ARG(chain3_supported(a.H, a.L, a.k_pad, a.rows), "chain3: unsupported shape");
-  INF_CHECK_ARG(bm == C3BM, "chain3: tile height");
+  INF_CHECK_ARG(bm == chain3_bm(a.rows), "chain3: tile height");
+  INF_CHECK_ARG(bm == C3BM || (a.encoding == INF_ENC_NONE && a.xpre == nullptr), "chain3: wide tiles gather tables only");
   INF_CHECK_ARG(a.rows % bm == 0 && a.rows >= bm, "chain3: rows must be a multiple of the tile height");
   INF_CHECK_ARG(a.nphase == 2 * a.L - 3, "chain3: phases");
   INF_CHECK_ARG(a.nblk >= 1 && a.nblk <= C3_MAX_BLOCKS, "chain3: weight-stream blocks");
@@ -903,14 +1162,15 @@ int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
   INF_CHECK_ARG(a.encoding == INF_ENC_NONE || a.encoding == INF_ENC_XYZ || a.enc_proj != nullptr,
                 "chain3: encoding projection missing");
   INF_CHECK_ARG(a.vid_dtype == INF_DTYPE_I32 || a.vid_dtype == INF_DTYPE_I64, "chain3: vertex id dtype");
-  INF_CHECK_ARG(a.kc == a.k_pad || (a.kc == C3_KC && a.encoding == INF_ENC_NONE && a.nchunk == ceil_div(a.k_pad, C3_KC)),
+  INF_CHECK_ARG(a.kc == chain3_kc(a.k_pad, a.rows) && a.nchunk == ceil_div(a.k_pad, a.kc) &&
+                    (a.kc == a.k_pad || a.encoding == INF_ENC_NONE),
                 "chain3: feature chunking");
   for (int i = 0; i < a.nblk; ++i) INF_CHECK_ARG(a.blk[i].img != nullptr, "chain3: weight image missing");
   // bias / output-layer rows are read as H/64-float vectors per lane
   for (int l = 0; l < a.L - 1; ++l) INF_CHECK_ARG((uintptr_t)a.bias[l] % 16 == 0, "chain3: bias alignment");
   INF_CHECK_ARG((uintptr_t)a.bias_y % 16 == 0 && (uintptr_t)a.W7 % 16 == 0, "chain3: vector alignment");
-  if (a.H == 256) return launch3_typed<256>(a, stream);
-  return launch3_typed<128>(a, stream);
+  if (a.H == 256) return launch3_typed<256>(a, bm, stream);
+  return launch3_typed<128>(a, bm, stream);
 }
 
 }  // namespace inf

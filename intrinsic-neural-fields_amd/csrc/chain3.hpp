@@ -3,6 +3,8 @@
 
 #include "chain.hpp"
 
+#include <cstdlib>
+
 namespace inf {
 
 constexpr int C3_MAX_PHASES = 2 * CHAIN_MAX_HIDDEN;
@@ -49,8 +51,9 @@ struct Chain3Args {
   int32_t encoding, enc_k, enc_ne, enc_in_dim;
   const float* enc_proj;
   const float* pos;
-  // feature columns held in LDS at a time: k_pad (whole tile) or C3_KC (chunked, k_pad >
-  // C3_KC: config D's k = 4096 tile is 128 KiB for 16 rays, above the LDS budget)
+  // feature columns held in LDS at a time (chain3_kc): k_pad (whole tile) or C3_KC (chunked,
+  // k_pad > C3_KC: config D's k = 4096 tile is 128 KiB for 16 rays, above the LDS budget);
+  // C3_KC_WIDE for the 64-ray tiles
   int32_t kc, nchunk;
   int32_t table_big;  // table of 4 GiB or more: 64-bit row addresses (set by launch_chain3)
   int32_t gather_nt;  // table rows read non-temporally: tables above the MALL (set by launch_chain3)
@@ -85,22 +88,44 @@ struct Chain3Args {
   unsigned long long* stamps;
 };
 
-// Rays per workgroup: one 16-row MFMA tile.  Every workgroup streams the whole weight
-// set per step either way, so the smallest tile puts the most CUs on the stream (4096
-// rays -> 256 workgroups).
-inline int chain3_bm(int64_t) { return 16; }
-// Largest padded batch routed to it (above, the LDS-ring chain's taller tiles win).
+// Rays per workgroup: one 16-row MFMA tile up to CHAIN3_MAX_ROWS.  Every workgroup streams
+// the whole weight set per step either way, so the smallest tile puts the most CUs on the
+// stream (4096 rays -> 256 workgroups).  Larger batches fill the chip with 16-ray tiles many
+// times over and pay the stream once per 16 rays: there a workgroup takes C3_NR_WIDE tiles
+// (64 rays; 65,536 rays -> 1024 workgroups), each weight fragment feeding C3_NR_WIDE MFMAs.
 constexpr int64_t CHAIN3_MAX_ROWS = 8192;
+constexpr int C3_NR_WIDE = 4;
+constexpr int64_t CHAIN3_WIDE_MAX_ROWS = (int64_t)1 << 24;
+// INF_CHAIN3_WIDE=1: wide tiles at any batch that is a multiple of 64 rays (tests compare
+// the two widths on one batch)
+inline bool chain3_force_wide() { return std::getenv("INF_CHAIN3_WIDE") != nullptr; }
+inline bool chain3_wide(int64_t rows) {
+  return rows > CHAIN3_MAX_ROWS || (chain3_force_wide() && rows % (16 * C3_NR_WIDE) == 0);
+}
+inline int chain3_bm(int64_t rows) { return chain3_wide(rows) ? 16 * C3_NR_WIDE : 16; }
 // Feature columns per LDS chunk when the whole 16 x k_pad tile does not fit (k_pad > C3_KC).
 constexpr int C3_KC = 1024;
+// ... and for the wide tiles, which always stream the feature tile in chunks
+constexpr int C3_KC_WIDE = 256;
 // Weight-stream blocks of a training step: the input layers' k_pad / (32 upl) blocks each,
 // one per hidden layer forward and backward.
 inline int chain3_blocks(int H, int L, int k_pad) { return 2 * (k_pad / H) + 2 * (L - 2); }
+// The kernel's LDS footprint for this shape fits the CU (chain3.hip)
+bool chain3_lds_fits(int H, int L, int k_pad, int64_t rows);
+inline int chain3_kc(int k_pad, int64_t rows);
 inline bool chain3_supported(int H, int L, int k_pad, int64_t rows) {
   const int upl = H / 32;
-  return (H == 128 || H == 256) && L >= 3 && L - 1 <= CHAIN_MAX_HIDDEN && rows <= CHAIN3_MAX_ROWS &&
+  const bool wide = chain3_wide(rows);
+  return (H == 128 || H == 256) && L >= 3 && L - 1 <= CHAIN_MAX_HIDDEN && rows <= CHAIN3_WIDE_MAX_ROWS &&
+         (!wide || (rows % (16 * C3_NR_WIDE) == 0 && C3_KC_WIDE % (32 * upl) == 0 &&
+                    (k_pad <= C3_KC_WIDE || H == 256))) &&
          k_pad % (32 * upl) == 0 && (k_pad <= C3_KC || C3_KC % (32 * upl) == 0) &&
-         chain3_blocks(H, L, k_pad) <= C3_MAX_BLOCKS;
+         chain3_blocks(H, L, k_pad) <= C3_MAX_BLOCKS && chain3_lds_fits(H, L, k_pad, rows);
+}
+// Feature columns held in LDS at a time for a batch of `rows`
+inline int chain3_kc(int k_pad, int64_t rows) {
+  if (chain3_wide(rows)) return k_pad < C3_KC_WIDE ? k_pad : C3_KC_WIDE;
+  return k_pad > C3_KC ? C3_KC : k_pad;
 }
 
 int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream);

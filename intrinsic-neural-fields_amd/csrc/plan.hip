@@ -257,7 +257,7 @@ int build_layout(inf_plan* p) {
   if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS)
     for (int i = 0; i < 2; ++i) p->o_xp[i] = take(Bp * p->k_pad * 2);
   const int64_t max_parts =
-      std::max<int64_t>({chain_max_partials(Bp), std::min<int64_t>(Bp, CHAIN3_MAX_ROWS) / 16, (int64_t)p->grid_hb});
+      std::max<int64_t>({chain_max_partials(Bp), std::min<int64_t>(Bp, CHAIN3_WIDE_MAX_ROWS) / 16, (int64_t)p->grid_hb});
   for (int l = 0; l < L - 1; ++l) {
     p->o_y.push_back(take(Bp * H * p->esz));
     p->o_yt.push_back(take(Bp * H * p->esz));
@@ -876,8 +876,9 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     return INF_OK;
   };
   int rc;
-  const bool xc = p->k_pad > C3_KC;
-  a.kc = xc ? C3_KC : p->k_pad;
+  const int kc = chain3_kc(p->k_pad, Bp);
+  const bool xc = p->k_pad > kc;
+  a.kc = kc;
   a.nchunk = (int)ceil_div(p->k_pad, a.kc);
   if (!xc) {
     for (int i = 0; i < nx; ++i)
@@ -885,8 +886,8 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   } else {
     INF_CHECK_ARG(b->encoding == INF_ENC_NONE, "chain3: chunked feature tiles are eigenfunction tables only");
     for (int c = 0; c < a.nchunk; ++c) {
-      const int nb = std::min(C3_KC, p->k_pad - c * C3_KC) / (32 * upl);  // stream blocks of the chunk
-      const int kb = c * (C3_KC / 32);
+      const int nb = std::min(kc, p->k_pad - c * kc) / (32 * upl);  // stream blocks of the chunk
+      const int kb = c * (kc / 32);
       for (int i = 0; i < nb; ++i) {
         if ((rc = add(img(p->weight_seg(s, 1), true), kb + i * upl, 1, i * upl, 0, 0))) return rc;
         if (i == 0) a.blk[a.nblk - 1].flags = C3F_SWAP | (c > 0 ? C3F_GATHER | (c << C3F_CHUNK_SHIFT) : 0);
@@ -1653,6 +1654,7 @@ int64_t inf_plan_grad_split(const inf_plan* p) { return p == nullptr ? -1 : p->g
 
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;
+  if (p->last_chain == 3 && chain3_wide(p->saved_bp)) return 5;
   return p->last_chain == 3 && p->k_pad > C3_KC ? 4 : p->last_chain;
 }
 

@@ -201,12 +201,13 @@ def test_out_of_range_rays_and_vertices_read_as_zero():
         assert np.abs(pred.cpu().numpy() - p_ref).max() < tol, mode
 
 
-def test_out_of_range_permutation_values_read_as_zero_rows():
+def test_out_of_range_permutation_values_read_as_zero_rows(monkeypatch):
     """A permutation ENTRY naming a row outside the ray arrays (negative, >= N, the int32
     limit) reads as a zero feature row and a zero target on every kernel path that reads
     ray records -- gather + layered head (fp32), the register chain (bf16 forward), the
-    fused training chain (bf16, <= 8192 rays), the LDS-ring chain (bf16, > 8192 rays) and
-    the projected-table render -- instead of loading outside vids / bary / rgb
+    fused training chain (bf16; 16-ray tiles <= 8192 rays, 64-ray tiles above), the
+    LDS-ring chain (bf16, INF_NO_CHAIN3) and the projected-table render -- instead of
+    loading outside vids / bary / rgb
     (inf_batch.num_source_rays; the cause of the illegal access recorded in f1fb648)."""
     k, H, L, s = 64, 128, 4, 2
     w0 = init_weights(k, H, L, s, seed=13)
@@ -230,7 +231,10 @@ def test_out_of_range_permutation_values_read_as_zero_rows():
             t[i] = 0.0
         return x, t
 
-    for mode, B in (("fp32", 64), ("bf16", 64), ("bf16", 256), ("bf16", 9000)):
+    for mode, B, env in (("fp32", 64, None), ("bf16", 64, None), ("bf16", 256, None), ("bf16", 9000, None),
+                         ("bf16", 9000, "INF_NO_CHAIN3")):
+        if env:
+            monkeypatch.setenv(env, "1")
         perm = torch.from_numpy(perm_for(B)).cuda()
         x, t = oracle(B, w0)
         p_ref, _ = O.mlp_forward(w0, x, L, s)
@@ -248,6 +252,9 @@ def test_out_of_range_permutation_values_read_as_zero_rows():
         loss_ref = float(((p_ref - t) ** 2).sum())
         loss = plan.read_ctrl()["loss_sum"]
         assert abs(loss - loss_ref) < (1e-5 if mode == "fp32" else 2e-2) * max(1.0, loss_ref), (mode, B, loss, loss_ref)
+        if mode == "bf16" and B > 8192:
+            assert plan.last_step_path() == ("chain" if env else "chain3_wide"), plan.last_step_path()
+    monkeypatch.delenv("INF_NO_CHAIN3", raising=False)
     # the projected-table render (bf16)
     import model as M
     m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()

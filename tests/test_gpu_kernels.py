@@ -225,12 +225,13 @@ def test_render_golden():
 
 
 @pytest.mark.parametrize("name,B", [("B", 1024), ("A", 512), ("R", 256), ("B", 4096), ("B", 8192), ("A", 16384),
-                                    ("B", 32768)])
+                                    ("B", 20000), ("B", 32768)])
 def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
-    """The fused bf16 chains (csrc/chain3.hip: batches up to 8192 rays, register-streamed
-    weights after the input GEMM; csrc/chain.hip: the LDS-ring chain) vs the layered bf16
-    kernels and the fp32 oracle: predictions within 2e-2; reduced gradients within 0.25
-    of each tensor's max.
+    """The fused bf16 chains (csrc/chain3.hip: register-streamed weights, 16-ray tiles up to
+    8192 rays and 64-ray tiles above -- config B's k = 1024 then streams the feature tile
+    in 256-column chunks with W_y x parked in LDS; csrc/chain.hip: the LDS-ring chain) vs
+    the layered bf16 kernels and the fp32 oracle: predictions within 2e-2; reduced
+    gradients within 0.25 of each tensor's max.
     bf16 rounding of activations and of dZ compounds backwards through the ReLU layers:
     PyTorch's own bf16 autocast of the reference on this exact problem (config B, 1024
     rays) is off by 0.135 (layers.0 weight) / 0.10 (Ly) / 0.005 (head) of max, and this
@@ -285,6 +286,54 @@ def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
         for n in O.layer_names(L, s):
             scale = max(np.abs(out["layered"][1][n]).max(), 1e-12)
             assert np.abs(out[tag][1][n] - out["layered"][1][n]).max() / scale < 1e-2, (tag, n)
+
+
+@pytest.mark.parametrize("name,B", [("A", 4096), ("R", 1024), ("B", 4096)])
+def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
+    """chain3's 64-ray tiles (INF_CHAIN3_WIDE forces them below 8192 rays) against its
+    16-ray tiles on one batch.  Per ray the two run the same MFMA k order and epilogue
+    arithmetic, so the predictions, the loss and the feature-major images the dW GEMM reads
+    are bitwise equal -- except where the feature tile is chunked (config B in wide tiles:
+    W_y x is a separate fp32 sum added in the skip epilogue, as in rchain.hip), where a
+    bf16 activation may round the other way (5e-4, the chain-vs-layered bar above).  The
+    bias / output-layer gradient partials are per workgroup (64 vs 16 rays), so their fp32
+    sums differ in order only: 1e-5 of max."""
+    rng = np.random.default_rng(5)
+    k, H, L, s = CFG[name]
+    V = 2000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda())
+    out = {}
+    for tag in ("narrow", "wide"):
+        if tag == "wide":
+            monkeypatch.setenv("INF_CHAIN3_WIDE", "1")
+        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
+        c = plan.read_ctrl()
+        assert plan.last_step_path() == ("chain3_wide" if tag == "wide" else "chain3"), plan.last_step_path()
+        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"])
+    chunked = name == "B"
+    pn, gn, ln = out["narrow"]
+    pw, gw, lw = out["wide"]
+    if chunked:
+        np.testing.assert_allclose(pw, pn, atol=5e-4)
+    else:
+        np.testing.assert_array_equal(pw, pn)
+    assert abs(lw - ln) <= (1e-3 if chunked else 1e-6) * max(1.0, abs(ln)), (lw, ln)
+    for n in O.layer_names(L, s):
+        scale = max(np.abs(gn[n]).max(), 1e-12)
+        err = np.abs(gw[n] - gn[n]).max() / scale
+        matrix_w = n.endswith(".weight") and not n.startswith(f"layers.{L - 1}.")
+        if matrix_w and not chunked:
+            assert err == 0.0, (n, err)  # lgemm over bitwise-equal images
+        else:
+            assert err < (1e-2 if chunked else 1e-5), (n, err)
 
 
 def test_bf16_chain_render_matches_layered(monkeypatch):
