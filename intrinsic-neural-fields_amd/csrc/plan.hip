@@ -19,6 +19,7 @@
 #include "chain3.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
+#include "fgemm.hpp"
 #include "lgemm.hpp"
 #include "rchain.hpp"
 #include "blaslt.hpp"
@@ -465,6 +466,36 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     // bucket 1 / 2: only the matrices of arena [grad_split, P) / [0, grad_split), with
     // bucket_splits partials each (the data-parallel bucketed step)
     const int splits = bucket ? p->bucket_splits : p->dw_splits;
+    // large batches (the 64-ray chain tiles): 256 x 256 output tiles over the same images
+    // (fgemm.hip), when every matrix is a whole number of them
+    bool fg = fuse == nullptr && chain3_wide(Bp) && std::getenv("INF_NO_FGEMM") == nullptr;
+    for (const ParamSeg& g : p->segs)
+      if (g.gemm) fg = fg && fgemm_shape_ok(g.c_pad, g.R, Bp, splits);
+    if (fg) {
+      FgemmBatch fb;
+      std::memset(&fb, 0, sizeof(fb));
+      fb.K = Bp;
+      fb.splits = splits;
+      for (size_t i = 0; i < p->segs.size(); ++i) {
+        const ParamSeg& g = p->segs[i];
+        if (!g.gemm) continue;
+        if ((bucket == 1 && g.off < p->grad_split) || (bucket == 2 && g.off >= p->grad_split)) continue;
+        INF_CHECK_ARG(fb.nprob < FGEMM_MAX_PROBLEMS, "fgemm: too many weight matrices");
+        FgemmProblem& q = fb.p[fb.nprob++];
+        const int l = g.layer;
+        const bool from_input = (l == 0) || (l == s && g.sub == 1);
+        q.Af = from_input ? p->W<bf16>(p->o_x0t) : p->W<bf16>(p->o_yt[l - 1]);
+        q.a_tiles = (from_input ? p->k_pad : H) / 16;
+        q.Bf = p->W<bf16>(p->o_dZT[l]);
+        q.b_tiles = H / 16;
+        q.M = g.c_pad;
+        q.N = g.R;
+        q.slab = p->W<float>(p->o_slab[i]);
+        q.slab_ld = g.c_pad;
+        q.slab_stride = (int64_t)g.R * g.c_pad;
+      }
+      return launch_fgemm(fb, st);
+    }
     // register-streamed chain: X^T, Y_l^T and dZ_l^T are fragment images (chain3.hip); one
     // lgemm launch computes every dW^T tile into the split-K slabs the update launch reduces
     LgemmBatch lb;

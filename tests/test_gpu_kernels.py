@@ -288,7 +288,7 @@ def test_bf16_chain_matches_layered_and_oracle(name, B, monkeypatch):
             assert np.abs(out[tag][1][n] - out["layered"][1][n]).max() / scale < 1e-2, (tag, n)
 
 
-@pytest.mark.parametrize("name,B", [("A", 4096), ("R", 1024), ("B", 4096)])
+@pytest.mark.parametrize("name,B", [("A", 4096), ("A", 8192), ("B", 8192)])
 def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
     """chain3's 64-ray tiles (INF_CHAIN3_WIDE forces them below 8192 rays) against its
     16-ray tiles on one batch.  Per ray the two run the same MFMA k order and epilogue
@@ -297,7 +297,9 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
     W_y x is a separate fp32 sum added in the skip epilogue, as in rchain.hip), where a
     bf16 activation may round the other way (5e-4, the chain-vs-layered bar above).  The
     bias / output-layer gradient partials are per workgroup (64 vs 16 rays), so their fp32
-    sums differ in order only: 1e-5 of max."""
+    sums differ in order only: 1e-5 of max.  Config B's weight gradients then come from
+    the 256 x 256-tile GEMM (fgemm.hip) instead of lgemm: on the same images the two agree
+    to fp32 summation order (1e-5 of max, INF_NO_FGEMM)."""
     rng = np.random.default_rng(5)
     k, H, L, s = CFG[name]
     V = 2000
@@ -309,14 +311,16 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
     src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
                          torch.from_numpy(rgb).cuda())
     out = {}
-    for tag in ("narrow", "wide"):
+    for tag in ("narrow", "wide", "wide_lgemm"):
         if tag == "wide":
             monkeypatch.setenv("INF_CHAIN3_WIDE", "1")
+        if tag == "wide_lgemm":
+            monkeypatch.setenv("INF_NO_FGEMM", "1")
         plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
         pred = torch.empty((B, 3), device="cuda")
         plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
         c = plan.read_ctrl()
-        assert plan.last_step_path() == ("chain3_wide" if tag == "wide" else "chain3"), plan.last_step_path()
+        assert plan.last_step_path() == ("chain3" if tag == "narrow" else "chain3_wide"), plan.last_step_path()
         out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"])
     chunked = name == "B"
     pn, gn, ln = out["narrow"]
@@ -334,6 +338,11 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
             assert err == 0.0, (n, err)  # lgemm over bitwise-equal images
         else:
             assert err < (1e-2 if chunked else 1e-5), (n, err)
+    pl, gl, _ = out["wide_lgemm"]
+    np.testing.assert_array_equal(pl, pw)
+    for n in O.layer_names(L, s):
+        scale = max(np.abs(gl[n]).max(), 1e-12)
+        assert np.abs(gw[n] - gl[n]).max() / scale < 1e-5, n
 
 
 def test_bf16_chain_render_matches_layered(monkeypatch):
