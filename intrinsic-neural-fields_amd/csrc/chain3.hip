@@ -62,7 +62,7 @@ constexpr int C3BM = 16;  // rays per 16-row MFMA tile (= per workgroup at NR = 
 // (64 x 1024 bf16 would not fit beside the activation tiles) and the fragment ring is
 // shallower (each k block now carries NR times the MFMA work)
 #ifndef C3_DEPTH_WIDE
-#define C3_DEPTH_WIDE 3
+#define C3_DEPTH_WIDE 4
 #endif
 // Cache policy of the table-row loads: non-temporal for tables larger than the MALL (rows
 // read once per step would evict the weight stream's L2 lines; config D's 4.1 GB table),
@@ -190,6 +190,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // fragment ring: D k-blocks (D * TN KiB per wave) in flight
     constexpr int D0 = NR == 1 ? C3_DEPTH : C3_DEPTH_WIDE;
     constexpr int D = D0 < UPL ? D0 : UPL;
+    // every block starts at ring slot 0 (slot = k block % D)
+    static_assert(UPL % D == 0, "the fragment ring depth must divide a block's k blocks");
     bf16x8 fr[D][TN];
     // buffer loads: descriptor per image in SGPRs, k-block offset in soffset, tile offset
     // as the immediate, one VGPR of lane offset -- no 64-bit address registers
@@ -499,7 +501,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         for (int r = 0; r < 4; ++r) t[j * 4 + r] = v[j][r];
       const float s = ray_sum<NV>(t, lane);
       const int idx = r16 % NV;
-      if (r16 < NV) dst[feat(idx >> 2) + (idx & 3)] = s;
+      int fo = feat(idx >> 2) + (idx & 3);
+      if constexpr (NR > 1) asm volatile("" : "+v"(fo));  // computed here, not hoisted (and spilled)
+      if (r16 < NV) dst[fo] = s;
     };
 
     // The chunked schedule's second accumulator set (W_y x, phase 0 .. the skip layer):
