@@ -421,6 +421,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
   return INF_OK;
 }
 
+bool use_fgemm(const inf_plan* p, int Bp, int splits);
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr,
                      int bucket = 0);
 
@@ -468,10 +469,7 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     const int splits = bucket ? p->bucket_splits : p->dw_splits;
     // large batches (the 64-ray chain tiles): 256 x 256 output tiles over the same images
     // (fgemm.hip), when every matrix is a whole number of them
-    bool fg = fuse == nullptr && chain3_wide(Bp) && std::getenv("INF_NO_FGEMM") == nullptr;
-    for (const ParamSeg& g : p->segs)
-      if (g.gemm) fg = fg && fgemm_shape_ok(g.c_pad, g.R, Bp, splits);
-    if (fg) {
+    if (fuse == nullptr && use_fgemm(p, Bp, splits)) {
       FgemmBatch fb;
       std::memset(&fb, 0, sizeof(fb));
       fb.K = Bp;
@@ -833,6 +831,15 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
   return launch_chain(a, bm, st);
 }
 
+// The large-batch dW GEMM (fgemm.hip) for this padded batch: 64-ray chain tiles and every
+// weight matrix a whole number of 256 x 256 tiles
+bool use_fgemm(const inf_plan* p, int Bp, int splits) {
+  if (!chain3_wide(Bp) || std::getenv("INF_NO_FGEMM") != nullptr) return false;
+  for (const ParamSeg& g : p->segs)
+    if (g.gemm && !fgemm_shape_ok(g.c_pad, g.R, Bp, splits)) return false;
+  return true;
+}
+
 bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   const ParamSeg* w1 = p->weight_seg(1, 0);
   const ParamSeg* w0 = p->weight_seg(0, 0);
@@ -844,7 +851,11 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
          w0->f_off >= 0 && b->table != nullptr &&
          (b->encoding == INF_ENC_NONE ? b->table_dtype == INF_DTYPE_BF16
                                       : (b->table_dtype == INF_DTYPE_F32 && b->vids != nullptr && p->k_pad <= C3_KC)) &&
-         (Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0 && std::getenv("INF_NO_CHAIN3") == nullptr;
+         // the dW GEMM's split-K: lgemm streams K = Bp / dw_splits rays per block in 256-ray
+         // steps, fgemm any multiple of 64 rays per split
+         (use_fgemm(p, Bp, p->dw_splits) ||
+          ((Bp / p->dw_splits) % 256 == 0 && Bp % p->dw_splits == 0)) &&
+         std::getenv("INF_NO_CHAIN3") == nullptr;
 }
 
 // Fused gather + forward + loss + dX chain of a bf16 training batch (csrc/chain3.hip).

@@ -211,7 +211,7 @@ def test_out_of_range_permutation_values_read_as_zero_rows(monkeypatch):
     (inf_batch.num_source_rays; the cause of the illegal access recorded in f1fb648)."""
     k, H, L, s = 64, 128, 4, 2
     w0 = init_weights(k, H, L, s, seed=13)
-    N = 9100
+    N = 10300
     E, vids, bary, rgb = synth_rays(k, 50, N, seed=21)
     src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
                          torch.from_numpy(rgb).cuda())
@@ -231,7 +231,9 @@ def test_out_of_range_permutation_values_read_as_zero_rows(monkeypatch):
             t[i] = 0.0
         return x, t
 
-    for mode, B, env in (("fp32", 64, None), ("bf16", 64, None), ("bf16", 256, None), ("bf16", 9000, None),
+    # (10240 rays: the 64-ray chain tiles -- its dW GEMM splits the padded batch into
+    # 256-ray multiples; 9000 rays with INF_NO_CHAIN3: the LDS-ring chain)
+    for mode, B, env in (("fp32", 64, None), ("bf16", 64, None), ("bf16", 256, None), ("bf16", 10240, None),
                          ("bf16", 9000, "INF_NO_CHAIN3")):
         if env:
             monkeypatch.setenv(env, "1")
