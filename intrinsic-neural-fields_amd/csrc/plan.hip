@@ -229,6 +229,9 @@ int build_layout(inf_plan* p) {
   // (tools/split_sweep.sh)
   if (d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
   if (d.mode == INF_MODE_BF16 && mb <= 4096 && S > 2) S = 2;
+  // the 64-ray chain tiles' dW through lgemm (shapes fgemm does not tile) stream
+  // K = Bp / S rays per block in 256-ray steps: 10,240 rays take 8 splits, not 16
+  while (d.mode == INF_MODE_BF16 && mb > CHAIN3_MAX_ROWS && S > 1 && mb % (256 * (int64_t)S) != 0) S /= 2;
   if (const char* e = std::getenv("INF_DW_SPLITS")) {  // tuning experiments
     const int want = std::atoi(e);
     if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 128) S = want;
