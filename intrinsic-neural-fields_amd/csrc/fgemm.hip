@@ -4,8 +4,8 @@
 //
 // Tile.  256 x 256 outputs per workgroup (the whole hidden-layer dW, a quarter of an
 // input layer's at k = 1024), 8 waves as 2 (rows) x 4 (columns), each wave 128 x 64: 8 x 4
-// v_mfma_f32_16x16x32_bf16 tiles, 128 fp32 accumulators per lane.  Per 64-ray k-step the
-// workgroup moves 64 KB for 2 x 256 x 256 x 64 FLOP (128 FLOP/B: ptab.hip's ratio).
+// v_mfma_f32_16x16x32_bf16 tiles, 128 fp32 accumulators per lane.  Per 32-ray k-step the
+// workgroup moves 32 KB for 2 x 256 x 256 x 32 FLOP (128 FLOP/B: ptab.hip's ratio).
 //
 // Operands need no layout work: a fragment image's k block holds each 16-row tile's MFMA
 // operand as one contiguous KiB (lane l's 16 bytes at 16 l), so a stage is 64 whole-KiB
@@ -13,9 +13,11 @@
 // (global_load_lds_dwordx4, lane-linear: the KiB lands in fragment order) and every
 // fragment read is one lane-contiguous ds_read_b128 (conflict-free, no swizzle).
 //
-// Pipeline (ptab.hip): 2 LDS stages of 64 KB; stage t + 1 is loaded while stage t feeds
-// the MFMAs, one `s_waitcnt vmcnt` + raw s_barrier per k-step.
-//
+// Pipeline: FG_NSTAGE LDS stages of one 32-ray k block each (32 KB: 16 KiB pieces of A and
+// of B); up to FG_NSTAGE - 1 stages in flight per workgroup (128 KB at 5 stages), so the
+// HBM latency of the streamed images is covered; one counted `s_waitcnt vmcnt` + raw
+// s_barrier per k-step.  (Two 64 KB stages of 64 rays -- one stage in flight behind a
+// vmcnt(0) wait -- ran at 0.29 of the MFMA peak: profiles/r03.)
 // Output.  Split s writes its partial dW (f32, the update launch's slab layout): a lane's
 // 4 accumulators of a tile are 4 consecutive input features of one output feature -- one
 // 16-byte store.  Blocks are ordered [problem][split][row tile][column tile] and remapped
@@ -31,8 +33,12 @@ using c3::u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int FG_THREADS = 512;
-constexpr int FG_STAGES = 2;
-constexpr int FG_PIECES = 2 * (FG_BK / 32) * (FG_TILE / 16);  // KiB pieces per stage (A then B)
+#ifndef FG_NSTAGE
+#define FG_NSTAGE 5
+#endif
+constexpr int FG_STAGES = FG_NSTAGE;
+constexpr int FG_KS = 32;                                     // rays per k-step (one k block)
+constexpr int FG_PIECES = 2 * (FG_KS / 32) * (FG_TILE / 16);  // KiB pieces per stage (A then B)
 constexpr int FG_STAGE_BYTES = FG_PIECES * 1024;
 constexpr int FG_GLDS = FG_PIECES / 8;  // direct-to-LDS loads per wave per stage
 constexpr int FG_LDS = FG_STAGES * FG_STAGE_BYTES;
@@ -42,6 +48,17 @@ static_assert(FG_LDS <= 160 * 1024, "fgemm LDS");
 template <int N>
 __device__ __forceinline__ void fg_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+// wait until at most `ahead` stages (wave-uniform, <= N) of this wave's direct-to-LDS loads
+// are in flight, then the workgroup barrier (vmcnt takes an immediate)
+template <int N>
+__device__ __forceinline__ void fg_wait_ahead(int ahead) {
+  if constexpr (N <= 0) {
+    fg_wait_barrier<0>();
+  } else {
+    if (ahead >= N) fg_wait_barrier<N * FG_GLDS>();
+    else fg_wait_ahead<N - 1>(ahead);
+  }
 }
 
 __global__ __launch_bounds__(FG_THREADS, 1) void fgemm_kernel(const FgemmBatch b) {
@@ -60,8 +77,8 @@ __global__ __launch_bounds__(FG_THREADS, 1) void fgemm_kernel(const FgemmBatch b
   const int split = r / (tiles_m * tiles_n);
   r -= split * tiles_m * tiles_n;
   const int tm = r / tiles_n, tn = r - tm * tiles_n;
-  // the split's 64-ray k-steps
-  const int KT = b.K / FG_BK;
+  // the split's 32-ray k-steps
+  const int KT = b.K / FG_KS;
   const int kt0 = (int)((int64_t)split * KT / b.splits), kt1 = (int)((int64_t)(split + 1) * KT / b.splits);
   const int nk = kt1 - kt0;
 
@@ -70,7 +87,7 @@ __global__ __launch_bounds__(FG_THREADS, 1) void fgemm_kernel(const FgemmBatch b
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
-  // piece p = wave + 8 i of a stage: A pieces 0..31 (k block p / 16, tile p % 16), B 32..63
+  // piece p = wave + 8 i of a stage: A pieces (k block p / 16, tile p % 16), then B
   const char* srcp[FG_GLDS];
   int64_t kb_stride[FG_GLDS];
 #pragma unroll
@@ -83,8 +100,8 @@ __global__ __launch_bounds__(FG_THREADS, 1) void fgemm_kernel(const FgemmBatch b
     const int tiles = isa ? P.a_tiles : P.b_tiles;
     const int t0 = (isa ? tm : tn) * (FG_TILE / 16);
     srcp[i] = reinterpret_cast<const char*>(img) +
-              ((int64_t)(2 * kt0 + kbl) * tiles + t0 + t) * 1024 + lane * 16;
-    kb_stride[i] = (int64_t)2 * tiles * 1024;  // bytes per 64-ray k-step
+              ((int64_t)((FG_KS / 32) * kt0 + kbl) * tiles + t0 + t) * 1024 + lane * 16;
+    kb_stride[i] = (int64_t)(FG_KS / 32) * tiles * 1024;  // bytes per k-step
   }
   auto issue = [&](int t) {
     char* st = smem + (t % FG_STAGES) * FG_STAGE_BYTES;
@@ -102,14 +119,18 @@ __global__ __launch_bounds__(FG_THREADS, 1) void fgemm_kernel(const FgemmBatch b
 #pragma unroll
     for (int i = 0; i < FG_TI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) issue(0);
+#pragma unroll
+  for (int q = 0; q < FG_STAGES - 1; ++q)
+    if (q < nk) issue(q);
 #pragma unroll 1
   for (int t = 0; t < nk; ++t) {
-    fg_wait_barrier<0>();  // stage t landed (every wave's loads) and stage t - 1 is read out
-    if (t + 1 < nk) issue(t + 1);
+    // stage t landed (every wave's loads; later stages may stay in flight) and stage t - 1
+    // is read out, so its buffer takes stage t + FG_STAGES - 1
+    fg_wait_ahead<FG_STAGES - 2>(min(FG_STAGES - 2, nk - 1 - t));
+    if (t + FG_STAGES - 1 < nk) issue(t + FG_STAGES - 1);
     const char* st = smem + (t % FG_STAGES) * FG_STAGE_BYTES + lane * 16;
 #pragma unroll
-    for (int kbl = 0; kbl < FG_BK / 32; ++kbl) {
+    for (int kbl = 0; kbl < FG_KS / 32; ++kbl) {
       bf16x8 af[FG_TI], bfr[FG_TJ];
 #pragma unroll
       for (int i = 0; i < FG_TI; ++i)
