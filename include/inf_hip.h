@@ -327,7 +327,8 @@ int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
 /* Diagnostics: the kernel path the last inf_train_step took -- 0 layered GEMMs, 2 the
  * LDS-ring chain (csrc/chain.hip), 3 the fused gather + register-streamed chain
  * (csrc/chain3.hip), 4 the same with the feature tile streamed in chunks (k_pad > 1024),
- * 5 the same in 64-ray tiles (batches above 8192 rays); -1 before any step. */
+ * 5 the same in 64-ray tiles (batches above 8192 rays), 6 the fused fp32 chain of the
+ * fp32 mode (csrc/chainf.hip); -1 before any step. */
 int inf_plan_last_step_path(const inf_plan* plan);
 
 /* Weight generation: a counter of the launches issued through this plan that may have

@@ -114,6 +114,16 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
         const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
       }
+    } else {
+      if (seg.WF != nullptr && ok[i]) {
+        // fp32 fragment image (chainf.hpp): 2 KiB per (k block, 16-row tile), half
+        // (gc / 4) % 2 of lane (gr % 16) + 16 ((gc % 32) / 8)
+        const int gr = item.r0 + r;
+        const int kk = gc & 31;
+        const int64_t e = (((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 2 + ((kk >> 2) & 1)) * 64 + (gr & 15) +
+                           16 * (kk >> 3)) * 4;
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(seg.WF) + e) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
+      }
     }
   }
   lds_barrier();
@@ -129,6 +139,24 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
         for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
         const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
         *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
+      }
+    }
+  } else {
+    if (seg.WTF != nullptr) {
+      // fp32 backward fragment image (A = W^T: rows = input features, k = output
+      // features): per (column cc, 32-row block kbl, lane group g, half h) four consecutive
+      // rows 32 kb + 8 g + 4 h .. + 3 of one column
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int idx = tid + 256 * s2;
+        const int cc = idx >> 4, kbl = (idx >> 3) & 1, g = (idx >> 1) & 3, h = idx & 1;
+        const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
+        if (gcc < seg.C && gr + 31 < seg.R) {
+          const int rr = kbl * 32 + 8 * g + 4 * h;
+          const int64_t off = (((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 2 + h) * 64 + (gcc & 15) + 16 * g) * 4;
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(seg.WTF) + off) =
+              make_float4(tile[cc][rr], tile[cc][rr + 1], tile[cc][rr + 2], tile[cc][rr + 3]);
+        }
       }
     }
   }

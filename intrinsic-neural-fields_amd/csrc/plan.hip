@@ -17,6 +17,7 @@
 #include "adam.hpp"
 #include "chain.hpp"
 #include "chain3.hpp"
+#include "chainf.hpp"
 #include "gemm.hpp"
 #include "head.hpp"
 #include "fgemm.hpp"
@@ -49,6 +50,8 @@ struct ParamSeg {
 };
 
 constexpr int64_t ALIGN = 256;
+// inf_plan::last_chain of a step on the fused fp32 chain (chainf.hip)
+constexpr int CHAIN_F32 = 6;
 
 }  // namespace
 }  // namespace inf
@@ -103,7 +106,8 @@ struct inf_plan {
   // saved forward
   int saved_batch = 0, saved_bp = 0;
   bool saved = false;
-  int last_chain = 0;  // fused chain of the last training step: 0 none, 2 LDS ring, 3 registers
+  int last_chain = 0;  // fused chain of the last training step: 0 none, 2 LDS ring, 3 registers,
+                       // CHAIN_F32 the fp32 register chain
   bool stepped = false;
   // Row-major / transposed bf16 shadows (W, W^T) are read only off the fused path (layered
   // and LDS-ring GEMMs, the table projection); the fused chain3 step's update writes the
@@ -193,19 +197,20 @@ int build_layout(inf_plan* p) {
     const int bt = (H % 128 == 0) ? 128 : 64;
     gemm_tiles += (g.R / bt) * (g.c_pad / bt);
   }
-  // fragment images (bf16 mode): the hidden H x H weights, forward and transposed, for
-  // the register-streamed chain; W_0 and W_y (forward) for the input GEMM (lgemm.hip)
-  if (p->mode == INF_MODE_BF16 && (H == 128 || H == 256)) {
+  // fragment images: the hidden H x H weights, forward and transposed, and W_0 / W_y
+  // (forward) for the register-streamed chains -- bf16 (chain3.hip, rchain.hip) or fp32
+  // (chainf.hip, the fp32 mode's fused step)
+  if ((p->mode == INF_MODE_BF16 || p->mode == INF_MODE_FP32) && (H == 128 || H == 256)) {
     for (auto& g : p->segs) {
       if (!g.gemm) continue;
       const bool hidden = g.layer >= 1 && g.layer <= L - 2 && g.sub == 0 && g.R == H && g.C == H;
       const bool input = (g.layer == 0 && g.sub == 0) || (g.layer == s && g.sub == 1);
       if (!hidden && !input) continue;
       g.f_off = sh;
-      sh = align_up(sh + (int64_t)g.R * g.c_pad * 2);
+      sh = align_up(sh + (int64_t)g.R * g.c_pad * p->esz);
       if (hidden) {
         g.ft_off = sh;
-        sh = align_up(sh + (int64_t)H * H * 2);
+        sh = align_up(sh + (int64_t)H * H * p->esz);
       }
     }
   }
@@ -550,9 +555,10 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     q.lda[0] = chain ? (int64_t)H * 16 : Bp;
     q.a_kblk = chain ? 1 : 0;
     const bool from_input = (l == 0) || (l == s && g.sub == 1);
-    const bool b_blocked = chain && !from_input && !(chain == 3 && l == 1);
+    // chainf (CHAIN_F32) writes every operand 16-ray blocked, X^T included
+    const bool b_blocked = chain && (chain == CHAIN_F32 || (!from_input && !(chain == 3 && l == 1)));
     q.B[0] = from_input ? (const void*)p->W(p->o_x0t) : (const void*)p->W(p->o_yt[l - 1]);
-    q.ldb[0] = b_blocked ? (int64_t)H * 16 : Bp;
+    q.ldb[0] = b_blocked ? (int64_t)(from_input ? p->k_pad : H) * 16 : Bp;
     q.b_kblk = b_blocked ? 1 : 0;
     q.K[0] = Bp;
     q.M = g.R;
@@ -632,7 +638,10 @@ int ensure_rowmajor(inf_plan* p, hipStream_t st) {
 // fused chain3 steps in bf16 leave the row-major shadows to ensure_rowmajor
 // (INF_EAGER_SHADOWS=1: every update rewrites all shadows)
 int step_shadow_mode(const inf_plan* p, int chain) {
-  return chain == 3 && p->mode == INF_MODE_BF16 && std::getenv("INF_EAGER_SHADOWS") == nullptr ? 2 : 1;
+  return ((chain == 3 && p->mode == INF_MODE_BF16) || (chain == CHAIN_F32 && p->mode == INF_MODE_FP32)) &&
+                 std::getenv("INF_EAGER_SHADOWS") == nullptr
+             ? 2
+             : 1;
 }
 
 // The seg table of the bucketed steps: the matrices' gradients summed over bucket_splits
@@ -646,7 +655,10 @@ std::vector<AdamSeg> bucket_segs(const inf_plan* p) {
 
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
-  const int parts = chain == 3 ? Bp / chain3_bm(Bp) : chain ? Bp / chain_partial_rows(chain_bm(Bp)) : Bp / 64;
+  const int parts = chain == 3 ? Bp / chain3_bm(Bp)
+                    : chain == CHAIN_F32 ? Bp / 16
+                    : chain ? Bp / chain_partial_rows(chain_bm(Bp))
+                            : Bp / 64;
   bool changed = false;
   for (size_t i = 0; i < p->segs.size(); ++i) {
     const ParamSeg& g = p->segs[i];
@@ -977,6 +989,101 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.stamps = p->stamps;
   a.xpre = b->encoding == INF_ENC_NONE ? xpre : nullptr;
   return launch_chain3(a, chain3_bm(Bp), st);
+}
+
+// The fp32 mode's fused step (chainf.hip): eigenfunction tables up to k_pad = 1024, fp32
+// fragment images, a dW GEMM over 16-ray blocked operands (K = Bp split dw_splits ways in
+// 32-ray k-tiles).  INF_NO_CHAINF=1: the layered kernels.
+bool use_chainf(const inf_plan* p, const inf_batch* b, int Bp) {
+  if (p->mode != INF_MODE_FP32 || !chainf_supported(p->H, p->L, p->k_pad)) return false;
+  if (b->table == nullptr || b->encoding != INF_ENC_NONE || b->table_dtype != INF_DTYPE_F32 || b->vids == nullptr ||
+      b->rgb == nullptr)
+    return false;
+  if (b->num_vertices >= ((int64_t)1 << 31) || Bp % 16 != 0 || (Bp / 32) % p->dw_splits != 0) return false;
+  for (int l = 0; l <= p->L - 2; ++l) {
+    const ParamSeg* w = p->weight_seg(l, 0);
+    if (w == nullptr || w->f_off < 0 || (l >= 1 && w->ft_off < 0)) return false;
+  }
+  const ParamSeg* wy = p->weight_seg(p->s, 1);
+  return wy != nullptr && wy->f_off >= 0 && std::getenv("INF_NO_CHAINF") == nullptr;
+}
+
+// Fused gather + forward + loss + dX chain of an fp32 training batch (csrc/chainf.hip).
+// Weight stream as chain3's unchunked schedule: W_0 over X, the hidden layers (the skip
+// layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
+int run_chainf(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
+  const int H = p->H, L = p->L, s = p->s;
+  const int upl = H / 32;
+  const int nx = p->k_pad / (32 * upl);
+  ChainFArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.L = L;
+  a.s = s;
+  a.H = H;
+  a.k_pad = p->k_pad;
+  a.rows = Bp;
+  a.batch = b->batch;
+  a.table = reinterpret_cast<const float*>(b->table);
+  a.num_vertices = b->num_vertices;
+  a.vids = b->vids;
+  a.vid_dtype = b->vid_dtype;
+  a.bary = b->bary;
+  a.rgb = b->rgb;
+  a.ray_idx = b->ray_idx;
+  a.idx_dtype = b->idx_dtype;
+  a.idx_offset = b->idx_offset;
+  a.num_rays = b->num_rays;
+  a.num_src = b->num_source_rays;
+  a.offset_from_ctrl = b->offset_from_ctrl;
+  auto img = [&](const ParamSeg* w, bool fwd) -> const float* {
+    const int64_t off = fwd ? w->f_off : w->ft_off;
+    return off >= 0 ? reinterpret_cast<const float*>(p->shadow + off) : nullptr;
+  };
+  auto add = [&](const float* im, int kb0, int a_x, int ak0, int phase, int last) -> int {
+    INF_CHECK_ARG(im != nullptr, "chainf: fragment image missing");
+    INF_CHECK_ARG(a.nblk < C3_MAX_BLOCKS, "chainf: too many weight-stream blocks");
+    CFBlock& blk = a.blk[a.nblk++];
+    blk.img = im;
+    blk.kb0 = kb0;
+    blk.a_x = a_x;
+    blk.ak0 = ak0;
+    blk.phase = phase;
+    blk.last = last;
+    return INF_OK;
+  };
+  int rc;
+  for (int i = 0; i < nx; ++i)
+    if ((rc = add(img(p->weight_seg(0, 0), true), i * upl, 1, i * upl, 0, i == nx - 1))) return rc;
+  for (int l = 1; l <= L - 2; ++l) {
+    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, l != s))) return rc;
+    if (l == s)
+      for (int i = 0; i < nx; ++i)
+        if ((rc = add(img(p->weight_seg(s, 1), true), i * upl, 1, i * upl, l, i == nx - 1))) return rc;
+  }
+  for (int l = L - 2; l >= 1; --l)
+    if ((rc = add(img(p->weight_seg(l, 0), false), 0, 0, 0, (L - 1) + (L - 2 - l), 1))) return rc;
+  a.nphase = 2 * L - 3;
+  for (int l = 0; l <= L - 2; ++l) {
+    a.bias[l] = p->params + p->bias_seg(l, 0)->off;
+    a.YT[l] = p->W<float>(p->o_yt[l]);
+    a.dZT[l] = p->W<float>(p->o_dZT[l]);
+    a.colsum[l] = p->W<float>(p->o_colsum[l]);
+  }
+  a.bias_y = p->params + p->bias_seg(s, 1)->off;
+  a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
+  a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
+  a.XT = p->W<float>(p->o_x0t);
+  a.hw_part = p->W<float>(p->o_hw);
+  a.hb_part = p->W<float>(p->o_hb);
+  a.loss_part = p->W<double>(p->o_loss);
+  a.pred = pred;
+  a.loss = b->loss >= 0 ? b->loss : p->d.loss;
+  INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
+  const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
+  a.inv_count = (float)(1.0 / (double)cnt);
+  a.ctrl = p->ctrl;
+  a.count_step = 1;
+  return launch_chainf(a, st);
 }
 
 bool use_rchain(const inf_plan* p, const inf_batch* b) {
@@ -1418,6 +1525,17 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       return launch_update(a, p->mode, st);
     }
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
+  } else if (use_chainf(p, batch, Bp3)) {
+    // fp32 mode: fused gather + chain (exact f32 MFMA) -> dW GEMM over its blocked
+    // operands (-> update below); the chain leaves per-workgroup loss partials
+    const int Bp = Bp3;
+    if ((rc = run_chainf(p, batch, Bp, pred, st))) return rc;
+    if ((rc = run_weight_grads(p, Bp, st, CHAIN_F32))) return rc;
+    p->saved = false;
+    p->saved_batch = batch->batch;
+    p->saved_bp = Bp;
+    ck = CHAIN_F32;
+    nloss = Bp / 16;
   } else if (chain) {
     // the chain leaves per-tile loss partials; the update launch stores their sum
     int Bp = 0;
@@ -1599,10 +1717,17 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       break;
     }
     case INF_STAGE_CHAIN: {
-      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && use_chain(p), "chain stage needs a bf16 training batch");
+      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && (use_chain(p) || p->last_chain == CHAIN_F32),
+                    "chain stage needs a fused training batch");
       // replay on the saved inputs; the step counter it advances is restored by the caller
       const double Lh = p->L;
-      if (p->last_chain == 3) {
+      if (p->last_chain == CHAIN_F32) {
+        rc = run_chainf(p, b, Bp, nullptr, st);
+        f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+        // fp32 weight images streamed per workgroup (L2 -> CU); rows in; blocked operands out
+        by = (double)(Bp / 16) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * 4.0 +
+             B * (3.0 * p->k_pad * 4.0 + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * 4.0;
+      } else if (p->last_chain == 3) {
         rc = run_chain3(p, b, Bp, nullptr, st);
         f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
         // every workgroup streams W_0, W_y and the hidden weights twice over (L2 -> CU);
