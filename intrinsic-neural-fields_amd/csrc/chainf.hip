@@ -252,19 +252,27 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
         if (kb + 1 < UPL) bread(kb + 1, bq[(kb + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         const f32x4(&bv)[2] = bq[kb & 1];
+        // (tiles interleaved: consecutive MFMAs update different accumulators)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int q = 0; q < 8; ++q)
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
+          for (int j = 0; j < TN; ++j)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fr[kb % D][j][q >> 2][q & 3], bv[q >> 2][q & 3], acc[j], 0, 0, 0);
+#ifndef CF_NO_LOADS  // diagnostics: the MFMAs on the prologue's fragments (wrong results)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int h = 0; h < 2; ++h)
             fr[kb % D][j][h] = kb + D < UPL ? frag(crs, ckb + kb + D, j, h) : frag(nrs, nkb + kb + D - UPL, j, h);
+#endif
         __builtin_amdgcn_sched_barrier(0);
       }
       if (!B.last) return;
+#ifdef CF_NO_EPI  // diagnostics: the weight stream and MFMAs with the barriers alone
+      if (B.phase == nfwd - 1) lbar();
+      lbar();
+      return;
+#endif
 
       // ---- epilogue of phase p ---------------------------------------------------------
       const int p = B.phase;

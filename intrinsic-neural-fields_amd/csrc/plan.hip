@@ -200,7 +200,7 @@ int build_layout(inf_plan* p) {
   // fragment images: the hidden H x H weights, forward and transposed, and W_0 / W_y
   // (forward) for the register-streamed chains -- bf16 (chain3.hip, rchain.hip) or fp32
   // (chainf.hip, the fp32 mode's fused step)
-  if ((p->mode == INF_MODE_BF16 || p->mode == INF_MODE_FP32) && (H == 128 || H == 256)) {
+  if ((p->mode == INF_MODE_BF16 || p->mode == INF_MODE_FP32 || p->mode == INF_MODE_BF16X3) && (H == 128 || H == 256)) {
     for (auto& g : p->segs) {
       if (!g.gemm) continue;
       const bool hidden = g.layer >= 1 && g.layer <= L - 2 && g.sub == 0 && g.R == H && g.C == H;
@@ -638,7 +638,7 @@ int ensure_rowmajor(inf_plan* p, hipStream_t st) {
 // fused chain3 steps in bf16 leave the row-major shadows to ensure_rowmajor
 // (INF_EAGER_SHADOWS=1: every update rewrites all shadows)
 int step_shadow_mode(const inf_plan* p, int chain) {
-  return ((chain == 3 && p->mode == INF_MODE_BF16) || (chain == CHAIN_F32 && p->mode == INF_MODE_FP32)) &&
+  return ((chain == 3 && p->mode == INF_MODE_BF16) || (chain == CHAIN_F32 && p->mode != INF_MODE_BF16)) &&
                  std::getenv("INF_EAGER_SHADOWS") == nullptr
              ? 2
              : 1;
@@ -991,11 +991,13 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
-// The fp32 mode's fused step (chainf.hip): eigenfunction tables up to k_pad = 1024, fp32
-// fragment images, a dW GEMM over 16-ray blocked operands (K = Bp split dw_splits ways in
-// 32-ray k-tiles).  INF_NO_CHAINF=1: the layered kernels.
+// The fused step of the fp32 parity modes (chainf.hip): eigenfunction tables up to k_pad =
+// 1024, fp32 fragment images, a dW GEMM over 16-ray blocked operands (K = Bp split
+// dw_splits ways in 32-ray k-tiles).  fp32 mode: exact-f32 dW; bf16x3 mode: the forward
+// and dX chain in exact f32 as well (more accurate than its 6 / 3 split products), the dW
+// GEMM on 3 split-bf16 products (gemm_mode).  INF_NO_CHAINF=1: the layered kernels.
 bool use_chainf(const inf_plan* p, const inf_batch* b, int Bp) {
-  if (p->mode != INF_MODE_FP32 || !chainf_supported(p->H, p->L, p->k_pad)) return false;
+  if ((p->mode != INF_MODE_FP32 && p->mode != INF_MODE_BF16X3) || !chainf_supported(p->H, p->L, p->k_pad)) return false;
   if (b->table == nullptr || b->encoding != INF_ENC_NONE || b->table_dtype != INF_DTYPE_F32 || b->vids == nullptr ||
       b->rgb == nullptr)
     return false;
