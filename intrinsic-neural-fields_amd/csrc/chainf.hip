@@ -162,6 +162,7 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
     lbar();  // barrier R: ray records in LDS
 
     // ---- gather: the fp32 feature tile, 16-byte chunks (4 columns) per thread -----------
+#ifndef CF_NO_GATHER  // diagnostics: no feature gather (garbage X)
     {
       const int cpr = k_pad >> 2;
       const int nch = BM * cpr;
@@ -198,6 +199,7 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
         }
       }
     }
+#endif
     // every load so far has landed (the fragment prologue was issued before the gather;
     // vmcnt is in order): clears the compiler's scoreboard of the gather registers
     __builtin_amdgcn_s_waitcnt(0);
@@ -270,6 +272,12 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
       if (!B.last) return;
 #ifdef CF_NO_EPI  // diagnostics: the weight stream and MFMAs with the barriers alone
       if (B.phase == nfwd - 1) lbar();
+      {  // keep every MFMA (and its loads) alive
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) t += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+        if (t == 1234.5f) act[lane] = 1;
+      }
       lbar();
       return;
 #endif
@@ -456,6 +464,9 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
     // words) and the wave writes 1 KiB contiguous; 4 groups of reads issued per batch
     const int tf = lane >> 2, tq = lane & 3;
     auto copy_block = [&](const char* tile, int rowb, int nf, float* dst) {
+#ifdef CF_NO_STORE  // diagnostics: the store wave mirrors the barriers only
+      return;
+#endif
       const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
       constexpr int NB = 4;
 #pragma unroll 1
