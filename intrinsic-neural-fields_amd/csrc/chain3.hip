@@ -70,7 +70,6 @@ constexpr int C3BM = 16;  // rays per 16-row MFMA tile (= per workgroup at NR = 
 // us per step faster that way (profiles/r02/sweeps/gather_policy.log); config D with it 2.5
 // us slower
 constexpr int C3_CPOL_NT = 2;
-constexpr size_t C3_NT_TABLE_BYTES = (size_t)256 << 20;
 
 // 1 if x != 0 else 0, as one v_min_u32 (asm: the compiler turns min(x, 1) back into a
 // compare whose lane mask lives in an SGPR pair)
@@ -134,12 +133,17 @@ struct L3 {
 // once, at its first block (two barriers: everyone is done with the previous chunk /
 // the new one is in LDS), and the store wave copies its X^T between them.
 // NR: 16-ray tiles per workgroup (1, or C3_NR_WIDE for large batches; not with ENC).
-template <int H, int LOSS, bool ENC, bool XC, int NR>
+// ZP: the input layers were computed ahead of the chain (igemm.hip: Z = [W_0; W_y] X^T in
+// the accumulator layout, X^T written by its gather): no gather here, phase 0 is the
+// layer-0 epilogue on Z, the skip layer adds W_y x from LDS (staged by the store wave with
+// direct-to-LDS loads) in its epilogue, and the weight stream holds the hidden layers only.
+template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
   using C = L3<H, NR>;
   constexpr int BM = C::BM, TN = C::TN, UPL = C::UPL;
   constexpr int NV = TN * 4;  // accumulator values per lane and ray tile
   static_assert(NR == 1 || !ENC, "wide tiles: eigenfunction tables only");
+  static_assert(!ZP || (NR == 1 && !ENC && !XC), "precomputed input layers: narrow whole-tile schedule only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = a.L;
   const int k_pad = a.k_pad;
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     };
     // ---- gather: ray records of the 16 rays (index, vertex ids, barycentrics), one
     // thread per (ray, corner) ------------------------------------------------------------
-    if (tid < BM * 3 && a.xpre == nullptr) {
+    if (!ZP && tid < BM * 3 && a.xpre == nullptr) {
       int64_t offset = a.idx_offset;
       if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
       const int rl = tid / 3, i = tid % 3;
@@ -333,6 +337,16 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       }
     };
+    // ZP: the lane's layer-0 pre-activations (its accumulators of phase 0), ahead of the
+    // fragment prologue in the in-order vmcnt queue
+    f32x4 z0[ZP ? TN : 1];
+    if constexpr (ZP) {
+      const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.zin), (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        z0[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rz, ((unsigned)(blockIdx.x * (2 * H / 16) + t0 + j) * 64u + lane) * 16u, 0, 0));
+    }
     // the first block's fragments, in k order (the loop's waits assume that order); issued
     // after the dependent ray-record loads so those are not queued behind them
     {
@@ -404,7 +418,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
         *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
       }
-    } else {
+    } else if constexpr (!ZP) {
       const int n0 = XC ? min(C::KC, k_pad) : k_pad;
       if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, std::true_type{}, 0, n0);
       else if (a.gather_nt || (XC && NR == 1)) gather_cols(std::integral_constant<int, 4>{}, std::false_type{}, std::true_type{}, 0, n0);
@@ -414,7 +428,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // prologue was issued before it; vmcnt is in order): an explicit wait here costs
     // nothing and clears the compiler's scoreboard of the gather registers, which it
     // otherwise drains the whole fragment ring for (vmcnt(0)) at every stream block
-    __builtin_amdgcn_s_waitcnt(0);
+    // (ZP: no gather; the compiler's counted waits cover Z's loads, the prologue stays in flight)
+    if constexpr (!ZP) __builtin_amdgcn_s_waitcnt(0);
     stamp(3 * nphase + 4);
     lbar();  // barrier 0: feature tile in LDS
     stamp(3 * nphase + 5);
@@ -533,141 +548,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         for (int j = 0; j < TN; ++j) *reinterpret_cast<f32x4*>(park_slot(n, j)) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-    // one block of the weight stream (and the epilogue of the phase it ends)
-    auto run_block = [&](int i) {
-      const C3Block& B = a.blk[i];
-      const C3Block& Bn = a.blk[i + 1 < a.nblk ? i + 1 : i];
-      if (i == 0 || a.blk[i - 1].last) stamp(1 + 3 * B.phase);
-      // ---- MFMAs of block i; slot kb % D refilled with k-block kb + D of this block or
-      // of block i+1 (the last block reloads itself: harmless loads keep waits exact)
-      if constexpr (XC) {
-        if (B.flags & C3F_GATHER) {
-          const int c = B.flags >> C3F_CHUNK_SHIFT;
-          lbar();  // G1: every wave is done with the previous chunk (and the store wave with its X^T)
-          const int nc = min(C::KC, k_pad - c * C::KC);
-          // chunked tiles (k_pad > C3_KC) are the large tables: non-temporal rows (wide
-          // tiles: the MALL policy decides, as for the whole-tile gather); one load set
-          // per thread in the wide variant (four accumulator sets are live)
-          constexpr int GRX = NR == 1 ? 2 : 1;
-#ifdef EXP_NOGATHER
-          if (NR > 1) {} else
-#endif
-          if (a.table_big)
-            gather_cols(std::integral_constant<int, GRX>{}, std::true_type{}, std::true_type{}, c * C::KC, nc);
-          else if (NR == 1 || a.gather_nt)
-            gather_cols(std::integral_constant<int, GRX>{}, std::false_type{}, std::true_type{}, c * C::KC, nc);
-          else
-            gather_cols(std::integral_constant<int, GRX>{}, std::false_type{}, std::false_type{}, c * C::KC, nc);
-          lbar();  // G2: chunk c in LDS
-        }
-        if (B.flags & C3F_SWAP) {
-#pragma unroll
-          for (int n = 0; n < NR; ++n)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              if constexpr (PARK) {
-                f32x4* q = reinterpret_cast<f32x4*>(park_slot(n, j));
-                const f32x4 t = *q;
-                *q = acc[n][j];
-                acc[n][j] = t;
-              } else {
-                const f32x4 t = acc[n][j];
-                acc[n][j] = accy[n][j];
-                accy[n][j] = t;
-              }
-            }
-        }
-      }
-      const __amdgpu_buffer_rsrc_t crs = rsrc_of(B.img);
-      const __amdgpu_buffer_rsrc_t nrs = rsrc_of(Bn.img);
-      const bool from_x = B.a_x != 0;
-      const char* act_in = act + (B.phase & 1) * C::ACT_BYTES;
-      const int ak0 = B.ak0, ckb = B.kb0, nkb = Bn.kb0;
-      // B operand: the feature tile (natural k order) or the activation tile.  One base per
-      // block and a branch-free per-k-block offset (a select on the uniform source flag):
-      // a pointer ternary inside the unrolled loop had compiled to scalar branches between
-      // the MFMAs.  X: chunk (m 4 + g4) ^ r16 of row r16 with m = ak0 + kb, and ak0 a
-      // multiple of UPL keeps the xor inside the k-block's 32-chunk (UPL = 8) / 16-chunk
-      // (UPL = 4) span: xlane + 64 ak0 + ((kb 4 + g4) ^ r16) 16.  Ray tile n: 16 rows of X
-      // / one activation tile further
-      const int fx = from_x ? 1 : 0;
-      const char* bbase = from_x ? xlane + ak0 * 64 : act_in;
-      const int nstride = from_x ? 16 * xrow : C::TILE_BYTES;
-      auto bread = [&](int kb, int n) -> bf16x8 {
-        const int xo = ((kb * 4 + g4) ^ r16) << 4;
-        const int ao = kb * 1024 + aoffs[kb & 3];
-        return *reinterpret_cast<const bf16x8*>(bbase + n * nstride + ao + fx * (xo - ao));
-      };
-      if constexpr (NR == 1) {
-        // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
-        // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
-        // latency is exposed at every k-block, behind only TN MFMAs)
-        // (not in the chunked variant: its second accumulator set leaves no room -- it spills)
-        constexpr bool BPF = !XC;
-        bf16x8 bq[2];
-        if constexpr (BPF) bq[0] = bread(0, 0);
-#pragma unroll
-        for (int kb = 0; kb < UPL; ++kb) {
-          if constexpr (BPF) {
-            if (kb + 1 < UPL) bq[(kb + 1) & 1] = bread(kb + 1, 0);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          const bf16x8 bv = BPF ? bq[kb & 1] : bread(kb, 0);
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[0][j], 0, 0, 0);
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        // wide tiles: NR TN MFMAs per k block; ray tile n's operand for k block kb + 1 is
-        // read right after its MFMAs of kb (one operand register set, rolling)
-#ifdef C3_WIDE_NOBQ
-        constexpr bool RB = false;
-#else
-        constexpr bool RB = true;
-#endif
-        auto mfma_block = [&](f32x4 (&tgt)[NR][TN]) {
-          bf16x8 bq[NR];
-          if constexpr (RB) {
-#pragma unroll
-            for (int n = 0; n < NR; ++n) bq[n] = bread(0, n);
-          }
-#pragma unroll
-          for (int kb = 0; kb < UPL; ++kb) {
-#pragma unroll
-            for (int n = 0; n < NR; ++n) {
-              const bf16x8 bv = RB ? bq[n] : bread(kb, n);
-#pragma unroll
-              for (int j = 0; j < TN; ++j)
-                tgt[n][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, tgt[n][j], 0, 0, 0);
-              if (RB && kb + 1 < UPL) bq[n] = bread(kb + 1, n);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        };
-        mfma_block(acc);
-      }
-#ifdef C3_STREAM_ONLY  // diagnostics: the weight stream and MFMAs alone (wrong results);
-                      // with C3_STREAM_BARRIERS also the two barriers per phase
-      if (B.last) {
-        stamp(2 + 3 * B.phase);
-#ifdef C3_STREAM_BARRIERS
-        lbar();
-        lbar();
-#endif
-      }
-      return;
-#endif
-      if (!B.last) return;
-
+    // epilogue of phase p (after the phase's last stream block)
+    auto epilogue = [&](const int p) {
       // ---- epilogue of phase p ---------------------------------------------------------
-      const int p = B.phase;
       stamp(2 + 3 * p);
       // no barrier before the writes: this epilogue's tiles (act (p + 1) & 1, colsum p & 1)
       // were last read in phase p - 1 / copied by the store wave before B2(p - 1)
@@ -706,10 +589,11 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               f32x4 wy = f32x4{0.f, 0.f, 0.f, 0.f};
               if constexpr (ACCY) wy = accy[n][j];
               else if constexpr (PARK) wy = *reinterpret_cast<const f32x4*>(wy_slot(n, j));
+              else if constexpr (ZP) wy = *reinterpret_cast<const f32x4*>(xs + ((t0 + j) * 64 + lane) * 16);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 float v = z[r];
-                if constexpr (XC) v += wy[r];
+                if constexpr (XC || ZP) v += wy[r];
                 z[r] = (v + bv[r]) + yv[r];
               }
             } else {
@@ -914,6 +798,147 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       lbar();  // B2: tile of the next phase and this phase's partials complete
       stamp(3 + 3 * p);
     };
+
+    // one block of the weight stream (and the epilogue of the phase it ends)
+    auto run_block = [&](int i) {
+      const C3Block& B = a.blk[i];
+      const C3Block& Bn = a.blk[i + 1 < a.nblk ? i + 1 : i];
+      if (i == 0 || a.blk[i - 1].last) stamp(1 + 3 * B.phase);
+      // ---- MFMAs of block i; slot kb % D refilled with k-block kb + D of this block or
+      // of block i+1 (the last block reloads itself: harmless loads keep waits exact)
+      if constexpr (XC) {
+        if (B.flags & C3F_GATHER) {
+          const int c = B.flags >> C3F_CHUNK_SHIFT;
+          lbar();  // G1: every wave is done with the previous chunk (and the store wave with its X^T)
+          const int nc = min(C::KC, k_pad - c * C::KC);
+          // chunked tiles (k_pad > C3_KC) are the large tables: non-temporal rows (wide
+          // tiles: the MALL policy decides, as for the whole-tile gather); one load set
+          // per thread in the wide variant (four accumulator sets are live)
+          constexpr int GRX = NR == 1 ? 2 : 1;
+#ifdef EXP_NOGATHER
+          if (NR > 1) {} else
+#endif
+          if (a.table_big)
+            gather_cols(std::integral_constant<int, GRX>{}, std::true_type{}, std::true_type{}, c * C::KC, nc);
+          else if (NR == 1 || a.gather_nt)
+            gather_cols(std::integral_constant<int, GRX>{}, std::false_type{}, std::true_type{}, c * C::KC, nc);
+          else
+            gather_cols(std::integral_constant<int, GRX>{}, std::false_type{}, std::false_type{}, c * C::KC, nc);
+          lbar();  // G2: chunk c in LDS
+        }
+        if (B.flags & C3F_SWAP) {
+#pragma unroll
+          for (int n = 0; n < NR; ++n)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              if constexpr (PARK) {
+                f32x4* q = reinterpret_cast<f32x4*>(park_slot(n, j));
+                const f32x4 t = *q;
+                *q = acc[n][j];
+                acc[n][j] = t;
+              } else {
+                const f32x4 t = acc[n][j];
+                acc[n][j] = accy[n][j];
+                accy[n][j] = t;
+              }
+            }
+        }
+      }
+      const __amdgpu_buffer_rsrc_t crs = rsrc_of(B.img);
+      const __amdgpu_buffer_rsrc_t nrs = rsrc_of(Bn.img);
+      const bool from_x = B.a_x != 0;
+      const char* act_in = act + (B.phase & 1) * C::ACT_BYTES;
+      const int ak0 = B.ak0, ckb = B.kb0, nkb = Bn.kb0;
+      // B operand: the feature tile (natural k order) or the activation tile.  One base per
+      // block and a branch-free per-k-block offset (a select on the uniform source flag):
+      // a pointer ternary inside the unrolled loop had compiled to scalar branches between
+      // the MFMAs.  X: chunk (m 4 + g4) ^ r16 of row r16 with m = ak0 + kb, and ak0 a
+      // multiple of UPL keeps the xor inside the k-block's 32-chunk (UPL = 8) / 16-chunk
+      // (UPL = 4) span: xlane + 64 ak0 + ((kb 4 + g4) ^ r16) 16.  Ray tile n: 16 rows of X
+      // / one activation tile further
+      const int fx = from_x ? 1 : 0;
+      const char* bbase = from_x ? xlane + ak0 * 64 : act_in;
+      const int nstride = from_x ? 16 * xrow : C::TILE_BYTES;
+      auto bread = [&](int kb, int n) -> bf16x8 {
+        const int xo = ((kb * 4 + g4) ^ r16) << 4;
+        const int ao = kb * 1024 + aoffs[kb & 3];
+        return *reinterpret_cast<const bf16x8*>(bbase + n * nstride + ao + fx * (xo - ao));
+      };
+      if constexpr (NR == 1) {
+        // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
+        // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
+        // latency is exposed at every k-block, behind only TN MFMAs)
+        // (not in the chunked variant: its second accumulator set leaves no room -- it spills)
+        constexpr bool BPF = !XC;
+        bf16x8 bq[2];
+        if constexpr (BPF) bq[0] = bread(0, 0);
+#pragma unroll
+        for (int kb = 0; kb < UPL; ++kb) {
+          if constexpr (BPF) {
+            if (kb + 1 < UPL) bq[(kb + 1) & 1] = bread(kb + 1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          const bf16x8 bv = BPF ? bq[kb & 1] : bread(kb, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, acc[0][j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        // wide tiles: NR TN MFMAs per k block; ray tile n's operand for k block kb + 1 is
+        // read right after its MFMAs of kb (one operand register set, rolling)
+#ifdef C3_WIDE_NOBQ
+        constexpr bool RB = false;
+#else
+        constexpr bool RB = true;
+#endif
+        auto mfma_block = [&](f32x4 (&tgt)[NR][TN]) {
+          bf16x8 bq[NR];
+          if constexpr (RB) {
+#pragma unroll
+            for (int n = 0; n < NR; ++n) bq[n] = bread(0, n);
+          }
+#pragma unroll
+          for (int kb = 0; kb < UPL; ++kb) {
+#pragma unroll
+            for (int n = 0; n < NR; ++n) {
+              const bf16x8 bv = RB ? bq[n] : bread(kb, n);
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                tgt[n][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bv, tgt[n][j], 0, 0, 0);
+              if (RB && kb + 1 < UPL) bq[n] = bread(kb + 1, n);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        };
+        mfma_block(acc);
+      }
+#ifdef C3_STREAM_ONLY  // diagnostics: the weight stream and MFMAs alone (wrong results);
+                      // with C3_STREAM_BARRIERS also the two barriers per phase
+      if (B.last) {
+        stamp(2 + 3 * B.phase);
+#ifdef C3_STREAM_BARRIERS
+        lbar();
+        lbar();
+#endif
+      }
+      return;
+#endif
+      if (!B.last) return;
+      epilogue(B.phase);
+    };
+    if constexpr (ZP) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[0][j] = z0[j];
+      stamp(1);
+      epilogue(0);
+    }
 #pragma unroll 1
     for (int i = 0; i < a.nblk; ++i) run_block(i);
 #ifdef C3_STREAM_ONLY
@@ -951,6 +976,15 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 #pragma unroll
       for (int o = 0; o < 3; ++o) *reinterpret_cast<rowv*>(w7s + o * H + lane * CPL) = tw[o];
       if (lane < 3) w7s[3 * H + lane] = tb;
+    }
+    // ZP: the workgroup's W_y x tiles (H / 16 KiB) into the idle feature-tile region, lane-
+    // linear (1 KiB per 16-feature tile: the compute lanes' accumulator slots); landed before
+    // B2(0), read in the skip layer's epilogue (phase s >= 1)
+    if constexpr (ZP) {
+      const char* zy = reinterpret_cast<const char*>(a.zin) + ((int64_t)blockIdx.x * (2 * H / 16) + H / 16) * 1024 + lane * 16;
+#pragma unroll
+      for (int t = 0; t < H / 16; ++t)
+        __builtin_amdgcn_global_load_lds(zy + t * 1024, (__attribute__((address_space(3))) void*)(xs + t * 1024), 16, 0, 0);
     }
     lbar();  // barrier 0: feature tile in LDS
     if (a.count_step && blockIdx.x == 0 && lane == 0) a.ctrl->step += 1;
@@ -1044,9 +1078,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         copy_tiles(x_addr, k_pad, a.XT, c * (C::KC / 32), min((c + 1) * C::KC, k_pad) / 32);
       }
       if (NR > 1) lbar();  // BX: the feature-tile region takes the parked W_y x
-    } else {
+    } else if constexpr (!ZP) {
       copy_tiles(x_addr, k_pad, a.XT, 0, xs_mid);
     }
+    if constexpr (ZP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W_y x landed before B2(0)
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
       const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(d, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -1079,7 +1114,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       if (p < nfwd) {
         const int l = p;
         if (!head_phase) copy_tiles(act_addr, H, a.YT[l], 0, H / 32);
-        if (!XC && p == a.s - 1) copy_tiles(x_addr, k_pad, a.XT, xs_mid, xs_total);
+        if (!XC && !ZP && p == a.s - 1) copy_tiles(x_addr, k_pad, a.XT, xs_mid, xs_total);
         if (head_phase) {
           copy_tiles(act_addr, H, a.dZT[L - 2], 0, H / 32);
           copy_out(cs, a.colsum[L - 2] + part0 * H, H * 4);
@@ -1099,18 +1134,18 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   }
 }
 
-template <int H, int LOSS, bool ENC, bool XC, int NR>
+template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP = false>
 int launch3_enc(const Chain3Args& a, hipStream_t stream) {
   using C = L3<H, NR>;
   const int lds = C::lds_bytes(a.L, a.kc, XC);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC, NR>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC, NR, ZP>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
-  chain3_kernel<H, LOSS, ENC, XC, NR><<<dim3((unsigned)(a.rows / C::BM)), dim3(C3_THREADS), lds, stream>>>(a);
+  chain3_kernel<H, LOSS, ENC, XC, NR, ZP><<<dim3((unsigned)(a.rows / C::BM)), dim3(C3_THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -1124,6 +1159,7 @@ int launch3_loss(const Chain3Args& a, int bm, hipStream_t stream) {
     INF_CHECK_ARG(a.kc == a.k_pad, "chain3: chunked wide tiles need H = 256");
     return launch3_enc<H, LOSS, false, false, C3_NR_WIDE>(a, stream);
   }
+  if (a.zin != nullptr) return launch3_enc<H, LOSS, false, false, 1, true>(a, stream);
   if (a.encoding != INF_ENC_NONE) return launch3_enc<H, LOSS, true, false, 1>(a, stream);
   if (a.kc < a.k_pad) return launch3_enc<H, LOSS, false, true, 1>(a, stream);
   return launch3_enc<H, LOSS, false, false, 1>(a, stream);
@@ -1159,6 +1195,11 @@ int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
   INF_CHECK_ARG(bm == C3BM || (a.encoding == INF_ENC_NONE && a.xpre == nullptr), "chain3: wide tiles gather tables only");
   INF_CHECK_ARG(a.rows % bm == 0 && a.rows >= bm, "chain3: rows must be a multiple of the tile height");
   INF_CHECK_ARG(a.nphase == 2 * a.L - 3, "chain3: phases");
+  // precomputed input layers: the narrow whole-tile schedule, W_y x staged in the idle
+  // feature-tile region (16 rays x H fp32 <= 16 x k_pad bf16)
+  INF_CHECK_ARG(a.zin == nullptr || (bm == C3BM && a.encoding == INF_ENC_NONE && a.xpre == nullptr &&
+                                     a.kc == a.k_pad && a.k_pad >= 2 * a.H),
+                "chain3: precomputed input layers need the whole-tile schedule");
   INF_CHECK_ARG(a.nblk >= 1 && a.nblk <= C3_MAX_BLOCKS, "chain3: weight-stream blocks");
   INF_CHECK_ARG(a.rgb != nullptr && (a.encoding != INF_ENC_NONE ? a.pos != nullptr : a.table != nullptr) &&
                     a.vids != nullptr && a.bary != nullptr && a.XT != nullptr,

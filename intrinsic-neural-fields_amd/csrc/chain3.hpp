@@ -60,6 +60,10 @@ struct Chain3Args {
   // pre-gathered features (inf_prefetch_batch): row b of xpre [rows][k_pad] bf16 is ray b's
   // feature row, read instead of gathering three table rows (null: gather)
   const bf16* xpre;
+  // precomputed input layers (igemm.hip): Z = [W_0; W_y] X^T without biases, fp32, in the
+  // accumulator layout ([rows / 16][2H / 16] KiB); X^T already written (null: the kernel
+  // gathers and streams W_0 / W_y itself)
+  const float* zin;
   // weight stream: phases 0..L-2 forward layer p, L-1.. dX of layer (L-2) - (p - (L-1))
   C3Block blk[C3_MAX_BLOCKS];
   int32_t nblk, nphase;
@@ -93,6 +97,8 @@ struct Chain3Args {
 // stream (4096 rays -> 256 workgroups).  Larger batches fill the chip with 16-ray tiles many
 // times over and pay the stream once per 16 rays: there a workgroup takes C3_NR_WIDE tiles
 // (64 rays; 65,536 rays -> 1024 workgroups), each weight fragment feeding C3_NR_WIDE MFMAs.
+// tables above this size are read with non-temporal row loads (chain3.hip, igemm.hip)
+constexpr size_t C3_NT_TABLE_BYTES = (size_t)256 << 20;
 constexpr int64_t CHAIN3_MAX_ROWS = 8192;
 constexpr int C3_NR_WIDE = 4;
 constexpr int64_t CHAIN3_WIDE_MAX_ROWS = (int64_t)1 << 24;

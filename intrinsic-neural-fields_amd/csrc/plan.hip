@@ -21,6 +21,7 @@
 #include "gemm.hpp"
 #include "head.hpp"
 #include "fgemm.hpp"
+#include "igemm.hpp"
 #include "lgemm.hpp"
 #include "rchain.hpp"
 #include "blaslt.hpp"
@@ -80,6 +81,7 @@ struct inf_plan {
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_tables_b = 0, o_ws_end = 0;
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
+  int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (igemm.hip), fp32 [bp_max][2H]
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
   int n_aux_items = 0;
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
@@ -265,6 +267,8 @@ int build_layout(inf_plan* p) {
   p->o_x0t = take((int64_t)p->k_pad * Bp * p->esz);
   if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS)
     for (int i = 0; i < 2; ++i) p->o_xp[i] = take(Bp * p->k_pad * 2);
+  if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS && igemm_supported(H, p->k_pad, Bp))
+    p->o_zin = take(Bp * 2 * H * 4);
   const int64_t max_parts =
       std::max<int64_t>({chain_max_partials(Bp), std::min<int64_t>(Bp, CHAIN3_WIDE_MAX_ROWS) / 16, (int64_t)p->grid_hb});
   for (int l = 0; l < L - 1; ++l) {
@@ -937,7 +941,48 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   const bool xc = p->k_pad > kc;
   a.kc = kc;
   a.nchunk = (int)ceil_div(p->k_pad, a.kc);
-  if (!xc) {
+  // INF_ZP=1: the input layers ahead of the chain (igemm.hip): gather X / X^T, then
+  // Z = [W_0; W_y] X^T as a GEMM tiled over output features; the chain's stream keeps the
+  // hidden layers only.  Opt-in: at config B the chain drops 42.3 -> 29.4 us but the gather
+  // (9.2 us) and the GEMM (10.6 us) cost more than the 1 MB per-CU L2 stream they replace
+  // -- the GEMM's X tiles come from the MALL at its per-CU rate (profiles/r03/s3/zp_step.json)
+  const bool zp = p->o_zin >= 0 && b->encoding == INF_ENC_NONE && xpre == nullptr && !xc && chain3_bm(Bp) == 16 &&
+                  igemm_supported(H, p->k_pad, Bp) && b->num_vertices * (int64_t)p->k_pad * 2 < ((int64_t)1 << 32) &&
+                  std::getenv("INF_ZP") != nullptr;
+  if (zp) {
+    XGatherArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.table = a.table;
+    g.num_vertices = b->num_vertices;
+    g.k_pad = p->k_pad;
+    g.vids = b->vids;
+    g.vid_dtype = b->vid_dtype;
+    g.bary = b->bary;
+    g.ray_idx = b->ray_idx;
+    g.idx_dtype = b->idx_dtype;
+    g.idx_offset = b->idx_offset;
+    g.num_rays = b->num_rays;
+    g.num_src = b->num_source_rays;
+    g.ctrl = p->ctrl;
+    g.offset_from_ctrl = b->offset_from_ctrl;
+    g.batch = b->batch;
+    g.rows = Bp;
+    g.gather_nt = (size_t)b->num_vertices * (size_t)p->k_pad * 2 > C3_NT_TABLE_BYTES;
+    g.X = p->W<bf16>(p->o_x0);
+    g.XT = p->W<bf16>(p->o_x0t);
+    if ((rc = launch_xgather(g, st))) return rc;
+    IGemmArgs q;
+    std::memset(&q, 0, sizeof(q));
+    q.X = g.X;
+    q.rows = Bp;
+    q.k_pad = p->k_pad;
+    q.H = H;
+    q.W0 = img(p->weight_seg(0, 0), true);
+    q.Wy = img(p->weight_seg(s, 1), true);
+    q.Z = p->W<float>(p->o_zin);
+    if ((rc = launch_igemm(q, st))) return rc;
+    a.zin = q.Z;
+  } else if (!xc) {
     for (int i = 0; i < nx; ++i)
       if ((rc = add(img(p->weight_seg(0, 0), true), i * upl, 1, i * upl, 0, i == nx - 1))) return rc;
   } else {
@@ -958,8 +1003,8 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     }
   }
   for (int l = 1; l <= L - 2; ++l) {
-    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || l != s))) return rc;
-    if (l == s && !xc)
+    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || zp || l != s))) return rc;
+    if (l == s && !xc && !zp)
       for (int i = 0; i < nx; ++i)
         if ((rc = add(img(p->weight_seg(s, 1), true), i * upl, 1, i * upl, l, i == nx - 1))) return rc;
   }

@@ -345,6 +345,52 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
         assert np.abs(gw[n] - gl[n]).max() / scale < 1e-5, n
 
 
+@pytest.mark.parametrize("name,B,bad", [("B", 4096, False), ("R", 4096, False), ("B", 2048, True)])
+def test_chain3_precomputed_input_layers(name, B, bad, monkeypatch):
+    """chain3's ZP schedule (INF_ZP=1, csrc/igemm.hip: gather X / X^T, then Z = [W_0; W_y] X^T
+    as a GEMM ahead of the chain; the chain streams the hidden layers only) against the
+    default in-kernel gather + input-layer stream on one batch.  Layer 0 runs the same MFMA k
+    order into one accumulator: bitwise.  The skip layer adds W_y x as a separate fp32 sum
+    (the chunked schedule's order), so a bf16 activation may round the other way: RGB 5e-4,
+    gradients 1e-2 of max, the chain-vs-layered bars.  `bad`: out-of-range vertex ids and
+    ray-index values read as zero rows / zero targets on both paths."""
+    rng = np.random.default_rng(8)
+    k, H, L, s = CFG[name]
+    V = 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    perm = torch.randperm(B)
+    if bad:
+        vids[::97, 1] = V + 5
+        perm[::131] = B + 7
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda(), validate=not bad)
+    out = {}
+    for tag in ("zp", "nozp"):
+        if tag == "zp":
+            monkeypatch.setenv("INF_ZP", "1")
+        else:
+            monkeypatch.delenv("INF_ZP")
+        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, batch=B, ray_idx=perm.cuda()), pred, apply_adam=False)
+        c = plan.read_ctrl()
+        assert plan.last_step_path() == "chain3", plan.last_step_path()
+        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"])
+    pz, gz, lz = out["zp"]
+    pn, gn, ln = out["nozp"]
+    assert np.isfinite(pz).all()
+    np.testing.assert_allclose(pz, pn, atol=5e-4)
+    assert abs(lz - ln) <= 1e-3 * max(1.0, abs(ln)), (lz, ln)
+    for n in O.layer_names(L, s):
+        scale = max(np.abs(gn[n]).max(), 1e-12)
+        err = np.abs(gz[n] - gn[n]).max() / scale
+        assert err < 1e-2, (n, err)
+
+
 def test_bf16_chain_render_matches_layered(monkeypatch):
     """bf16 render of the G7 frame: the forward-only register chain (rchain.hip, default),
     the LDS-ring chain (INF_NO_RCHAIN) and the layered kernels (INF_NO_CHAIN).  The register

@@ -1,0 +1,9 @@
+#!/bin/bash
+# ZP timing iteration: ZP kernel tests, the step line, its kernel trace
+set -o pipefail
+O=gpurun_out
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_prefetch.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/r3s_tests.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --only none --no-cpu-baseline --extra-batches "" > $O/r3s_bench.log 2>&1 || exit 1
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_r3s -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --only none --no-cpu-baseline --extra-batches "" > $O/r3s_prof.log 2>&1
