@@ -14,11 +14,11 @@ from collections import defaultdict
 
 
 def short(name):
-    if "chain3_kernel" in name and ("Lb0ELb1E" in name or "false, true>" in name):
+    if "chain3_kernel" in name and ("Lb0ELb1E" in name or "false, true>" in name or "false, true, 1," in name):
         return "chain3_kernel<chunked>"
     if name.startswith("Cijk_"):  # hipBLASLt's kernels (the projection GEMM)
         return "hipblaslt_gemm"
-    for key in ("rproj_kernel", "rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
+    for key in ("proj_gemm_kernel", "fgemm_kernel", "igemm_kernel", "xgather_kernel", "chainf_kernel", "rproj_kernel", "rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
                 "head_bwd_kernel", "pack_kernel", "ctrl_advance_kernel"):
         if key in name:
             tail = ""
@@ -66,7 +66,7 @@ def counters(d, counter):
 # bench.py stage -> kernel, for the per-launch traffic table bench.py reads
 STAGE_KERNEL = {"chain3": "chain3_kernel", "dw_gemm": "lgemm_kernel", "update": "update_kernel",
                 "rchain": "rchain_kernel", "chain3_chunked": "chain3_kernel<chunked>",
-                "rproj": "rproj_kernel", "project_gemm": "hipblaslt_gemm"}
+                "rproj": "rproj_kernel", "project_gemm": "proj_gemm_kernel"}
 
 
 def main(root, tag=None):
