@@ -814,7 +814,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           // chunked tiles (k_pad > C3_KC) are the large tables: non-temporal rows (wide
           // tiles: the MALL policy decides, as for the whole-tile gather); one load set
           // per thread in the wide variant (four accumulator sets are live)
-          constexpr int GRX = NR == 1 ? 2 : 1;
+#ifndef C3_GRX_WIDE
+#define C3_GRX_WIDE 1
+#endif
+          constexpr int GRX = NR == 1 ? 2 : C3_GRX_WIDE;
 #ifdef EXP_NOGATHER
           if (NR > 1) {} else
 #endif

@@ -492,6 +492,51 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
         }
       }
     };
+    // split_images: [16 rays][nf] fp32 tile -> the hi / lo bf16 fragment images of the
+    // [nf features][rows] operand.  The workgroup's 16 rays are half h of 32-ray k block
+    // b0 / 32: per 16-feature tile one 512-byte piece, lane slot i + 16 rh = feature i, rays
+    // 8 rh .. 8 rh + 7 (natural k order).  Lane (i, rh, tt) builds the slot of tile
+    // 2 s + tt from 8 fp32 reads, so one store writes the pieces of two tiles (2 x 512
+    // contiguous bytes) per image
+    auto copy_split = [&](const char* tile, int rowb, int nf, void* img) {
+#ifdef CF_NO_STORE
+      return;
+#endif
+      char* hi = reinterpret_cast<char*>(img);
+      const int64_t part = (int64_t)nf * a.rows * 2;  // bytes of one image
+      const __amdgpu_buffer_rsrc_t rh_ = __builtin_amdgcn_make_buffer_rsrc(hi, (short)0, 0x7FFFFFFF, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rl_ = __builtin_amdgcn_make_buffer_rsrc(hi + part, (short)0, 0x7FFFFFFF, 0x00020000);
+      const int fi = lane & 15, rh = (lane >> 4) & 1, tt = lane >> 5;
+      const unsigned base = (unsigned)((b0 >> 5) * (nf / 16) * 1024 + ((b0 >> 4) & 1) * 512 + (lane & 31) * 16);
+      // NB passes per batch: all their LDS reads issued before the first conversion
+      constexpr int NB = 4;
+#pragma unroll 1
+      for (int s0 = 0; s0 < nf / 32; s0 += NB) {
+        float x[NB][8];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int f = 16 * (2 * min(s0 + u, nf / 32 - 1) + tt) + fi;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            x[u][e] = *reinterpret_cast<const float*>(tile + cf_off(rowb, 8 * rh + e, f >> 2) + 4 * (f & 3));
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          if (s0 + u >= nf / 32) break;
+          c3::u16x8 vh, vl;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bf16 h = (bf16)x[u][e];
+            vh[e] = __builtin_bit_cast(unsigned short, h);
+            vl[e] = __builtin_bit_cast(unsigned short, (bf16)(x[u][e] - (float)h));
+          }
+          // write-through (sc1), as the blocked operands: the dW GEMM reads them next launch
+          const unsigned o = base + (unsigned)(2 * (s0 + u) + tt) * 1024u;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vh), rh_, o, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vl), rl_, o, 0, 16);
+        }
+      }
+    };
     auto copy_out = [&](const char* src, void* dst, int bytes) {
       char* d = reinterpret_cast<char*>(dst);
       const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(d, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -499,7 +544,8 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
         __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(src + c), rd, (unsigned)c, 0, 16);
     };
     // X^T while the compute waves stream W_0 (phase 0: the longest)
-    copy_block(xs, xrow, k_pad, a.XT + (int64_t)blockIdx.x * k_pad * 16);
+    if (a.split_images) copy_split(xs, xrow, k_pad, a.XT);
+    else copy_block(xs, xrow, k_pad, a.XT + (int64_t)blockIdx.x * k_pad * 16);
 #pragma unroll 1
     for (int p = 0; p < nphase; ++p) {
       const bool head_phase = p == nfwd - 1;
@@ -510,9 +556,13 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
       const int64_t part0 = blockIdx.x;
       if (p < nfwd) {
         const int l = p;
-        if (!head_phase) copy_block(act_p, C::ROWB, H, a.YT[l] + part0 * H * 16);
+        if (!head_phase) {
+          if (a.split_images) copy_split(act_p, C::ROWB, H, a.YT[l]);
+          else copy_block(act_p, C::ROWB, H, a.YT[l] + part0 * H * 16);
+        }
         if (head_phase) {
-          copy_block(act_p, C::ROWB, H, a.dZT[L - 2] + part0 * H * 16);
+          if (a.split_images) copy_split(act_p, C::ROWB, H, a.dZT[L - 2]);
+          else copy_block(act_p, C::ROWB, H, a.dZT[L - 2] + part0 * H * 16);
           copy_out(cs, a.colsum[L - 2] + part0 * H, H * 4);
           copy_out(reinterpret_cast<const char*>(hws), a.hw_part + part0 * 3 * H, 3 * H * 4);
           if (lane < 3) a.hb_part[part0 * 3 + lane] = hbs[lane];
@@ -521,7 +571,8 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
         }
       } else {
         const int l = (L - 2) - (p - nfwd);
-        copy_block(act_p, C::ROWB, H, a.dZT[l - 1] + part0 * H * 16);
+        if (a.split_images) copy_split(act_p, C::ROWB, H, a.dZT[l - 1]);
+        else copy_block(act_p, C::ROWB, H, a.dZT[l - 1] + part0 * H * 16);
         copy_out(cs, a.colsum[l - 1] + part0 * H, H * 4);
       }
     }

@@ -63,6 +63,11 @@ struct ChainFArgs {
   float inv_count;
   inf_ctrl* ctrl;
   int32_t count_step;
+  // bf16x3 mode's dW on the split-bf16 register GEMM (lgemm.hip SPLIT): X^T, Y^T and dZ^T
+  // are written instead as pairs of bf16 fragment images (lgemm.hpp: rows = features,
+  // k = rays), hi = bf16(x) at the buffer's start and lo = bf16(x - hi) right after the R x
+  // rows hi image
+  int32_t split_images;
 };
 
 constexpr int CHAINF_MAX_KPAD = 1024;  // the 16 x k_pad fp32 feature tile stays in LDS

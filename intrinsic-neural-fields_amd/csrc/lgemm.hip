@@ -22,6 +22,11 @@
 // Epilogues: bias + ReLU into row-major C (bf16 / f32) and a plain transposed copy
 // (input GEMM), or the transposed f32 tile into a split-K slab (weight gradients: the
 // block computes dW^T, the slab holds dW as the update kernel reads it).
+//
+// SPLIT (the bf16x3 parity mode's dW): each operand is a pair of images, hi = bf16(x) and
+// lo = bf16(x - hi) (chainf.hip writes them), and every k block runs three MFMAs per tile,
+// lo*hi + hi*lo + hi*hi (gemm.hip's split-bf16 order, small terms first) -- the dW of an
+// fp32 product to ~2^-16 relative at 2x the operand bytes and 3x the MFMAs of the bf16 step.
 #include <algorithm>
 
 #include "adam_dev.hpp"
@@ -42,7 +47,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define LG_RA 4
 #endif
 
-template <int BM>
+template <int BM, int NP = 1>
 struct LG {
   static constexpr int TM = BM / 16, TN = 2;
   static constexpr int D = LG_DEPTH;  // B units in flight per wave (fragment register ring)
@@ -52,15 +57,18 @@ struct LG {
   static constexpr int A_STAGE = BM * 128;  // bytes: BM rows x 64 bf16
   static constexpr int CLD = LG_BN + 4;     // f32 staging row stride
   // + the fused update's LDS (adam_dev tile + scalars) and a flag word at the end
-  static constexpr int LDS = std::max(std::max(2 * A_STAGE, BM * CLD * 4), ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
+  // NP operand parts (SPLIT: hi, lo) per stage
+  static constexpr int LDS = std::max(std::max(2 * NP * A_STAGE, BM * CLD * 4), ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
   static_assert(ACH >= 1 && BM * 8 % 256 == 0, "A stage must split over 256 threads");
 };
 
 __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM, bool FUSED>
+template <int BM, bool FUSED, bool SPLIT = false>
 __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
-  using C = LG<BM>;
+  static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
+  constexpr int NP = SPLIT ? 2 : 1;
+  using C = LG<BM, NP>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -108,6 +116,9 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   const char* a_base = reinterpret_cast<const char*>(P.Af) + (int64_t)(k_begin >> 5) * a_kstride;
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a_base), (short)0, 0x7FFFFFFF, 0x00020000);
+  const char* a_base_lo = SPLIT ? reinterpret_cast<const char*>(P.Af_lo) + (int64_t)(k_begin >> 5) * a_kstride : a_base;
+  const __amdgpu_buffer_rsrc_t ral =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a_base_lo), (short)0, 0x7FFFFFFF, 0x00020000);
   const int a_step = 2 * a_kstride;  // bytes per 64-deep stage
   const int a_tile0 = (P.a_row0 + m0) >> 4;
   unsigned aoff[ACH];
@@ -119,27 +130,38 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   // ---- B: fragment image; this wave's two 16-row tiles ---------------------------------
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(P.Bf), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbl =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(SPLIT ? P.Bf_lo : P.Bf), (short)0, 0x7FFFFFFF, 0x00020000);
   const unsigned boff = (unsigned)((((P.b_row0 + n0) >> 4) + 2 * wc) * 64 + lane) * 16u;
   const int bstep = P.b_tiles * 1024;  // bytes per unit
   const int kb0 = k_begin >> 5;
 
-  auto loadA = [&](int st, u32x4 (&dst)[ACH]) {
+  // (SPLIT: part p = 0 hi, 1 lo; a stage's LDS holds the hi tiles, then the lo tiles)
+  auto loadA = [&](int st, u32x4 (&dst)[NP][ACH]) {
     st = min(st, nst - 1);  // past the end: reload the last stage (never stored)
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) dst[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, aoff[i], st * a_step, 0);
-  };
-  auto storeA = [&](int buf, const u32x4 (&src)[ACH]) {
+    for (int pp = 0; pp < NP; ++pp)
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int q = tid + 256 * i;
-      *reinterpret_cast<u32x4*>(smem + buf * C::A_STAGE + q * 16) = src[i];
-    }
+      for (int i = 0; i < ACH; ++i)
+        dst[pp][i] = __builtin_amdgcn_raw_buffer_load_b128(pp ? ral : ra, aoff[i], st * a_step, 0);
   };
-  auto loadB = [&](int u, bf16x8 (&dst)[TN]) {
+  auto storeA = [&](int buf, const u32x4 (&src)[NP][ACH]) {
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp)
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int q = tid + 256 * i;
+        *reinterpret_cast<u32x4*>(smem + (buf * NP + pp) * C::A_STAGE + q * 16) = src[pp][i];
+      }
+  };
+  auto loadB = [&](int u, bf16x8 (&dst)[NP][TN]) {
     u = min(u, nun - 1);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      dst[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + j * 1024, (kb0 + u) * bstep, 0));
+    for (int pp = 0; pp < NP; ++pp)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        dst[pp][j] = __builtin_bit_cast(
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(pp ? rbl : rb, boff + j * 1024, (kb0 + u) * bstep, 0));
   };
 
   f32x4 acc[TM][TN];
@@ -148,8 +170,8 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ar[RA][ACH];
-  bf16x8 fr[D][TN];
+  u32x4 ar[RA][NP][ACH];
+  bf16x8 fr[D][NP][TN];
 #pragma unroll
   for (int q = 0; q < RA; ++q) {
     loadA(q, ar[q]);
@@ -173,18 +195,26 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
       const int nxt = (ss + 1) % RA;  // compile-time after unrolling
       if (s + 1 < nst) storeA((s + 1) & 1, ar[nxt]);
       loadA(s + 1 + RA, ar[nxt]);
-      const char* As = smem + (s & 1) * C::A_STAGE;
+      const char* As = smem + (s & 1) * NP * C::A_STAGE;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int slot = (2 * ss + kk) % D;
-        bf16x8 av[TM];
+        bf16x8 av[NP][TM];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(As + (kk * TM + i) * 1024 + lane * 16);
+        for (int pp = 0; pp < NP; ++pp)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            av[pp][i] = *reinterpret_cast<const bf16x8*>(As + pp * C::A_STAGE + (kk * TM + i) * 1024 + lane * 16);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], fr[slot][j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (SPLIT) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], fr[slot][0][j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], fr[slot][1][j], acc[i][j], 0, 0, 0);
+            }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], fr[slot][0][j], acc[i][j], 0, 0, 0);
+          }
         loadB(2 * s + kk + D, fr[slot]);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -314,16 +344,16 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   }
 }
 
-template <int BM, bool FUSED>
+template <int BM, bool FUSED, bool SPLIT = false>
 int launch_typed(const LgemmBatch& b, hipStream_t stream) {
-  constexpr int lds = LG<BM>::LDS;
+  constexpr int lds = LG<BM, SPLIT ? 2 : 1>::LDS;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    lds));
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
-  lgemm_kernel<BM, FUSED><<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256), lds, stream>>>(b);
+  lgemm_kernel<BM, FUSED, SPLIT><<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -338,6 +368,8 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     LgemmProblem& p = b.p[i];
     if (p.splits < 1) p.splits = 1;
     INF_CHECK_ARG(p.Af != nullptr && p.Bf != nullptr, "lgemm: null operand");
+    INF_CHECK_ARG(!b.split || (p.Af_lo != nullptr && p.Bf_lo != nullptr && p.slab != nullptr),
+                  "lgemm: split operands need both parts and a slab");
     INF_CHECK_ARG(p.M > 0 && p.M % bm == 0 && p.N > 0 && p.N % LG_BN == 0, "lgemm: M/N not tile multiples");
     INF_CHECK_ARG(p.K > 0 && p.K % (64 * LG_RA * p.splits) == 0, "lgemm: K per split must be a multiple of 64 RA");
     INF_CHECK_ARG(p.a_row0 % 16 == 0 && p.a_row0 + p.M <= 16 * p.a_tiles && p.b_row0 % 16 == 0 &&
@@ -357,6 +389,8 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
                     "lgemm: fused update needs split-K slabs (at most 4), 16-byte rows");
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: fused update reduces the slabs");
   }
+  INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
+  if (b.split) return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
   if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }

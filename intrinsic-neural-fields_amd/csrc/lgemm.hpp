@@ -28,6 +28,9 @@ struct LgemmProblem {
   const bf16* Bf;
   int32_t b_tiles;  // R / 16
   int32_t b_row0;
+  // LgemmBatch::split: the lo parts of both operands (same layout; Af / Bf are the hi parts)
+  const bf16* Af_lo;
+  const bf16* Bf_lo;
   int32_t M, N, K;  // M % BM == 0, N % 128 == 0, (K / splits) % 256 == 0
   int32_t splits;
   // epilogue (non-split): + bias[n], ReLU, row-major C and/or plain transposed CT
@@ -61,6 +64,8 @@ struct LgemmBatch {
   const AdamItem* aux_items;
   int32_t* counters;
   AdamArgs adam;
+  // split-bf16 operands (hi + lo images, three MFMAs per k block: the bf16x3 mode's dW)
+  int32_t split;
 };
 
 // Rows per block for an M: 64 (the shapes of config B) or 32.

@@ -234,8 +234,10 @@ int build_layout(inf_plan* p) {
   // 4096 rays: 2 splits (224 blocks of 8 k-steps, one per CU) beat 4 (448 blocks of 4 on
   // 256 CUs, the same 8-step critical path) by the halved slab bytes: step 73.0 -> 71.3 us
   // (tools/split_sweep.sh)
-  if (d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
-  if (d.mode == INF_MODE_BF16 && mb <= 4096 && S > 2) S = 2;
+  // (the bf16x3 mode's dW runs on the same register GEMM over split operands: lgemm SPLIT)
+  const bool reg_dw = d.mode == INF_MODE_BF16 || d.mode == INF_MODE_BF16X3;
+  if (reg_dw && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
+  if (reg_dw && mb <= 4096 && S > 2) S = 2;
   // the 64-ray chain tiles' dW through lgemm (shapes fgemm does not tile) stream
   // K = Bp / S rays per block in 256-ray steps: 10,240 rays take 8 splits, not 16
   while (d.mode == INF_MODE_BF16 && mb > CHAIN3_MAX_ROWS && S > 1 && mb % (256 * (int64_t)S) != 0) S /= 2;
@@ -434,6 +436,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
 }
 
 bool use_fgemm(const inf_plan* p, int Bp, int splits);
+bool use_split_lgemm(const inf_plan* p, int Bp);
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr,
                      int bucket = 0);
 
@@ -473,8 +476,53 @@ int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
 
 // chain (2, 3): Y^T / dZ^T were written by the fused chain in its 16-ray blocked layout;
 // with the register-streamed chain (3) Y_0^T comes plain from the input GEMM
+// bf16x3 mode behind the fused fp32 chain: the chain writes X^T / Y^T / dZ^T as hi / lo bf16
+// fragment images and the dW runs on the register GEMM with three MFMAs per k block
+// (lgemm.hip SPLIT) instead of gemm.hip's split-bf16 over 16-ray blocked fp32 operands.
+// INF_NO_SPLIT_LGEMM=1: the blocked operands and gemm.hip.
+bool use_split_lgemm(const inf_plan* p, int Bp) {
+  if (p->mode != INF_MODE_BF16X3 || std::getenv("INF_NO_SPLIT_LGEMM") != nullptr) return false;
+  if (Bp % p->dw_splits != 0 || (Bp / p->dw_splits) % (64 * 4) != 0) return false;
+  for (const ParamSeg& g : p->segs)
+    if (g.gemm && (g.c_pad % 64 != 0 || g.R % LG_BN != 0)) return false;
+  return true;
+}
+
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket) {
   const int H = p->H, s = p->s;
+  if (chain == CHAIN_F32 && use_split_lgemm(p, Bp)) {
+    INF_CHECK_ARG(fuse == nullptr, "split-operand dW: no fused update");
+    const int splits = bucket ? p->bucket_splits : p->dw_splits;
+    LgemmBatch lb;
+    std::memset(&lb, 0, sizeof(lb));
+    lb.split = 1;
+    for (size_t i = 0; i < p->segs.size(); ++i) {
+      const ParamSeg& g = p->segs[i];
+      if (!g.gemm) continue;
+      if ((bucket == 1 && g.off < p->grad_split) || (bucket == 2 && g.off >= p->grad_split)) continue;
+      INF_CHECK_ARG(lb.nprob < LGEMM_MAX_PROBLEMS, "lgemm: too many weight matrices");
+      LgemmProblem& q = lb.p[lb.nprob++];
+      const int l = g.layer;
+      const bool from_input = (l == 0) || (l == s && g.sub == 1);
+      const int R = from_input ? p->k_pad : H;
+      bf16* a_img = from_input ? p->W<bf16>(p->o_x0t) : p->W<bf16>(p->o_yt[l - 1]);
+      bf16* b_img = p->W<bf16>(p->o_dZT[l]);
+      q.Af = a_img;
+      q.Af_lo = a_img + (int64_t)R * Bp;
+      q.a_tiles = R / 16;
+      q.Bf = b_img;
+      q.Bf_lo = b_img + (int64_t)H * Bp;
+      q.b_tiles = H / 16;
+      q.M = g.c_pad;
+      q.N = g.R;
+      q.K = Bp;
+      q.splits = splits;
+      q.slab = p->W<float>(p->o_slab[i]);
+      q.slab_ld = g.c_pad;
+      q.slab_stride = (int64_t)g.R * g.c_pad;
+    }
+    return launch_lgemm(lb, 64, st);
+  }
   if (chain == 3) {
     // bucket 1 / 2: only the matrices of arena [grad_split, P) / [0, grad_split), with
     // bucket_splits partials each (the data-parallel bucketed step)
@@ -1130,6 +1178,7 @@ int run_chainf(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.inv_count = (float)(1.0 / (double)cnt);
   a.ctrl = p->ctrl;
   a.count_step = 1;
+  a.split_images = use_split_lgemm(p, Bp) ? 1 : 0;
   return launch_chainf(a, st);
 }
 

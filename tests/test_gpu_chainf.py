@@ -107,3 +107,31 @@ def test_chainf_adam_steps_match_oracle():
     plan.forward(plan.make_batch(features=feats), pf, save=False)
     p2, _ = O.mlp_forward(tr.w, feats.cpu().numpy(), L, s)
     np.testing.assert_allclose(pf.cpu().numpy(), p2, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,B", [("B", 4096), ("R", 2048)])
+def test_bf16x3_split_register_dw_matches_blocked(name, B, monkeypatch):
+    """The bf16x3 mode's dW on the register GEMM over hi / lo bf16 fragment images
+    (lgemm.hip SPLIT, the default) against gemm.hip's split-bf16 over 16-ray blocked fp32
+    operands (INF_NO_SPLIT_LGEMM=1): the same three products per k block, other summation
+    orders -- the reduced gradients within 2e-5 of each tensor's max, RGB and loss bitwise
+    (the chain is the same launch)."""
+    k, H, L, s = CFG[name]
+    w0 = weights(golden(f"g2_forward_{name}.npz"))
+    E, vids, bary, rgb, src = rays(k, 2000, B, seed=53, clear=(w0, L, s))
+    out = {}
+    for tag in ("split", "blocked"):
+        if tag == "blocked":
+            monkeypatch.setenv("INF_NO_SPLIT_LGEMM", "1")
+        plan, params, w = make_plan(name, mode="bf16x3", loss="L2", max_batch=B, adam=True)
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
+        assert plan.last_step_path() == "chain_f32", plan.last_step_path()
+        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), plan.read_ctrl()["loss_sum"])
+    np.testing.assert_array_equal(out["split"][0], out["blocked"][0])
+    assert out["split"][2] == out["blocked"][2]
+    for n in O.layer_names(L, s):
+        ref = out["blocked"][1][n]
+        scale = max(np.abs(ref).max(), 1e-12)
+        err = float(np.abs(out["split"][1][n] - ref).max() / scale)
+        assert err < 2e-5, (n, err)
