@@ -44,6 +44,11 @@ constexpr int CF_LDS_CAP = 160 * 1024;
 #ifndef CF_DEPTH
 #define CF_DEPTH 4
 #endif
+// 16-byte feature chunks per thread per gather round (4: two rounds at k_pad = 1024 with the
+// fragment prologue in flight; 8: one round, the prologue after it)
+#ifndef CF_GR
+#define CF_GR 4
+#endif
 
 template <int H>
 struct LF {
@@ -146,6 +151,7 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
       rbary[rl * 3 + i] = w;
       rvid[BM * 4 + tid] = ok;
     }
+#if CF_GR <= 4
     // the first block's fragments (k order: the loop's waits assume it)
     {
       const CFBlock& B0 = a.blk[0];
@@ -159,6 +165,7 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+#endif
     lbar();  // barrier R: ray records in LDS
 
     // ---- gather: the fp32 feature tile, 16-byte chunks (4 columns) per thread -----------
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
     {
       const int cpr = k_pad >> 2;
       const int nch = BM * cpr;
-      constexpr int GR = 4;
+      constexpr int GR = CF_GR;
 #pragma unroll 1
       for (int q0 = tid; q0 < nch; q0 += CF_CT * GR) {
         f32x4 ev[GR][3];
@@ -197,6 +204,22 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
             *reinterpret_cast<f32x4*>(xs + cf_off(xrow, r, ch)) = o;
           }
         }
+      }
+    }
+#endif
+#if CF_GR > 4
+    // one gather round (CF_GR = 8): the fragment prologue after it, outside the gather's
+    // register peak
+    {
+      const CFBlock& B0 = a.blk[0];
+      const __amdgpu_buffer_rsrc_t rs0 = rsrc_of(B0.img);
+#pragma unroll
+      for (int kb = 0; kb < D; ++kb) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) fr[kb][j][h] = frag(rs0, B0.kb0 + kb, j, h);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #endif
@@ -523,17 +546,21 @@ __global__ __launch_bounds__(CF_THREADS) void chainf_kernel(const ChainFArgs a) 
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
           if (s0 + u >= nf / 32) break;
-          c3::u16x8 vh, vl;
+          // pairs through v_cvt_pk_bf16_f32 (RNE, the bits of a scalar conversion): hi, then
+          // lo = bf16(x - hi) with hi unpacked exactly (the store wave's VALU time is what
+          // the split images add to the chain)
+          u32x4 vh, vl;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bf16 h = (bf16)x[u][e];
-            vh[e] = __builtin_bit_cast(unsigned short, h);
-            vl[e] = __builtin_bit_cast(unsigned short, (bf16)(x[u][e] - (float)h));
+          for (int e = 0; e < 8; e += 2) {
+            const unsigned w = pack_bf16x2(x[u][e], x[u][e + 1]);
+            vh[e >> 1] = w;
+            vl[e >> 1] = pack_bf16x2(x[u][e] - __builtin_bit_cast(float, w << 16),
+                                     x[u][e + 1] - __builtin_bit_cast(float, w & 0xFFFF0000u));
           }
           // write-through (sc1), as the blocked operands: the dW GEMM reads them next launch
           const unsigned o = base + (unsigned)(2 * (s0 + u) + tt) * 1024u;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vh), rh_, o, 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vl), rl_, o, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(vh, rh_, o, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(vl, rl_, o, 0, 16);
         }
       }
     };

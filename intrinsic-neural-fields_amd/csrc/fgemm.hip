@@ -20,9 +20,11 @@
 // vmcnt(0) wait -- ran at 0.29 of the MFMA peak: profiles/r03.)
 // Output.  Split s writes its partial dW (f32, the update launch's slab layout): a lane's
 // 4 accumulators of a tile are 4 consecutive input features of one output feature -- one
-// 16-byte store.  Blocks are ordered [problem][split][row tile][column tile] and remapped
-// so consecutive ones share an XCD: the tiles of one split read the same rays' dZ / input
-// panels, once from HBM and then from that XCD's L2.
+// 16-byte store.  Blocks are ordered [split][problem][row tile][column tile] and remapped
+// so consecutive ones share an XCD: every tile of one split reads the same rays' panels, so
+// a panel two problems share (X^T for W_0 and W_y, dZ_s^T for the skip layer's two halves,
+// dZ_l^T for the column tiles of one matrix) comes from HBM once and then from that XCD's
+// L2 -- problem-major order had put W_0's and W_y's tiles of a split on different XCDs.
 #include "fgemm.hpp"
 #include "c3common.hpp"
 
@@ -68,14 +70,14 @@ __global__ __launch_bounds__(FG_THREADS, 1) void fgemm_kernel(const FgemmBatch b
   const int orig = (int)blockIdx.x;
   const int q8 = nblocks / 8, r8 = nblocks % 8, xcd = orig % 8;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int split = bid / b.tiles_per_split;
+  int r = bid - split * b.tiles_per_split;
   int pi = 0;
 #pragma unroll 1
-  while (pi + 1 < b.nprob && bid >= b.p[pi + 1].block_begin) ++pi;
+  while (pi + 1 < b.nprob && r >= b.p[pi + 1].block_begin) ++pi;
   const FgemmProblem& P = b.p[pi];
-  const int tiles_m = P.M / FG_TILE, tiles_n = P.N / FG_TILE;
-  int r = bid - P.block_begin;
-  const int split = r / (tiles_m * tiles_n);
-  r -= split * tiles_m * tiles_n;
+  const int tiles_n = P.N / FG_TILE;
+  r -= P.block_begin;
   const int tm = r / tiles_n, tn = r - tm * tiles_n;
   // the split's 32-ray k-steps
   const int KT = b.K / FG_KS;
@@ -175,17 +177,18 @@ int launch_fgemm(FgemmBatch& b, hipStream_t stream) {
                   "fgemm: image / slab extents");
     // 32-bit buffer offsets into each split's slab
     INF_CHECK_ARG((int64_t)q.N * q.slab_ld * 4 < ((int64_t)1 << 31), "fgemm: slab too large");
-    q.block_begin = (int32_t)blocks;
-    blocks += (int64_t)(q.M / FG_TILE) * (q.N / FG_TILE) * b.splits;
+    q.block_begin = (int32_t)blocks;  // first tile of this problem inside a split
+    blocks += (int64_t)(q.M / FG_TILE) * (q.N / FG_TILE);
   }
-  INF_CHECK_ARG(blocks >= 1 && blocks < ((int64_t)1 << 31), "fgemm: block count");
-  b.total_blocks = (int32_t)blocks;
+  INF_CHECK_ARG(blocks >= 1 && blocks * b.splits < ((int64_t)1 << 31), "fgemm: block count");
+  b.tiles_per_split = (int32_t)blocks;
+  b.total_blocks = (int32_t)(blocks * b.splits);
   static bool attr = false;
   if (!attr) {
     INF_HIP_TRY(hipFuncSetAttribute((const void*)fgemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FG_LDS));
     attr = true;
   }
-  fgemm_kernel<<<dim3((unsigned)blocks), dim3(FG_THREADS), FG_LDS, stream>>>(b);
+  fgemm_kernel<<<dim3((unsigned)b.total_blocks), dim3(FG_THREADS), FG_LDS, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }

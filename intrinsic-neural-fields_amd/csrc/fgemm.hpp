@@ -21,7 +21,7 @@ struct FgemmProblem {
   int32_t M, N;  // multiples of FG_TILE
   float* slab;
   int64_t slab_ld, slab_stride;
-  int32_t block_begin;  // first block of this problem (set by launch_fgemm)
+  int32_t block_begin;  // first tile of this problem within a split (set by launch_fgemm)
 };
 
 struct FgemmBatch {
@@ -30,6 +30,7 @@ struct FgemmBatch {
   int32_t K;       // rays (multiple of FG_BK)
   int32_t splits;  // split-K factor shared by every problem
   int32_t total_blocks;
+  int32_t tiles_per_split;  // blocks of one split: every problem's tiles (set by launch_fgemm)
 };
 
 // True when every matrix of the step is a whole number of 256 x 256 tiles.
