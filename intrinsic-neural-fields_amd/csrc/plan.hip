@@ -521,7 +521,9 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       q.slab_ld = g.c_pad;
       q.slab_stride = (int64_t)g.R * g.c_pad;
     }
-    return launch_lgemm(lb, 64, st);
+    // rows per block: 64 (INF_SPLIT_LGEMM_BM=32: twice the blocks, half the A tile each)
+    const char* e = std::getenv("INF_SPLIT_LGEMM_BM");
+    return launch_lgemm(lb, e != nullptr && std::atoi(e) == 32 ? 32 : 64, st);
   }
   if (chain == 3) {
     // bucket 1 / 2: only the matrices of arena [grad_split, P) / [0, grad_split), with
