@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 3 closing run at HEAD: whole GPU suite + smoke
+set -o pipefail
+O=gpurun_out
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/fin2_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> $O/fin2_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/fin2_smoke.log 2>&1
