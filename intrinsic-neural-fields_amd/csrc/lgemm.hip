@@ -225,14 +225,22 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   if (stl != nullptr) stl[2] = wall_clock64();
 
   // ---- epilogue: accumulators -> f32 LDS tile ------------------------------------------
+  // split-K slabs are read back column-wise (16 lanes down one column, rows 4 apart): the
+  // column index is XOR-swizzled by row / 4 so those reads spread over the banks (they were
+  // 8-way conflicts at CLD = 132; the writes stay conflict-free -- the XOR stays inside a
+  // lane group's 16 columns).  The row-major C / CT epilogue reads rows as vectors: unswizzled
   float* Cs = reinterpret_cast<float*>(smem);
   constexpr int CLD = C::CLD;
+  const bool swz = P.slab != nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Cs[(i * 16 + g4 * 4 + r) * CLD + wc * 32 + j * 16 + r16] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + g4 * 4 + r;
+        Cs[row * CLD + ((wc * 32 + j * 16 + r16) ^ (swz ? (row >> 2) & 15 : 0))] = acc[i][j][r];
+      }
   __syncthreads();
 
   if (P.slab != nullptr) {
@@ -244,8 +252,9 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
 #pragma unroll 4
     for (int q = tid; q < LG_BN * MQ; q += 256) {
       const int col = q / MQ, mq = q - col * MQ;
-      const f32x4 v = {Cs[(mq * 4 + 0) * CLD + col], Cs[(mq * 4 + 1) * CLD + col], Cs[(mq * 4 + 2) * CLD + col],
-                       Cs[(mq * 4 + 3) * CLD + col]};
+      const int cs = col ^ (mq & 15);  // rows mq 4 .. mq 4 + 3 share the swizzle
+      const f32x4 v = {Cs[(mq * 4 + 0) * CLD + cs], Cs[(mq * 4 + 1) * CLD + cs], Cs[(mq * 4 + 2) * CLD + cs],
+                       Cs[(mq * 4 + 3) * CLD + cs]};
       const int64_t eo = (int64_t)(n0 + col) * P.slab_ld + m0 + mq * 4;
       if (FUSED || LG_SLAB_SC1)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (unsigned)(eo * 4), 0, 16);
