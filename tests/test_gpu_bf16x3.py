@@ -54,7 +54,7 @@ def test_backward_bf16x3_golden(name, loss):
     print(name, loss, "grad err (of max)", worst)
 
 
-@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1")])
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1"), ("B", "L2")])
 def test_fused_step_bf16x3_golden(name, loss):
     d = golden(f"g3_step_{name}_{loss}.npz")
     k, H, L, s = CFG[name]
@@ -72,7 +72,8 @@ def test_fused_step_bf16x3_golden(name, loss):
         assert_adam_close(w1[n], d["w1:" + n], lr=1e-4, steps=1, name=n, atol=2e-6)
 
 
-@pytest.mark.parametrize("tag,name,L,s", [("A_L2", "A", 4, 2), ("R_L1", "R", 6, 3)])
+@pytest.mark.parametrize("tag,name,L,s", [("A_L2", "A", 4, 2), ("R_L1", "R", 6, 3), ("B_L2", "B", 8, 4),
+                                          ("B_L1", "B", 8, 4)])
 def test_adam20_bf16x3_golden(tag, name, L, s):
     d = golden(f"g4_adam20_{tag}.npz")
     loss = tag.split("_")[1]

@@ -205,13 +205,25 @@ def _val_curve(tmp_path):
     return [r["value"] for r in rows if r["tag"] == "Val Epoch-PSNR"]
 
 
-@pytest.mark.parametrize("mode,tol,layered", [("fp32", 0.1, False), ("fp32", 0.05, True), ("bf16", 0.2, False)])
-def test_trainer_g8_training_curve(tmp_path, mode, tol, layered, monkeypatch):
-    """Statistical PSNR parity: 12 epochs of the reference's synthetic G8 run.  In fp32 the
-    first five epochs match the reference to 1e-5 dB on both fp32 paths; later the
-    trajectory is chaotic in the summation order (L1 loss, lr 1e-3): the fused fp32 chain
-    (chainf.hip) ends 0.08 dB off it, the layered kernels 0.023 dB -- two fp32 orders, neither
-    the reference's.  The tight fp32 bar on a non-chaotic run is G13 (every epoch 0.05 dB)."""
+def g8_reference_spread():
+    """The reference's own G8 curve moves by this much (dB, max over epochs) when only its
+    fp32 summation order changes: nn.DataParallel's scatter over 2 / 4 replicas, 1 / 3 / 8
+    CPU threads, float64 (tests/golden/make_golden.py g8_spread -> g8_spread.npz).  The
+    largest is DataParallel over two replicas at the last epoch (0.142 dB)."""
+    s = golden("g8_spread.npz")
+    return max(float(np.abs(s[v] - s["ref"]).max()) for v in s.files if v != "ref")
+
+
+@pytest.mark.parametrize("mode,layered", [("fp32", False), ("fp32", True), ("bf16", False)])
+def test_trainer_g8_training_curve(tmp_path, mode, layered, monkeypatch):
+    """Statistical PSNR parity: 12 epochs of the reference's synthetic G8 run (L1, lr 1e-3).
+    The first five epochs match the reference to 1e-3 dB on both fp32 paths (the reference's
+    own summation-order variants agree there to 1e-4).  Later the trajectory depends on the
+    fp32 summation order: the reference itself, run under nn.DataParallel's 2-replica
+    scatter, ends 0.142 dB from its single-device curve (g8_spread.npz).  So the fp32 bar is
+    that measured spread, read from the fixture.  The fused fp32 chain (chainf.hip) was
+    seen 0.080 dB off, the layered kernels 0.023 dB.  bf16 keeps SURVEY §8(d)'s 0.2 dB.  The
+    tight fp32 bar on a non-chaotic run is G13 (0.05 dB at every epoch)."""
     if layered:
         monkeypatch.setenv("INF_NO_CHAINF", "1")
     tr, d = _g8_trainer(tmp_path, mode)
@@ -220,6 +232,11 @@ def test_trainer_g8_training_curve(tmp_path, mode, tol, layered, monkeypatch):
     assert len(val) == len(d["val_psnr"])
     if mode == "fp32":
         np.testing.assert_allclose(val[:5], d["val_psnr"][:5], atol=1e-3)
+        tol = g8_reference_spread()
+        assert 0.05 <= tol < 0.2
+    else:
+        tol = 0.2
+    print(mode, "layered" if layered else "fused", np.round(np.array(val) - d["val_psnr"], 4).tolist(), "bar", tol)
     np.testing.assert_allclose(val, d["val_psnr"], atol=tol)
     assert os.path.exists(os.path.join(tmp_path, "model.pt"))
     assert os.path.exists(os.path.join(tmp_path, "model_last_epoch.pt"))

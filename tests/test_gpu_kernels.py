@@ -125,9 +125,12 @@ def test_backward_grads_golden(name, loss):
         assert err < 1e-4, (n, err)
 
 
-@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1")])
+@pytest.mark.parametrize("name,loss", [("A", "L2"), ("A", "L1"), ("A", "cauchy"), ("R", "L1"), ("B", "L2")])
 def test_fused_train_step_golden(name, loss):
-    """inf_train_step (gather-free features form) + Adam vs the reference's step-1 weights."""
+    """inf_train_step (gather-free features form) + Adam vs the reference's step-1 weights.
+    Config B (the headline MLP) is held like the multi-step checks: Adam's step 1 moves each
+    weight by lr * sign(g), so an element whose gradient is at rounding level may take the
+    opposite step (<= 0.1 % of elements, by at most 2 lr)."""
     d = golden(f"g3_step_{name}_{loss}.npz")
     k, H, L, s = CFG[name]
     plan, params, w = make_plan(name, loss=loss, adam=True)
@@ -142,15 +145,20 @@ def test_fused_train_step_golden(name, loss):
     np.testing.assert_allclose(pred.cpu().numpy(), d["pred"], atol=1e-5)
     w1 = arena_to_dict(params, w, L, s)
     for n in O.layer_names(L, s):
-        np.testing.assert_allclose(w1[n], d["w1:" + n], atol=2e-6, err_msg=n)
+        if name == "B":
+            assert_adam_close(w1[n], d["w1:" + n], lr=1e-4, steps=1, name=n, atol=2e-6)
+        else:
+            np.testing.assert_allclose(w1[n], d["w1:" + n], atol=2e-6, err_msg=n)
 
 
-@pytest.mark.parametrize("tag,name,L,s", [("A_L2", "A", 4, 2), ("A_cauchy", "A", 4, 2), ("R_L1", "R", 6, 3)])
+@pytest.mark.parametrize("tag,name,L,s", [("A_L2", "A", 4, 2), ("A_cauchy", "A", 4, 2), ("R_L1", "R", 6, 3),
+                                          ("B_L2", "B", 8, 4), ("B_L1", "B", 8, 4)])
 def test_adam20_golden(tag, name, L, s):
     d = golden(f"g4_adam20_{tag}.npz")
     loss = tag.split("_")[1]
     plan, params, w = make_plan(name, loss=loss, adam=True)
-    plan.set_lr(float(d["lr"]))
+    lr = float(d["lr"])
+    plan.set_lr(lr)
     for i in range(d["features"].shape[0]):
         feats = torch.from_numpy(d["features"][i]).cuda()
         rgb = torch.from_numpy(d["rgb"][i]).cuda()
@@ -161,7 +169,10 @@ def test_adam20_golden(tag, name, L, s):
     m = arena_to_dict(plan.exp_avg, w, L, s)
     v = arena_to_dict(plan.exp_avg_sq, w, L, s)
     for n in O.layer_names(L, s):
-        np.testing.assert_allclose(w20[n], d["w20:" + n], atol=5e-5, err_msg=n)
+        if name == "B":  # config B at its own lr 1e-4 (see make_golden.g4_adam20)
+            assert_adam_close(w20[n], d["w20:" + n], lr=lr, steps=20, name=n, atol=5e-6)
+        else:
+            np.testing.assert_allclose(w20[n], d["w20:" + n], atol=5e-5, err_msg=n)
         np.testing.assert_allclose(m[n], d["m:" + n], atol=1e-5, err_msg=n)
         np.testing.assert_allclose(v[n], d["v:" + n], rtol=1e-3, atol=1e-10, err_msg=n)
 
@@ -493,13 +504,15 @@ def test_dp_step_shape_bitwise_equals_fused_step():
         assert f[5] == d[5]
 
 
-@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("A", 4096), ("R", 2048)])
+@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("A", 4096), ("R", 2048), ("B", 65536)])
 def test_bf16_chain3_matches_bf16_oracle(name, B):
     """The fused bf16 step (csrc/chain3.hip + lgemm.hip) against an independent restatement
     of the bf16 mode's arithmetic (oracle.inf_oracle.mlp_forward_bf16 / mlp_backward_bf16:
     bf16 weights and activations, fp32 accumulation, the rounding points of the chain's
     epilogues) -- not against the builder's own layered bf16 kernels.  What is left is the
-    fp32 summation order, which can flip a bf16 rounding now and then."""
+    fp32 summation order, which can flip a bf16 rounding now and then.  65,536 rays is the
+    bench's large-batch line: chain3's 64-ray tiles (the feature tile streamed in 256-column
+    chunks, W_y x a separate fp32 sum) and the 256 x 256-tile dW GEMM (fgemm.hip)."""
     rng = np.random.default_rng(77)
     k, H, L, s = CFG[name]
     w0 = weights(golden(f"g2_forward_{name}.npz"))
@@ -514,7 +527,7 @@ def test_bf16_chain3_matches_bf16_oracle(name, B):
     plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
     pred = torch.empty((B, 3), device="cuda")
     plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
-    assert plan.last_step_path() in ("chain3", "chain3_chunked")
+    assert plan.last_step_path() == ("chain3_wide" if B > 8192 else "chain3"), plan.last_step_path()
     c = plan.read_ctrl()
     p = pred.cpu().numpy()
     g = arena_to_dict(plan.grads, w, L, s)
