@@ -235,12 +235,14 @@ int inf_backward(inf_plan* plan, const float* dpred, float* grads, inf_stream_t 
  * ctrl->loss_sum / sse_sum and added to the epoch sums. */
 /* INF_STEP_PART1 / PART2 (gradient-only steps; not with ADAM / ADVANCE): the step split at
  * inf_plan_grad_split for a bucketed data-parallel all-reduce.  PART1 runs the forward,
- * loss and backward chain, the weight-gradient GEMM of the matrices in bucket 1 (arena
- * [grad_split, P): the skip layer's Ly and every layer after it) and the reduction of
- * bucket 1 (with every bias and the step's loss sums) into `grads`; PART2 (same batch)
- * the GEMM and reduction of bucket 2 (arena [0, grad_split)).  The caller all-reduces
- * bucket 1 while PART2 runs.  Where the step does not take the fused chain, PART1
- * reduces the whole gradient and PART2 does nothing. */
+ * loss and backward chain, the weight-gradient GEMM of the matrices in bucket 1 and the
+ * reduction of bucket 1 into `grads`: the arena range [grad_split, P) -- the skip layer's
+ * Ly and every tensor after it, their biases included -- plus the step's loss sums.
+ * PART2 (same batch) does the GEMM and reduction of bucket 2, the arena [0, grad_split):
+ * every earlier tensor, the earlier layers' biases (Lx.bias among them) included.  The
+ * caller all-reduces bucket 1 while PART2 runs.  Where the step does not take the fused
+ * chain, PART1 reduces the whole gradient and PART2 does nothing
+ * (inf_plan_last_part1_bucketed tells which). */
 enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2, INF_STEP_XSLOT0 = 4, INF_STEP_XSLOT1 = 8, INF_STEP_PART1 = 16,
        INF_STEP_PART2 = 32 };
 int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int flags,
@@ -341,6 +343,12 @@ int64_t inf_plan_weight_generation(const inf_plan* plan);
 /* First float of gradient bucket 1 in the parameter arena (the skip layer's Ly weight;
  * INF_STEP_PART1 / PART2): bucket 1 = [split, P), bucket 2 = [0, split). */
 int64_t inf_plan_grad_split(const inf_plan* plan);
+
+/* Whether the last INF_STEP_PART1 step really split the gradient: 1 = bucketed (PART2 still
+ * to run), 0 = it reduced the whole gradient (not the fused chain3 path, INF_FUSED_UPDATE, or
+ * a batch not a multiple of 256 x the bucket splits: PART2 is then a no-op), -1 = no PART1
+ * step yet. */
+int inf_plan_last_part1_bucketed(const inf_plan* plan);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

@@ -71,6 +71,7 @@ struct inf_plan {
   int bucket_splits = 1;
   int64_t grad_split = 0;  // bucket 1 = arena [grad_split, P) (Ly and the layers after it)
   int n_items_b1 = 0;      // update work items of bucket 1 (listed first), end-of-step item included
+  int last_part1 = -1;     // the last PART1 step: 1 bucketed, 0 reduced the whole gradient
   int train_unit = 128;
   int bp_max = 0;
   int grid_hb = 1;
@@ -1555,11 +1556,13 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   int Bp3 = 0;
   if ((rc = pad_batch(p, batch->batch, true, &Bp3))) return rc;
   // bucketed halves of a gradient-only step (fused chain3 path): PART1 = the fused chain,
-  // the dW GEMM of bucket 1's matrices and the reduction of bucket 1 (arena [grad_split, P),
-  // biases and the step's loss sums included) into `grads`; PART2 = the same for bucket 2
-  // (arena [0, grad_split)).  The caller all-reduces bucket 1 while PART2 runs.
+  // the dW GEMM of bucket 1's matrices and the reduction of bucket 1 -- the arena range
+  // [grad_split, P): the matrices and biases from the skip layer's Ly on, plus the step's
+  // loss sums -- into `grads`; PART2 = the same for bucket 2, the arena [0, grad_split)
+  // (the earlier layers' biases included).  The caller all-reduces bucket 1 while PART2 runs.
   const bool bucketed = part != 0 && use_chain3(p, batch, Bp3) && Bp3 % (256 * p->bucket_splits) == 0 &&
                         std::getenv("INF_FUSED_UPDATE") == nullptr;
+  if (part == 1) p->last_part1 = bucketed ? 1 : 0;
   if (part == 2 && !bucketed) return INF_OK;  // PART1 reduced the whole gradient
   if (part == 2) {
     INF_CHECK_ARG(p->stepped && p->last_chain == 3 && p->saved_bp == Bp3, "train_step: PART2 without its PART1");
@@ -1919,6 +1922,8 @@ int inf_prefetch_batch(inf_plan* p, const inf_batch* b, int slot, inf_stream_t s
 }
 
 int64_t inf_plan_grad_split(const inf_plan* p) { return p == nullptr ? -1 : p->grad_split; }
+
+int inf_plan_last_part1_bucketed(const inf_plan* p) { return p == nullptr ? -1 : p->last_part1; }
 
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;

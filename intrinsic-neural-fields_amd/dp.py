@@ -206,14 +206,37 @@ class DataParallelEpoch:
             for _ in range(count):
                 self._step(rt, plan, batch)
 
-    def _candidate_shapes(self):
+    def _candidate_shapes(self, full=None):
         want = os.environ.get("INF_DP_SHAPE", "auto")
         if want != "auto":
             if want not in self.SHAPES:
                 raise ValueError(f"INF_DP_SHAPE must be one of {self.SHAPES} or auto")
             return [want]
-        # one GPU: nothing to hide behind, the plain step is the fastest (bench.py INF_BENCH_DP)
-        return list(self.SHAPES) if self.world > 1 else ["serial"]
+        # one GPU: nothing to hide behind, the plain step is the fastest (bench.py INF_BENCH_DP).
+        # Fewer full batches than one multi-step graph: _time_graphs could only time the
+        # one-step graphs, which every shape captures as the serial step -- no autotune.
+        if self.world == 1 or (full is not None and full < self.GRAPH_STEPS):
+            return ["serial"]
+        return list(self.SHAPES)
+
+    def _common_shapes(self, candidates, captured, device):
+        """The candidate shapes EVERY rank captured, in candidate order (one MIN all-reduce
+        of an availability mask).  A rank may fail to capture a shape the others did -- the
+        prefetch pipeline needs pre-gather slots, which a plan grown past CHAIN3_MAX_ROWS
+        (rank 0 alone renders the validation views) does not allocate -- and the timing
+        replays hold captured all-reduces, so every rank must time the same shapes."""
+        avail = torch.tensor([1 if n in captured else 0 for n in candidates], dtype=torch.int32, device=device)
+        if self.world > 1:
+            dist.all_reduce(avail, op=dist.ReduceOp.MIN, group=self.group)
+        names = [n for n, a in zip(candidates, avail.tolist()) if a]
+        if not names:
+            raise RuntimeError(f"data-parallel step: no step shape every rank can capture ({candidates})")
+        return names
+
+    def _capture_stream(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        return s
 
     def _capture_shape(self, shape, plan, rt, batch, s):
         from inf_hip import runtime
@@ -227,6 +250,8 @@ class DataParallelEpoch:
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
                 self._steps("bucketed" if shape == "bucketed" else "serial", 1, rt, plan, batch)
+            if shape == "bucketed" and plan.last_part1_bucketed() != 1:
+                return None  # PART1 reduced the whole gradient: no overlap, not a real shape
             with torch.cuda.graph(gm, stream=s):
                 self._steps(shape, self.GRAPH_STEPS, rt, plan, batch)
         torch.cuda.current_stream().wait_stream(s)
@@ -262,14 +287,14 @@ class DataParallelEpoch:
         plan.set_batch_index(0)
         plan.train_step(batch, None, apply_adam=False)  # settles the plan's tables before capture
         self._tail_all_reduce(rt, plan)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
+        s = self._capture_stream()
         graphs = {}
-        for shape in self._candidate_shapes():
+        candidates = self._candidate_shapes(full)
+        for shape in candidates:
             g = self._capture_shape(shape, plan, rt, batch, s)
             if g is not None:
                 graphs[shape] = g
-        names = list(graphs)
+        names = self._common_shapes(candidates, graphs, rt.device)
         chosen = names[0]
         if len(names) > 1:
             ms = torch.tensor([self._time_graphs(graphs[n], plan, full) for n in names], dtype=torch.float64,

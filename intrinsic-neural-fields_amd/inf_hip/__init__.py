@@ -103,6 +103,7 @@ _SIGNATURES = {
     "inf_ctrl_advance": (c_int, [c_void_p, c_void_p]),
     "inf_plan_last_step_path": (c_int, [c_void_p]),
     "inf_plan_grad_split": (c_int64, [c_void_p]),
+    "inf_plan_last_part1_bucketed": (c_int, [c_void_p]),
     "inf_plan_weight_generation": (c_int64, [c_void_p]),
     "inf_prefetch_batch": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
@@ -147,31 +148,42 @@ BUILD_ID = None       # inf_build_id() of the loaded library
 BUILD_VERIFIED = None  # True: recomputed from the sources beside it; None: sources absent
 
 
-def source_hash(files, base=CSRC) -> str:
+def source_hash(files, base=CSRC, flags=None) -> str:
     import hashlib
     h = hashlib.sha256()
     for f in files:
         with open(os.path.join(base, f), "rb") as fh:
             h.update(fh.read())
+    if flags is not None:
+        h.update(flags.encode())
     return h.hexdigest()[:16]
 
 
+def parse_build_id(build_id: str):
+    """inf_build_id() = "<hash> <files...> -- <compile flags>" -> (hash, files, flags)."""
+    head, _, flags = build_id.partition(" -- ")
+    want, *files = head.split()
+    return want, files, flags.strip()
+
+
 def _check_provenance(lib):
-    """The library must have been linked from the sources next to it (csrc/Makefile writes
-    the hash of their bytes into inf_build_id): a stale or foreign libinf_hip.so raises
-    here instead of running other kernels than the tree's.  INF_ALLOW_STALE_LIB=1 skips
-    the refusal (tuning experiments on variant builds)."""
+    """The library must have been linked from the sources next to it, with the plain
+    compile flags (csrc/Makefile hashes the source bytes and the flags into inf_build_id): a
+    stale or foreign libinf_hip.so, or a variant build (-D... diagnostics such as
+    C3_STREAM_ONLY, which compute garbage), raises here instead of running other kernels
+    than the tree's.  INF_ALLOW_STALE_LIB=1 skips the refusal (tuning experiments)."""
     global BUILD_ID, BUILD_VERIFIED
     BUILD_ID = lib.inf_build_id().decode()
-    want, *files = BUILD_ID.split()
+    want, files, flags = parse_build_id(BUILD_ID)
     if not files or not all(os.path.exists(os.path.join(CSRC, f)) for f in files):
         BUILD_VERIFIED = None
         return
-    got = source_hash(files)
-    BUILD_VERIFIED = got == want
+    got = source_hash(files, flags=flags)
+    variant = any(t.startswith("-D") for t in flags.split())
+    BUILD_VERIFIED = got == want and not variant
     if not BUILD_VERIFIED and os.environ.get("INF_ALLOW_STALE_LIB", "0") == "0":
-        raise ImportError(f"{LIB_PATH} was built from other sources (build id {want}, sources hash {got}): "
-                          "rebuild it (make -C intrinsic-neural-fields_amd/csrc)")
+        why = f"with variant flags ({flags})" if got == want else f"from other sources (build id {want}, sources hash {got})"
+        raise ImportError(f"{LIB_PATH} was built {why}: rebuild it (make -C intrinsic-neural-fields_amd/csrc)")
 
 
 lib = _load()

@@ -468,6 +468,11 @@ class Plan:
         """inf_plan_grad_split: gradient bucket 1 = arena [split, P), bucket 2 = [0, split)."""
         return int(lib.inf_plan_grad_split(self.handle))
 
+    def last_part1_bucketed(self) -> int:
+        """inf_plan_last_part1_bucketed: 1 if the last part=1 step split the gradient, 0 if it
+        reduced all of it (part=2 then does nothing), -1 before any."""
+        return int(lib.inf_plan_last_part1_bucketed(self.handle))
+
     def ctrl_advance(self):
         check(lib.inf_ctrl_advance(self.handle, stream_handle()), "ctrl_advance")
 

@@ -195,3 +195,73 @@ def test_recapture_is_collective_when_one_rank_changes_plan():
     assert counts[0] == counts[1], counts
     assert counts[0][0] == 2, counts
     assert caught
+
+
+def _shape_worker(rank, world, port, out_q):
+    """The real DataParallelEpoch._capture shape selection with the HIP parts faked: rank 0
+    cannot capture the prefetch shape (its plan grew past CHAIN3_MAX_ROWS: no pre-gather
+    slots), and each rank's timings favour a different shape."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "..", "intrinsic-neural-fields_amd"))
+    import dp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.pop("INF_DP_SHAPE", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    timed = []
+
+    class Epoch(dp.DataParallelEpoch):
+        def _capture_stream(self):
+            return None
+
+        def _capture_shape(self, shape, plan, rt, batch, s):
+            if shape == "prefetch" and rank == 0:
+                return None
+            return (shape, shape, None)
+
+        def _time_graphs(self, g, plan, full):
+            timed.append(g[0])
+            # rank 1 finds prefetch fastest, rank 0 bucketed; the MAX over ranks decides
+            return {"serial": 3.0, "prefetch": 1.0 if rank == 1 else 9.0, "bucketed": 2.0 + rank}[g[0]]
+
+    log = []
+    plan, rt = _Plan(log), _Rt()
+    res = {}
+    for full in (16, 4):
+        ep = Epoch()
+        timed.clear()
+        ep._capture(plan, rt, None, full=full)
+        res[full] = (ep.shape, list(timed), ep.shape_times)
+    out = [None] * world
+    dist.all_gather_object(out, res)
+    if rank == 0:
+        out_q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_capture_shape_choice_is_collective():
+    """every rank must time the same step shapes -- the timing replays
+    hold captured all-reduces -- and pick the same one.  With fewer full batches than one
+    multi-step graph there is nothing to time: serial, without autotune (ADVICE medium)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_shape_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0, r1 = out
+    for full in (16, 4):
+        assert r0[full][0] == r1[full][0], (full, r0[full], r1[full])
+    # 16 full batches: prefetch dropped on both ranks (rank 0 could not capture it); times
+    # serial 3 / bucketed max(2, 3) = 3 -> the first of the tie, serial
+    assert r0[16][1] == r1[16][1] == ["serial", "bucketed"], (r0[16], r1[16])
+    assert r0[16][0] == "serial"
+    assert set(r0[16][2]) == set(r1[16][2]) == {"serial", "bucketed"}
+    # 4 full batches (< GRAPH_STEPS = 8): serial, nothing timed
+    assert r0[4][0] == "serial" and r0[4][1] == [] and r1[4][1] == []

@@ -3,7 +3,7 @@
 set -o pipefail
 for rep in 1 2; do
 for l in "" "$@"; do
-  if [ -n "$l" ]; then export INF_LIB=$PWD/intrinsic-neural-fields_amd/inf_hip/libinf_hip_$l.so; else unset INF_LIB; fi
+  if [ -n "$l" ]; then export INF_LIB=$PWD/intrinsic-neural-fields_amd/inf_hip/libinf_hip_$l.so INF_ALLOW_STALE_LIB=1; else unset INF_LIB INF_ALLOW_STALE_LIB; fi
   echo "== lib ${l:-default}"
   timeout -k 10 200 python bench.py --steps 30 --warmup 5 --only configD 2>/dev/null | python3 -c "
 import json,sys

@@ -4,7 +4,7 @@
 #   bash tools/gpu_variants.sh X Y ...      (the default library first)
 set -o pipefail
 for l in "" "$@"; do
-  if [ -n "$l" ]; then export INF_LIB=$PWD/intrinsic-neural-fields_amd/inf_hip/libinf_hip_$l.so; else unset INF_LIB; fi
+  if [ -n "$l" ]; then export INF_LIB=$PWD/intrinsic-neural-fields_amd/inf_hip/libinf_hip_$l.so INF_ALLOW_STALE_LIB=1; else unset INF_LIB INF_ALLOW_STALE_LIB; fi
   echo "== lib ${l:-default}"
   PROJ=1 timeout -k 10 100 python tools/rchain_timing.py 2>&1 | grep -v amdgpu.ids | sed -n '2p;4p' || exit 1
 done
