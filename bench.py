@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra-batches", default="65536", help="comma list of extra per-GPU batch sizes to report")
     ap.add_argument("--no-config-d", action="store_true")
+    ap.add_argument("--strong-batch", type=int, default=4096,
+                    help="global batch of the strong-scaling leg (the YAML batch_size, split over the GPUs)")
+    ap.add_argument("--strong-local", default="512,1024,2048",
+                    help="N=1: per-GPU batches of the strong-scaling points (4096 / 8, / 4, / 2) to time")
     ap.add_argument("--only", default="", help="debug: run only these comma-separated secondary sections "
                                                 "(configD, render, rff, psnr, cpu) after the headline")
     return ap.parse_args()
@@ -98,10 +102,13 @@ class Trainer:
     the dW GEMM and gradient reduction in two halves (inf_train_step PART1 / PART2), bucket 1
     all-reduced on a side stream while the second half runs (dp.DataParallelEpoch)."""
 
-    def __init__(self, args, device, B, rank, world, nb=32, shape="serial"):
+    def __init__(self, args, device, B, rank, world, nb=32, shape="serial", global_batch=None, dp=None):
         from inf_hip import runtime
         self.args, self.B, self.world = args, B, world
         self.shape = shape
+        # the loss is normalised by the GLOBAL batch: world x B (weak scaling), or the
+        # reference's batch split over the ranks (strong scaling, nn.DataParallel semantics)
+        self.global_batch = global_batch if global_batch is not None else B * world
         self.model = build_model(args, device)
         rt = self.model.hip_runtime()
         rt.ensure_optimizer_arenas()
@@ -115,12 +122,12 @@ class Trainer:
         self.src = runtime.RaySource(E, vids, bary, rgb)
         self.perm = torch.randperm(self.N, device=device)
         self.batch = self.plan.make_batch(source=self.src, ray_idx=self.perm, offset=0, batch=B,
-                                          offset_from_ctrl=True, loss_count=3 * B * world, loss=args.loss)
+                                          offset_from_ctrl=True, loss_count=3 * self.global_batch, loss=args.loss)
         self.graphs = None
         self.i = 0
         # the data-parallel step shape (flat-gradient all-reduce between the update and Adam);
         # INF_BENCH_DP=1 runs it at world 1 too (rehearses RCCL capture on a one-GPU box)
-        self.dp = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
+        self.dp = (world > 1 or bool(os.environ.get("INF_BENCH_DP"))) if dp is None else dp
         self.ar_in_graph = False
         # shape "prefetch" (or INF_PREFETCH=1 on the single-GPU step): the next batch's gather
         # on a side stream beside the gradient all-reduce (runtime.StepPipeline lead 0)
@@ -128,6 +135,10 @@ class Trainer:
         self.side = torch.cuda.Stream(device=device)
         want = shape == "prefetch" if self.dp else os.environ.get("INF_PREFETCH", "0") != "0"
         self.prefetch = want and self.pipe.start()
+        if self.dp and shape == "sharded":
+            if not self.plan.can_shard(self.batch):
+                raise RuntimeError("sharded step shape: this batch's step has no fused chain")
+            self.plan.shard(world, rank)  # item-major staging (dp.py shape "sharded")
 
     # steps per replayed graph (divides nb)
     GRAPH_STEPS = int(os.environ.get("INF_GRAPH_STEPS", "8"))
@@ -137,7 +148,7 @@ class Trainer:
             # Adam + the batch-index advance ride in the step's update launch
             self.plan.train_step(self.batch, None, apply_adam=True, advance=True, xslot=xslot)
         else:
-            self.plan.train_step(self.batch, None, apply_adam=False, xslot=xslot)
+            self.plan.train_step(self.batch, None, apply_adam=False, xslot=xslot, shard=self.shape == "sharded")
 
     def _bucketed_step(self):
         plan, dist = self.plan, torch.distributed
@@ -170,10 +181,26 @@ class Trainer:
                     tail()
 
     def _dp_tail(self):
-        """all-reduce of the flat gradient bucket, then the replicated Adam + batch advance"""
+        """all-reduce of the flat gradient bucket, then the replicated Adam + batch advance;
+        sharded: reduce-scatter, Adam on this rank's items + advance, all-gather of the new
+        weights, image rewrite (dp.DataParallelEpoch._step_sharded)"""
+        if self.shape == "sharded":
+            import dp
+            plan = self.plan
+            dp.reduce_scatter_grads(plan.grad_chunk, plan.grad_staging)
+            plan.adam_shard(advance=True)
+            dp.all_gather_chunks(plan.weight_staging, plan.weight_chunk())
+            plan.shard_scatter()
+            return
         if torch.distributed.is_initialized():
             torch.distributed.all_reduce(self.plan.grads)
         self.plan.adam(0, 0.0, advance=True)
+
+    def gather_state(self):
+        """Sharded shape: masters and Adam state whole again (before stage timings read them)."""
+        if self.dp and self.shape == "sharded":
+            import dp
+            dp.gather_sharded_state(self.plan)
 
     def _capture_dp_steps(self, s):
         """GRAPH_STEPS whole data-parallel steps (RCCL all-reduce included) in one graph: no
@@ -238,7 +265,7 @@ class Trainer:
         self.i += 1
 
     def step(self):
-        if self.graphs is None or self.prefetch or (self.dp and self.shape == "bucketed"):
+        if self.graphs is None or self.prefetch or (self.dp and self.shape in ("bucketed", "sharded")):
             return self.step_eager()
         self._wrap()
         g1, g2, _ = self.graphs
@@ -282,6 +309,33 @@ def time_steps(tr, steps, warmup, world):
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t[0]) / steps, float(t[1]) / steps
+
+
+def strong_local_steps(args, device):
+    """N=1: the per-GPU step of each strong-scaling point -- the reference's 4096-ray batch
+    split over 8 / 4 / 2 GPUs is 512 / 1024 / 2048 rays per GPU -- in the data-parallel step
+    shapes at world 1 (serial: gradient -> [all-reduce] -> Adam; sharded: gradient ->
+    [reduce-scatter] -> Adam -> [all-gather] -> image rewrite), collectives absent.  The
+    strong-scaling projection adds a collective model to these; the
+    N > 1 runs measure the real thing (data_parallel.strong)."""
+    out = {}
+    for bl in [int(x) for x in args.strong_local.split(",") if x]:
+        row = {}
+        for shape in ("serial", "sharded"):
+            try:
+                tr = Trainer(args, device, bl, 0, 1, shape=shape, global_batch=args.strong_batch, dp=True)
+            except RuntimeError as exc:  # no fused chain at this batch: the shape does not apply
+                row[shape] = repr(exc)
+                continue
+            tr.capture()
+            ms, _ = time_steps(tr, max(20, args.steps // 4), 5, 1)
+            tr.gather_state()
+            row[shape] = ms
+            del tr
+            torch.cuda.empty_cache()
+        out[str(bl)] = {"gpus": args.strong_batch // bl, "ms_per_step": row,
+                        "chain3_workgroups": bl // 16}
+    return out
 
 
 def time_allreduce(tr, steps, warmup, world):
@@ -870,10 +924,11 @@ def main():
         # and the gradient all-reduce alone; `value` is the fastest shape's
         dp_shapes = {}
         best = None
-        for shape in [x for x in os.environ.get("INF_DP_SHAPES", "serial,prefetch,bucketed").split(",") if x]:
+        for shape in [x for x in os.environ.get("INF_DP_SHAPES", "serial,prefetch,bucketed,sharded").split(",") if x]:
             tr = Trainer(args, device, args.batch, rank, world, shape=shape)
             tr.capture()
             ms_s, wall_s = time_steps(tr, args.steps, args.warmup, world)
+            tr.gather_state()
             dp_shapes[shape] = {"ms_per_step": ms_s, "value": world * args.batch / (ms_s * 1e-3),
                                 "allreduce_in_graph": tr.ar_in_graph, "prefetch_active": bool(tr.prefetch)}
             if best is None or ms_s < best[1]:
@@ -890,8 +945,29 @@ def main():
         dp_shapes["chosen"] = chosen
         dp_shapes["note"] = ("serial: fused step -> flat-gradient all-reduce -> Adam in order; prefetch: the next "
                              "batch's gather on a side stream beside the all-reduce; bucketed: the dW GEMM in two "
-                             "halves, bucket 1 all-reduced beside the second; value = the fastest shape (dp.py's "
-                             "autotune picks the same way)")
+                             "halves, bucket 1 all-reduced beside the second; sharded: reduce-scatter of the "
+                             "gradient -> Adam on 1/N of the parameters -> all-gather of the new bf16 weights; "
+                             "value = the fastest shape (dp.py's autotune picks the same way)")
+        if world > 1:
+            # strong scaling (nn.DataParallel semantics, reference train.py:46-48): the YAML's
+            # global batch of 4096 split over the ranks, in the chosen shape (serial if it cannot)
+            gb = args.strong_batch
+            bl = -(-gb // world)
+            st_shape = chosen if chosen != "prefetch" else "serial"
+            try:
+                trs = Trainer(args, device, bl, rank, world, shape=st_shape, global_batch=gb)
+            except RuntimeError:
+                st_shape = "serial"
+                trs = Trainer(args, device, bl, rank, world, shape=st_shape, global_batch=gb)
+            trs.capture()
+            ms_st, _ = time_steps(trs, args.steps, args.warmup, world)
+            trs.gather_state()
+            dp_shapes["strong"] = {"global_batch": gb, "rays_per_gpu": bl, "shape": st_shape, "ms_per_step": ms_st,
+                                   "value": gb / (ms_st * 1e-3), "unit": "rays/s",
+                                   "note": "the reference's batch of 4096 split over the GPUs (DataParallel "
+                                           "semantics); `value` above is weak scaling (4096 rays per GPU)"}
+            del trs
+            torch.cuda.empty_cache()
     else:
         tr = Trainer(args, device, args.batch, rank, world)
         tr.capture()
@@ -967,6 +1043,10 @@ def main():
             psnr = [psnr_vs_ref(m, f) for f in PSNR_RUNS for m in ("bf16", "fp32")]
         except Exception as exc:  # reported, never fatal to the throughput line
             psnr = {"error": repr(exc)}
+
+    strong_local = None
+    if rank == 0 and world == 1 and want("strong") and args.mode == "bf16":
+        strong_local = strong_local_steps(args, device)
 
     secondary = {}
     if rank == 0 and world == 1 and want("configs"):
@@ -1050,6 +1130,7 @@ def main():
             "stages": stage_lines,
             "host_wall_ms_per_step": wall_ms,
             "data_parallel": dp_shapes,
+            "strong_scaling_local_steps": strong_local,
             "large_batch": extra,
             "config_D": config_d,
             "secondary": secondary,

@@ -243,8 +243,13 @@ int inf_backward(inf_plan* plan, const float* dpred, float* grads, inf_stream_t 
  * caller all-reduces bucket 1 while PART2 runs.  Where the step does not take the fused
  * chain, PART1 reduces the whole gradient and PART2 does nothing
  * (inf_plan_last_part1_bucketed tells which). */
+/* INF_STEP_SHARD (gradient-only, after inf_plan_shard + inf_plan_bind_shard): the reduced
+ * local gradient goes to the item-major gradient staging (the reduce-scatter input) instead
+ * of `grads`; see inf_adam_shard.  Only where the step takes a fused chain (chain3 / chainf,
+ * which read nothing but the weight images and the fp32 vectors): INF_ERR_UNSUPPORTED, with
+ * nothing launched, otherwise. */
 enum { INF_STEP_ADAM = 1, INF_STEP_ADVANCE = 2, INF_STEP_XSLOT0 = 4, INF_STEP_XSLOT1 = 8, INF_STEP_PART1 = 16,
-       INF_STEP_PART2 = 32 };
+       INF_STEP_PART2 = 32, INF_STEP_SHARD = 64 };
 int inf_train_step(inf_plan* plan, const inf_batch* batch, float* pred, int flags,
                    inf_stream_t stream);
 
@@ -330,7 +335,8 @@ int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
  * LDS-ring chain (csrc/chain.hip), 3 the fused gather + register-streamed chain
  * (csrc/chain3.hip), 4 the same with the feature tile streamed in chunks (k_pad > 1024),
  * 5 the same in 64-ray tiles (batches above 8192 rays), 6 the fused fp32 chain of the
- * fp32 mode (csrc/chainf.hip); -1 before any step. */
+ * fp32 mode (csrc/chainf.hip), 7 the split-bf16 register chain of the bf16x3 mode
+ * (csrc/chain3.hip X3); -1 before any step. */
 int inf_plan_last_step_path(const inf_plan* plan);
 
 /* Weight generation: a counter of the launches issued through this plan that may have
@@ -349,6 +355,40 @@ int64_t inf_plan_grad_split(const inf_plan* plan);
  * a batch not a multiple of 256 x the bucket splits: PART2 is then a no-op), -1 = no PART1
  * step yet. */
 int inf_plan_last_part1_bucketed(const inf_plan* plan);
+
+/* ---- Sharded optimizer step (data parallel; replaces nn.DataParallel's reduce to GPU 0 +
+ * GPU-0 Adam + re-broadcast, reference train.py:46-48, config.py:108, trainer.py:80-82) ----
+ * One step on `world` ranks:
+ *   inf_train_step(..., INF_STEP_SHARD)  the local gradient, item-major, into grad_staging
+ *   reduce-scatter(sum) grad_staging [world][grad_floats] -> grad_chunk [grad_floats]
+ *   inf_adam_shard                       Adam on this rank's items only, their new weights
+ *                                        (GEMM dtype; fp32 vectors) into its chunk of
+ *                                        weight_staging [world][weight_bytes]
+ *   all-gather weight_staging (this rank's chunk in place)
+ *   inf_shard_scatter                    every rank rewrites all weight images and the fp32
+ *                                        vector parameters from weight_staging
+ * Each parameter is updated by exactly one rank, so replicas stay bitwise equal.  The fp32
+ * masters and the Adam state are then current on this rank's items only: before anything
+ * reads them whole (checkpoints, evaluation, inf_adam, row-major shadows -- refused until
+ * then), gather each arena: inf_shard_pack(arena -> grad_chunk), all-gather grad_chunk into
+ * grad_staging, inf_shard_unpack(grad_staging -> arena). */
+
+/* The item-major staging layout for `world` ranks (re-writes the update work list; not on
+ * the hot path).  Returns the per-rank chunk sizes: grad_floats (fp32 elements) and
+ * weight_bytes. */
+int inf_plan_shard(inf_plan* plan, int world, int rank, int64_t* grad_floats, int64_t* weight_bytes);
+/* 1 when this batch's training step can run sharded (a fused chain, see INF_STEP_SHARD), else 0. */
+int inf_plan_can_shard(inf_plan* plan, const inf_batch* batch);
+/* Caller-owned staging: grad_staging [world * grad_floats] f32, grad_chunk [grad_floats] f32,
+ * weight_staging [world * weight_bytes] bytes (zeroed here). */
+int inf_plan_bind_shard(inf_plan* plan, float* grad_staging, float* grad_chunk, void* weight_staging);
+/* Adam (torch formula, ctrl's step and lr) on this rank's items from grad_chunk;
+ * flags: INF_STEP_ADVANCE. */
+int inf_adam_shard(inf_plan* plan, int flags, inf_stream_t stream);
+int inf_shard_scatter(inf_plan* plan, inf_stream_t stream);
+/* arena (P floats) -> grad_chunk (this rank's items) / grad_staging (all items) -> arena. */
+int inf_shard_pack(inf_plan* plan, const float* arena, float* grad_chunk, inf_stream_t stream);
+int inf_shard_unpack(inf_plan* plan, const float* grad_staging, float* arena, inf_stream_t stream);
 
 /* Advance ctrl->batch_index by one (captured at the end of a graph-replayed step). */
 int inf_ctrl_advance(inf_plan* plan, inf_stream_t stream);

@@ -27,7 +27,46 @@ __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   adam_dev::update_item<T>(a, a.items[blockIdx.x], tile, sc);
 }
 
+// one item per workgroup: a 64 x 32 matrix tile (row-major [64][32] in the staging, zero
+// beyond the tensor) or a 64-element vector chunk
+__global__ __launch_bounds__(256) void shard_copy_kernel(const AdamSeg* segs, const AdamItem* items, const float* src,
+                                                         float* dst, int64_t base, int unpack) {
+  const AdamItem it = items[blockIdx.x];
+  if (it.seg < 0) return;
+  const AdamSeg seg = segs[it.seg];
+  const int64_t s0 = it.goff - base;
+  if (seg.matrix) {
+    for (int q = threadIdx.x; q < ADAM_TILE_R * ADAM_TILE_C; q += 256) {
+      const int gr = it.r0 + q / ADAM_TILE_C, gc = it.c0 + q % ADAM_TILE_C;
+      const bool ok = gr < seg.R && gc < seg.C;
+      const int64_t e = seg.off + (int64_t)gr * seg.C + gc;
+      if (unpack) {
+        if (ok) dst[e] = src[s0 + q];
+      } else {
+        dst[s0 + q] = ok ? src[e] : 0.f;
+      }
+    }
+  } else if (threadIdx.x < ADAM_VEC) {
+    const int gi = it.c0 + threadIdx.x;
+    const bool ok = gi < seg.C;
+    if (unpack) {
+      if (ok) dst[seg.off + gi] = src[s0 + threadIdx.x];
+    } else {
+      dst[s0 + threadIdx.x] = ok ? src[seg.off + gi] : 0.f;
+    }
+  }
+}
+
 }  // namespace
+
+int launch_shard_copy(const AdamSeg* segs, const AdamItem* items, int num_items, const float* src, float* dst,
+                      int64_t base, int unpack, hipStream_t stream) {
+  INF_CHECK_ARG(num_items > 0 && items != nullptr && segs != nullptr && src != nullptr && dst != nullptr,
+                "shard_copy: empty work list");
+  shard_copy_kernel<<<num_items, 256, 0, stream>>>(segs, items, src, dst, base, unpack);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
 
 int launch_update(const AdamArgs& a, int mode, hipStream_t stream) {
   INF_CHECK_ARG(a.num_items > 0 && a.items != nullptr && a.segs != nullptr, "update: empty work list");

@@ -29,7 +29,9 @@ struct AdamSeg {
   // layers, fed the gathered features), 1 = accumulator order (k = 16 (e / 4) + 4 g + e % 4:
   // fed activations straight from 16x16x32 accumulators, chain3.hip).  WTF: always 1.
   int32_t wf_acc_order;
-  int32_t pad_;
+  // fp32 updates (bf16x3 mode): WF / WTF hold hi / lo bf16 image pairs (lo right after hi:
+  // + R ldw elements for WF, + R C for WTF) instead of fp32 images -- chain3.hip X3
+  int32_t x3;
 };
 
 // Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = ADAM_VEC elements.
@@ -41,7 +43,21 @@ constexpr int ITEM_VEC4 = 1;  // AdamItem.pad flag: 16-byte aligned rows in the 
 struct AdamItem {
   int32_t seg;
   int32_t r0, c0;
-  int32_t pad;  // flags
+  int32_t pad;   // flags
+  // sharded update (inf_plan_shard): the item's slots in the item-major staging buffers --
+  // its gradient at float goff of the gradient staging (a matrix tile as [64][32], a vector
+  // chunk as [64]), its new weights at byte woff of the weight staging (the GEMM dtype for
+  // matrix tiles, fp32 for vector chunks)
+  int32_t goff;
+  int32_t woff;
+};
+
+// AdamArgs.shard_mode
+enum ShardMode {
+  SHARD_NONE = 0,
+  SHARD_GRAD_OUT = 1,  // write_grads into the gradient staging (gsh) instead of the arena
+  SHARD_ADAM = 2,      // gradient from the staging (this rank's chunk), new weights also to wsh
+  SHARD_SCATTER = 3,   // no gradient: weight images (matrix) / fp32 parameters (vector) from wsh
 };
 
 struct AdamArgs {
@@ -66,8 +82,21 @@ struct AdamArgs {
   int32_t advance;
   double beta1_d, beta2_d;
   float one_minus_b1, beta2, one_minus_b2, eps;
+  // sharded update (ShardMode): item it's gradient slot is gsh[it.goff - g_base], its weight
+  // slot wsh + (it.woff - w_base) bytes (the bases: this rank's chunk of a reduce-scatter)
+  int32_t shard_mode;
+  float* gsh;
+  int64_t g_base;
+  char* wsh;
+  int64_t w_base;
 };
 
 int launch_update(const AdamArgs& a, int mode, hipStream_t stream);
+
+// The sharded state's gather (inf_shard_pack / unpack): unpack = 0 copies `items` of the
+// arena `src` into the item-major staging `dst` (item it at dst[it.goff - base]), 1 copies
+// the staging `src` back into the arena `dst`.
+int launch_shard_copy(const AdamSeg* segs, const AdamItem* items, int num_items, const float* src, float* dst,
+                      int64_t base, int unpack, hipStream_t stream);
 
 }  // namespace inf

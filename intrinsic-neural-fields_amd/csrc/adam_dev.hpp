@@ -32,11 +32,23 @@ struct Scalars {
   float bc2_sqrt;  // sqrt(1 - b2^t)
 };
 
+// torch's single-tensor Adam op by op (torch/optim/adam.py, CPU kernels), with the
+// roundings pinned so no code path's FMA contraction can move a bit (the compiler contracted
+// differently in different inlined copies, which made two update paths disagree in the last
+// bit): measured against torch 2.10 CPU on 2^20 random elements (tools/adam_bits.py), m and v
+// match bitwise, p in 99.99 % of elements (torch's vectorised sqrt is not correctly rounded
+// in 0.6 % of them; ours is).
+//   exp_avg.lerp_(grad, 1 - b1)              m = fma(1 - b1, g - m, m)
+//   exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2) v = fma((1 - b2) g, g, v b2)
+//   denom = sqrt(v) / sqrt(bc2) + eps
+//   param.addcdiv_(exp_avg, denom, -step)    p = p + (-step m) / denom
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamArgs& a, const Scalars& s) {
-  m = m + a.one_minus_b1 * (g - m);
-  v = v * a.beta2 + (a.one_minus_b2 * g) * g;
+#pragma clang fp contract(off)
+  m = __builtin_fmaf(a.one_minus_b1, g - m, m);
+  const float vb = v * a.beta2;
+  v = __builtin_fmaf(a.one_minus_b2 * g, g, vb);
   const float denom = sqrtf(v) / s.bc2_sqrt + a.eps;
-  p = p + s.step_neg * (m / denom);
+  p = p + (s.step_neg * m) / denom;
 }
 
 // The part of a matrix item after its gradient is summed: Adam (or the gradient store),
@@ -64,7 +76,13 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
     }
   };
   if (a.grad_src != GRAD_NONE) {
-    if (a.write_grads) {
+    if (a.write_grads && a.shard_mode == SHARD_GRAD_OUT) {
+      // the item's tile in the gradient staging, [64][32] (out-of-range elements are 0)
+      float* gs = a.gsh + (item.goff - a.g_base) + cl;
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+        *reinterpret_cast<float4*>(gs + (rb + 32 * i) * ADAM_TILE_C) = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+    } else if (a.write_grads) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) st4(a.grads, i, g[i]);
     }
@@ -76,6 +94,20 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
         st4(a.params, i, w[i]);
         st4(a.exp_avg, i, m[i]);
         st4(a.exp_avg_sq, i, v[i]);
+      }
+      if (a.shard_mode == SHARD_ADAM) {
+        // the new weights in the GEMM dtype, [64][32], for the all-gather of the images
+        T* ws = reinterpret_cast<T*>(a.wsh + (item.woff - a.w_base)) + cl;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          T* d = ws + (rb + 32 * i) * ADAM_TILE_C;
+          if constexpr (sizeof(T) == 2) {
+            const bf16x4 pk = {(bf16)w[i][0], (bf16)w[i][1], (bf16)w[i][2], (bf16)w[i][3]};
+            *reinterpret_cast<bf16x4*>(d) = pk;
+          } else {
+            *reinterpret_cast<float4*>(d) = make_float4(w[i][0], w[i][1], w[i][2], w[i][3]);
+          }
+        }
       }
     }
   }
@@ -115,7 +147,24 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(seg.WF) + e) = pk;
       }
     } else {
-      if (seg.WF != nullptr && ok[i]) {
+      if (seg.WF != nullptr && ok[i] && seg.x3) {
+        // hi / lo bf16 fragment images (the bf16 layout above; lo = bf16(w - hi), R ldw
+        // elements after hi)
+        const int gr = item.r0 + r;
+        const int kk = gc & 31;
+        const int slot = seg.wf_acc_order ? (kk & 15) >> 2 : kk >> 3;
+        const int e0 = seg.wf_acc_order ? (kk >> 4) << 2 : kk & 7;
+        const int64_t e = ((int64_t)((gc >> 5) * (seg.R >> 4) + (gr >> 4)) * 64 + (gr & 15) + 16 * slot) * 8 + e0;
+        bf16x4 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hi[j] = (bf16)w[i][j];
+          lo[j] = (bf16)(w[i][j] - (float)hi[j]);
+        }
+        bf16* base = reinterpret_cast<bf16*>(seg.WF);
+        *reinterpret_cast<bf16x4*>(base + e) = hi;
+        *reinterpret_cast<bf16x4*>(base + (int64_t)seg.R * seg.ldw + e) = lo;
+      } else if (seg.WF != nullptr && ok[i]) {
         // fp32 fragment image (chainf.hpp): 2 KiB per (k block, 16-row tile), half
         // (gc / 4) % 2 of lane (gr % 16) + 16 ((gc % 32) / 8)
         const int gr = item.r0 + r;
@@ -139,6 +188,25 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
         for (int e = 0; e < 8; ++e) v[e] = (bf16)tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
         const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
         *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(seg.WTF) + off) = v;
+      }
+    }
+  } else if (seg.x3) {
+    if (seg.WTF != nullptr) {
+      // hi / lo bf16 backward images (the bf16 layout above; lo R C elements after hi)
+      const int cc = tid >> 3, kbl = (tid >> 2) & 1, g = tid & 3;
+      const int gcc = item.c0 + cc, gr = item.r0 + kbl * 32;
+      if (gcc < seg.C && gr + 31 < seg.R) {
+        bf16x8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = tile[cc][kbl * 32 + 16 * (e >> 2) + 4 * g + (e & 3)];
+          hi[e] = (bf16)x;
+          lo[e] = (bf16)(x - (float)hi[e]);
+        }
+        const int64_t off = ((int64_t)((gr >> 5) * (seg.C >> 4) + (gcc >> 4)) * 64 + (gcc & 15) + 16 * g) * 8;
+        bf16* base = reinterpret_cast<bf16*>(seg.WTF);
+        *reinterpret_cast<bf16x8*>(base + off) = hi;
+        *reinterpret_cast<bf16x8*>(base + (int64_t)seg.R * seg.C + off) = lo;
       }
     }
   } else {
@@ -204,7 +272,14 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
     const int gr = item.r0 + rb + 32 * i;
     ok[i] = gr < seg.R && gc < seg.C;
     e[i] = seg.off + (int64_t)(ok[i] ? gr : 0) * seg.C + (ok[i] ? gc : 0);
-    ld4(a.params, i, w[i]);
+    if (a.shard_mode == SHARD_SCATTER) {
+      // another rank's (or this rank's) new weights from the gathered staging: the images only
+      const T* ws = reinterpret_cast<const T*>(a.wsh + (item.woff - a.w_base)) + cl + (rb + 32 * i) * ADAM_TILE_C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[i][j] = (float)ws[j];
+    } else {
+      ld4(a.params, i, w[i]);
+    }
   }
   const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
   if (adam) {
@@ -214,7 +289,15 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
       ld4(a.exp_avg_sq, i, v[i]);
     }
   }
-  if (a.grad_src == GRAD_FLAT) {
+  if (a.grad_src == GRAD_FLAT && a.shard_mode == SHARD_ADAM) {
+    // this rank's chunk of the reduce-scattered gradient staging
+    const float* gs = a.gsh + (item.goff - a.g_base) + cl;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const float4 t = *reinterpret_cast<const float4*>(gs + (rb + 32 * i) * ADAM_TILE_C);
+      g[i][0] = t.x, g[i][1] = t.y, g[i][2] = t.z, g[i][3] = t.w;
+    }
+  } else if (a.grad_src == GRAD_FLAT) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) ld4(a.grads, i, g[i]);
   } else if (a.grad_src == GRAD_SLABS) {
@@ -443,16 +526,24 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
     if (w == 0 && ok) {
       g = ((vs[el] + vs[64 + el]) + vs[128 + el]) + vs[192 + el];
       const int64_t e = seg.off + gi;
-      if (a.grad_src == GRAD_FLAT) g = a.grads[e];
+      if (a.grad_src == GRAD_FLAT) g = a.shard_mode == SHARD_ADAM ? a.gsh[item.goff - a.g_base + el] : a.grads[e];
       if (a.grad_src != GRAD_NONE) {
-        if (a.write_grads) a.grads[e] = g;
+        if (a.write_grads) {
+          if (a.shard_mode == SHARD_GRAD_OUT)
+            a.gsh[item.goff - a.g_base + el] = g;
+          else
+            a.grads[e] = g;
+        }
         if (a.do_adam) {
           float pw = a.params[e], m = a.exp_avg[e], v = a.exp_avg_sq[e];
           adam_elem(pw, m, v, g, a, sc);
           a.params[e] = pw;
           a.exp_avg[e] = m;
           a.exp_avg_sq[e] = v;
+          if (a.shard_mode == SHARD_ADAM) reinterpret_cast<float*>(a.wsh + (item.woff - a.w_base))[el] = pw;
         }
+      } else if (a.shard_mode == SHARD_SCATTER) {
+        a.params[e] = reinterpret_cast<const float*>(a.wsh + (item.woff - a.w_base))[el];
       }
     }
   }

@@ -79,7 +79,7 @@ __device__ __forceinline__ unsigned nz1(unsigned x) {
   return r;
 }
 
-template <int H, int NR>
+template <int H, int NR, bool X3 = false>
 struct L3 {
   static constexpr int BM = C3BM * NR;          // rays per workgroup
   static constexpr int TN = H / (16 * C3_CW);  // 16-feature tiles per wave (2: H = 256, 1: H = 128)
@@ -93,8 +93,11 @@ struct L3 {
   // writes tile (p + 1) & 1, phase p reads tile p & 1, so one barrier per phase suffices
   // per-workgroup partials (sums over all BM rays) of the bias / output-layer gradients
   // and the loss
+  // X3 (split-bf16 mode): the lo halves of the two activation buffers follow the hi ones
+  // (buffer b: hi at b ACT_BYTES, lo at (2 + b) ACT_BYTES), the lo feature tile the hi one
   static constexpr int OFF_ACT = 0;
-  static constexpr int OFF_CS = OFF_ACT + 2 * ACT_BYTES;  // [2][H] bias-gradient partials (epilogue p: p & 1)
+  static constexpr int ACT_LO = 2 * ACT_BYTES;  // lo tile of a buffer, from its hi tile
+  static constexpr int OFF_CS = OFF_ACT + (X3 ? 4 : 2) * ACT_BYTES;  // [2][H] bias-gradient partials (epilogue p: p & 1)
   static constexpr int OFF_HW = OFF_CS + 2 * H * 4;       // [3][H] output-layer weight grad
   static constexpr int OFF_HB = OFF_HW + 3 * H * 4;       // [4]
   static constexpr int OFF_LS = OFF_HB + 16;              // [2] f64 loss / SSE
@@ -115,7 +118,7 @@ struct L3 {
   static constexpr int ACCY_BYTES = C3_CW * 64 * NR * TN * 16;
   __host__ __device__ static int off_x(int L) { return OFF_VEC + L * H * 4; }
   __host__ __device__ static int x_region(int kx, bool xc) {
-    return (NR > 1 && xc && ACCY_BYTES > BM * kx * 2) ? ACCY_BYTES : BM * kx * 2;
+    return (NR > 1 && xc && ACCY_BYTES > BM * kx * 2) ? ACCY_BYTES : (X3 ? 2 : 1) * BM * kx * 2;
   }
   __host__ __device__ static int off_stamp(int L, int kx, bool xc) { return off_x(L) + x_region(kx, xc); }
   static int lds_bytes(int L, int kx, bool xc) { return off_stamp(L, kx, xc) + (7 * C3_MAX_PHASES + 8) * 8; }
@@ -137,13 +140,16 @@ struct L3 {
 // the accumulator layout, X^T written by its gather): no gather here, phase 0 is the
 // layer-0 epilogue on Z, the skip layer adds W_y x from LDS (staged by the store wave with
 // direct-to-LDS loads) in its epilogue, and the weight stream holds the hidden layers only.
-template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP>
+// X3: the split-bf16 parity mode (Chain3Args::x3): hi / lo weight images, hi / lo
+// feature and activation tiles, three MFMAs per k block, fp32 gather / epilogues / head.
+template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP, bool X3>
 __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) {
-  using C = L3<H, NR>;
+  using C = L3<H, NR, X3>;
   constexpr int BM = C::BM, TN = C::TN, UPL = C::UPL;
   constexpr int NV = TN * 4;  // accumulator values per lane and ray tile
   static_assert(NR == 1 || !ENC, "wide tiles: eigenfunction tables only");
   static_assert(!ZP || (NR == 1 && !ENC && !XC), "precomputed input layers: narrow whole-tile schedule only");
+  static_assert(!X3 || (NR == 1 && !ENC && !XC && !ZP), "split-bf16 chain: narrow whole-tile schedule only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = a.L;
   const int k_pad = a.k_pad;
@@ -163,6 +169,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   char* xs = smem + C::off_x(L);  // gathered features [BM][kx] bf16 (tile_off layout)
   const int kx = XC ? C::KC : k_pad;  // columns resident in LDS
   const int xrow = kx * 2;
+  const int x_lo = BM * xrow;  // X3: the lo feature tile, from the hi one
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -192,11 +199,17 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     const int wc = wave;
     const int t0 = wc * TN;  // the wave's first 16-feature tile
     // fragment ring: D k-blocks (D * TN KiB per wave) in flight
-    constexpr int D0 = NR == 1 ? C3_DEPTH : C3_DEPTH_WIDE;
+    // X3: hi and lo fragments per k block, half the depth (the same bytes in flight)
+    constexpr int D0 = NR == 1 ? (X3 ? C3_DEPTH / 2 : C3_DEPTH) : C3_DEPTH_WIDE;
     constexpr int D = D0 < UPL ? D0 : UPL;
     // every block starts at ring slot 0 (slot = k block % D)
     static_assert(UPL % D == 0, "the fragment ring depth must divide a block's k blocks");
     bf16x8 fr[D][TN];
+    bf16x8 frl[X3 ? D : 1][TN];  // X3: the lo image's fragments
+    // X3: the lo image of a block's weight follows its hi image -- k block kb of lo is k
+    // block kb + (k blocks of the image): k_pad / 32 for the input layers (fed X), H / 32
+    // for the hidden ones (forward and transposed)
+    auto lo_kb = [&](const C3Block& B) { return B.a_x ? k_pad / 32 : UPL; };
     // buffer loads: descriptor per image in SGPRs, k-block offset in soffset, tile offset
     // as the immediate, one VGPR of lane offset -- no 64-bit address registers
     const unsigned lane_off = (unsigned)(t0 * 64 + lane) * 16u;
@@ -337,6 +350,71 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       }
     };
+    // X3: the gather from the fp32 table (the split-bf16 mode keeps fp32 eigenfunctions): a
+    // thread's 8 columns are two 16-byte loads per corner, x in fp32 in the reference order
+    // (b0 e0 + b1 e1 + b2 e2), then hi = bf16(x) into the feature tile and lo = bf16(x - hi)
+    // into the lo tile (chainf.hip's split of the same fp32 values)
+    const __amdgpu_buffer_rsrc_t rtf = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(X3 ? a.table_f32 : reinterpret_cast<const float*>(a.table)), (short)0, (int)0xFFFFFFFFu,
+        0x00020000);
+    auto gather_x3 = [&](auto BIGc, int col0, int ncols) {
+      constexpr bool BIG = decltype(BIGc)::value;
+      constexpr int GR = 2;
+      const int cpr = ncols >> 3;
+      const int nch = BM * cpr;
+#pragma unroll 1
+      for (int q0 = tid; q0 < nch; q0 += C3_CT * GR) {
+        u32x4 ev[GR][3][2];
+        float wv[GR][3];
+        int okv[GR];
+#pragma unroll
+        for (int g = 0; g < GR; ++g) {
+          const int q = q0 + C3_CT * g;
+          const int r = (q < nch ? q : 0) / cpr, ch = (q < nch ? q : 0) % cpr;
+          okv[g] = q < nch ? (rvid[BM * 4 + r * 3] & rvid[BM * 4 + r * 3 + 1] & rvid[BM * 4 + r * 3 + 2]) : 0;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            wv[g][i] = rbary[r * 3 + i];
+            if constexpr (BIG) {
+              const float* src = a.table_f32 + (int64_t)rvid[r * 4 + i] * k_pad + col0 + ch * 8;
+              ev[g][i][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+              ev[g][i][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 4));
+            } else {
+              const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + col0 + ch * 8) * 4u;
+              ev[g][i][0] = __builtin_amdgcn_raw_buffer_load_b128(rtf, off, 0, 0);
+              ev[g][i][1] = __builtin_amdgcn_raw_buffer_load_b128(rtf, off + 16u, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < GR; ++g) {
+          const int q = q0 + C3_CT * g;
+          if (q < nch) {
+            const int r = q / cpr, ch = q % cpr;
+            u32x4 oh, ol;
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              float x[2];
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const int ee = e + u;
+                const float e0 = __builtin_bit_cast(float, ev[g][0][ee >> 2][ee & 3]);
+                const float e1 = __builtin_bit_cast(float, ev[g][1][ee >> 2][ee & 3]);
+                const float e2 = __builtin_bit_cast(float, ev[g][2][ee >> 2][ee & 3]);
+                const float v = fmaf(wv[g][2], e2, fmaf(wv[g][1], e1, wv[g][0] * e0));
+                x[u] = okv[g] ? v : 0.f;
+              }
+              const unsigned w = pack_bf16x2(x[0], x[1]);
+              oh[e >> 1] = w;
+              ol[e >> 1] = pack_bf16x2(x[0] - __builtin_bit_cast(float, w << 16), x[1] - __builtin_bit_cast(float, w & 0xFFFF0000u));
+            }
+            char* d = xs + r * xrow + ((ch ^ (r & 15)) << 4);
+            *reinterpret_cast<u32x4*>(d) = oh;
+            *reinterpret_cast<u32x4*>(d + x_lo) = ol;
+          }
+        }
+      }
+    };
     // ZP: the lane's layer-0 pre-activations (its accumulators of phase 0), ahead of the
     // fragment prologue in the in-order vmcnt queue
     f32x4 z0[ZP ? TN : 1];
@@ -355,6 +433,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       for (int kb = 0; kb < D; ++kb) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) fr[kb][j] = frag(rs0, a.blk[0].kb0 + kb, j);
+        if constexpr (X3) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) frl[kb][j] = frag(rs0, a.blk[0].kb0 + lo_kb(a.blk[0]) + kb, j);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -418,6 +500,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
         *reinterpret_cast<u16x8*>(xs + r * xrow + ((ch ^ (r & 15)) << 4)) = o;
       }
+    } else if constexpr (X3) {
+      if (a.table_big) gather_x3(std::true_type{}, 0, k_pad);
+      else gather_x3(std::false_type{}, 0, k_pad);
     } else if constexpr (!ZP) {
       const int n0 = XC ? min(C::KC, k_pad) : k_pad;
       if (a.table_big) gather_cols(std::integral_constant<int, 4>{}, std::true_type{}, std::true_type{}, 0, n0);
@@ -478,6 +563,18 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
           const int t = t0 + j;
           *reinterpret_cast<u32x2*>(act + act_off(t >> 1, r16, g4) + 8 * (t & 1)) = w;
         }
+      }
+    };
+    // X3: the hi tile as put_act, then lo = v - bf16(v) into the buffer's lo tile
+    auto put_act2 = [&](const float (&v)[TN][4], char* act) {
+      put_act(v, act);
+      if constexpr (X3) {
+        float lo[TN][4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lo[j][r] = v[j][r] - __builtin_bit_cast(float, (unsigned)bf_bits3(v[j][r]) << 16);
+        put_act(lo, act + C::ACT_LO);
       }
     };
     // the inverse of put_act for this lane's own slots
@@ -601,6 +698,13 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
             }
 #pragma unroll
             for (int r = 0; r < 4; r += 2) {
+              if constexpr (X3) {  // fp32 activations: the head reads them, put_act2 splits them
+                hq[j][r] = relu1(z[r]);
+                hq[j][r + 1] = relu1(z[r + 1]);
+                bits |= (hq[j][r] > 0.f ? 1u : 0u) << (n * NV + j * 4 + r);
+                bits |= (hq[j][r + 1] > 0.f ? 1u : 0u) << (n * NV + j * 4 + r + 1);
+                continue;
+              }
               const unsigned w = pack_bf16x2(relu1(z[r]), relu1(z[r + 1]));
               hq[j][r] = __builtin_bit_cast(float, w << 16);
               hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
@@ -617,7 +721,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
             }
           }
           if (!last) {
-            put_act(hq, act_out + n * C::TILE_BYTES);
+            put_act2(hq, act_out + n * C::TILE_BYTES);
           } else {
             // ---- head on the registers of the last hidden layer (model.py:89-94) --------
             // z partials over this lane's features, then over the 4 row groups (a wave's WN
@@ -739,7 +843,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
                 gv[j][r] = hq[j][r] > 0.f ? g : 0.f;
               }
             }
-            put_act(gv, act_out + n * C::TILE_BYTES);
+            put_act2(gv, act_out + n * C::TILE_BYTES);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -786,7 +890,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               v[j][r] = ((bits >> (n * NV + j * 4 + r)) & 1u) ? acc[n][j][r] : 0.f;
               cst[j][r] = n == 0 ? v[j][r] : cst[j][r] + v[j][r];
             }
-          put_act(v, act_out + n * C::TILE_BYTES);
+          put_act2(v, act_out + n * C::TILE_BYTES);
         }
         ray_sums_to(cst, cs_out);
       }
@@ -867,7 +971,43 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         const int ao = kb * 1024 + aoffs[kb & 3];
         return *reinterpret_cast<const bf16x8*>(bbase + n * nstride + ao + fx * (xo - ao));
       };
-      if constexpr (NR == 1) {
+      if constexpr (X3) {
+        // split-bf16: per k block the lo operands too, three MFMAs per tile in gemm.hip's
+        // order (lo.hi, hi.lo, hi.hi: the small terms first); both operands read one k block
+        // ahead, hi and lo fragments refilled together
+        const int lod = from_x ? x_lo : C::ACT_LO;
+        const int clo = lo_kb(B), nlo = lo_kb(Bn);
+        auto bread_lo = [&](int kb) -> bf16x8 {
+          const int xo = ((kb * 4 + g4) ^ r16) << 4;
+          const int ao = kb * 1024 + aoffs[kb & 3];
+          return *reinterpret_cast<const bf16x8*>(bbase + lod + ao + fx * (xo - ao));
+        };
+        bf16x8 bq[2], bl[2];
+        bq[0] = bread(0, 0);
+        bl[0] = bread_lo(0);
+#pragma unroll
+        for (int kb = 0; kb < UPL; ++kb) {
+          if (kb + 1 < UPL) {
+            bq[(kb + 1) & 1] = bread(kb + 1, 0);
+            bl[(kb + 1) & 1] = bread_lo(kb + 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+#ifndef X3_DBG_NOLO  // diagnostics: the hi.hi product alone
+            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frl[kb % D][j], bq[kb & 1], acc[0][j], 0, 0, 0);
+            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bl[kb & 1], acc[0][j], 0, 0, 0);
+#endif
+            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kb % D][j], bq[kb & 1], acc[0][j], 0, 0, 0);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            fr[kb % D][j] = kb + D < UPL ? frag(crs, ckb + kb + D, j) : frag(nrs, nkb + kb + D - UPL, j);
+            frl[kb % D][j] = kb + D < UPL ? frag(crs, ckb + clo + kb + D, j) : frag(nrs, nkb + nlo + kb + D - UPL, j);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else if constexpr (NR == 1) {
         // the B operand of k-block kb + 1 is read ahead of kb's MFMAs (a scheduling barrier
         // keeps the read there: left alone, the scheduler sinks it to its use and the LDS
         // latency is exposed at every k-block, behind only TN MFMAs)
@@ -1065,6 +1205,15 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 #pragma unroll 1
       for (int n = 0; n < NR; ++n) copy_image(addr, R, img, s_begin, s_end, n);
     };
+    // X3: the lo tile (lo_delta bytes from the hi one) into the lo image, R x rows after
+    // the hi one (lgemm SPLIT's operand pair)
+    auto copy_tiles2 = [&](auto addr, int lo_delta, int R, bf16* img, int s_begin, int s_end) {
+      copy_tiles(addr, R, img, s_begin, s_end);
+      if constexpr (X3) {
+        auto lo_addr = [&](int t, int n, int r, int q) -> const char* { return addr(t, n, r, q) + lo_delta; };
+        copy_tiles(lo_addr, R, img + (int64_t)R * a.rows, s_begin, s_end);
+      }
+    };
     // X^T for the dW GEMMs of layer 0 and Ly, copied while the compute waves stream the
     // long input-layer phases (W_0: phase 0, W_y: the skip phase s), half in each
     const int xs_total = k_pad / 32;
@@ -1082,7 +1231,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       }
       if (NR > 1) lbar();  // BX: the feature-tile region takes the parked W_y x
     } else if constexpr (!ZP) {
-      copy_tiles(x_addr, k_pad, a.XT, 0, xs_mid);
+      copy_tiles2(x_addr, x_lo, k_pad, a.XT, 0, xs_mid);
     }
     if constexpr (ZP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W_y x landed before B2(0)
     auto copy_out = [&](const char* src, void* dst, int bytes) {
@@ -1116,10 +1265,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const int64_t part0 = blockIdx.x;
       if (p < nfwd) {
         const int l = p;
-        if (!head_phase) copy_tiles(act_addr, H, a.YT[l], 0, H / 32);
-        if (!XC && !ZP && p == a.s - 1) copy_tiles(x_addr, k_pad, a.XT, xs_mid, xs_total);
+        if (!head_phase) copy_tiles2(act_addr, C::ACT_LO, H, a.YT[l], 0, H / 32);
+        if (!XC && !ZP && p == a.s - 1) copy_tiles2(x_addr, x_lo, k_pad, a.XT, xs_mid, xs_total);
         if (head_phase) {
-          copy_tiles(act_addr, H, a.dZT[L - 2], 0, H / 32);
+          copy_tiles2(act_addr, C::ACT_LO, H, a.dZT[L - 2], 0, H / 32);
           copy_out(cs, a.colsum[L - 2] + part0 * H, H * 4);
           copy_out(reinterpret_cast<const char*>(hws), a.hw_part + part0 * 3 * H, 3 * H * 4);
           if (lane < 3) a.hb_part[part0 * 3 + lane] = hbs[lane];
@@ -1130,25 +1279,25 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
         }
       } else {
         const int l = (L - 2) - (p - nfwd);
-        copy_tiles(act_addr, H, a.dZT[l - 1], 0, H / 32);
+        copy_tiles2(act_addr, C::ACT_LO, H, a.dZT[l - 1], 0, H / 32);
         copy_out(cs, a.colsum[l - 1] + part0 * H, H * 4);
       }
     }
   }
 }
 
-template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP = false>
+template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP = false, bool X3 = false>
 int launch3_enc(const Chain3Args& a, hipStream_t stream) {
-  using C = L3<H, NR>;
+  using C = L3<H, NR, X3>;
   const int lds = C::lds_bytes(a.L, a.kc, XC);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC, NR, ZP>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain3_kernel<H, LOSS, ENC, XC, NR, ZP, X3>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = lds;
   }
-  chain3_kernel<H, LOSS, ENC, XC, NR, ZP><<<dim3((unsigned)(a.rows / C::BM)), dim3(C3_THREADS), lds, stream>>>(a);
+  chain3_kernel<H, LOSS, ENC, XC, NR, ZP, X3><<<dim3((unsigned)(a.rows / C::BM)), dim3(C3_THREADS), lds, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -1161,6 +1310,11 @@ int launch3_loss(const Chain3Args& a, int bm, hipStream_t stream) {
     }
     INF_CHECK_ARG(a.kc == a.k_pad, "chain3: chunked wide tiles need H = 256");
     return launch3_enc<H, LOSS, false, false, C3_NR_WIDE>(a, stream);
+  }
+  if (a.x3) {
+    INF_CHECK_ARG(a.kc == a.k_pad && a.encoding == INF_ENC_NONE && a.zin == nullptr && a.xpre == nullptr,
+                  "chain3: the split-bf16 chain is the whole-tile eigenfunction schedule");
+    return launch3_enc<H, LOSS, false, false, 1, false, true>(a, stream);
   }
   if (a.zin != nullptr) return launch3_enc<H, LOSS, false, false, 1, true>(a, stream);
   if (a.encoding != INF_ENC_NONE) return launch3_enc<H, LOSS, true, false, 1>(a, stream);
@@ -1179,6 +1333,12 @@ int launch3_typed(const Chain3Args& a, int bm, hipStream_t stream) {
 
 }  // namespace
 
+bool chain3_x3_lds_fits(int H, int L, int k_pad) {
+  if ((H != 128 && H != 256) || k_pad > C3_KC) return false;
+  const int lds = H == 256 ? L3<256, 1, true>::lds_bytes(L, k_pad, false) : L3<128, 1, true>::lds_bytes(L, k_pad, false);
+  return lds <= C3_LDS_CAP;
+}
+
 bool chain3_lds_fits(int H, int L, int k_pad, int64_t rows) {
   if (H != 128 && H != 256) return false;
   const int kc = chain3_kc(k_pad, rows);
@@ -1191,7 +1351,7 @@ bool chain3_lds_fits(int H, int L, int k_pad, int64_t rows) {
 
 int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
   Chain3Args a = a_in;
-  a.table_big = a.encoding == INF_ENC_NONE && a.num_vertices * (int64_t)a.k_pad * 2 >= ((int64_t)1 << 32);
+  a.table_big = a.encoding == INF_ENC_NONE && a.num_vertices * (int64_t)a.k_pad * (a.x3 ? 4 : 2) >= ((int64_t)1 << 32);
   a.gather_nt = a.encoding == INF_ENC_NONE && (size_t)a.num_vertices * (size_t)a.k_pad * 2 > C3_NT_TABLE_BYTES;
   INF_CHECK_ARG(chain3_supported(a.H, a.L, a.k_pad, a.rows), "chain3: unsupported shape");
   INF_CHECK_ARG(bm == chain3_bm(a.rows), "chain3: tile height");
@@ -1204,7 +1364,9 @@ int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
                                      a.kc == a.k_pad && a.k_pad >= 2 * a.H),
                 "chain3: precomputed input layers need the whole-tile schedule");
   INF_CHECK_ARG(a.nblk >= 1 && a.nblk <= C3_MAX_BLOCKS, "chain3: weight-stream blocks");
-  INF_CHECK_ARG(a.rgb != nullptr && (a.encoding != INF_ENC_NONE ? a.pos != nullptr : a.table != nullptr) &&
+  INF_CHECK_ARG(!a.x3 || (bm == C3BM && a.table_f32 != nullptr && chain3_x3_lds_fits(a.H, a.L, a.k_pad)),
+                "chain3: split-bf16 chain: 16-ray tiles over an fp32 table");
+  INF_CHECK_ARG(a.rgb != nullptr && (a.encoding != INF_ENC_NONE ? a.pos != nullptr : (a.table != nullptr || a.x3)) &&
                     a.vids != nullptr && a.bary != nullptr && a.XT != nullptr,
                 "chain3: inputs");
   INF_CHECK_ARG(a.encoding == INF_ENC_NONE || a.encoding == INF_ENC_XYZ || a.enc_proj != nullptr,

@@ -60,6 +60,13 @@ struct Chain3Args {
   // pre-gathered features (inf_prefetch_batch): row b of xpre [rows][k_pad] bf16 is ray b's
   // feature row, read instead of gathering three table rows (null: gather)
   const bf16* xpre;
+  // split-bf16 parity mode (INF_MODE_BF16X3): every weight image is a hi /
+  // lo pair of bf16 images (lo right after hi: k block kb of lo = k block kb + kblocks of
+  // the image), the feature and activation tiles hold hi / lo pairs, and each k block runs
+  // three MFMAs (lo.hi + hi.lo + hi.hi); the table is fp32 (table_f32) and the X^T / Y^T /
+  // dZ^T outputs are hi / lo image pairs for lgemm's SPLIT dW (lo image at + features x rows)
+  int32_t x3;
+  const float* table_f32;
   // precomputed input layers (igemm.hip): Z = [W_0; W_y] X^T without biases, fp32, in the
   // accumulator layout ([rows / 16][2H / 16] KiB); X^T already written (null: the kernel
   // gathers and streams W_0 / W_y itself)
@@ -118,6 +125,8 @@ constexpr int C3_KC_WIDE = 256;
 inline int chain3_blocks(int H, int L, int k_pad) { return 2 * (k_pad / H) + 2 * (L - 2); }
 // The kernel's LDS footprint for this shape fits the CU (chain3.hip)
 bool chain3_lds_fits(int H, int L, int k_pad, int64_t rows);
+// ... and that of the split-bf16 variant (Chain3Args::x3: 16-ray tiles, k_pad <= C3_KC)
+bool chain3_x3_lds_fits(int H, int L, int k_pad);
 inline int chain3_kc(int k_pad, int64_t rows);
 inline bool chain3_supported(int H, int L, int k_pad, int64_t rows) {
   const int upl = H / 32;

@@ -197,13 +197,16 @@ __global__ void adam_dense_kernel(int64_t n, float* __restrict__ p, const float*
                                   float* __restrict__ m, float* __restrict__ v, float one_minus_b1, float beta2,
                                   float one_minus_b2, float eps, float step_neg, float bc2_sqrt) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+#pragma clang fp contract(off)
     const float gi = g[i];
     float mi = m[i], vi = v[i];
-    // the plan's update arithmetic (adam_dev.hpp adam_elem): torch's single-tensor Adam
-    mi = mi + one_minus_b1 * (gi - mi);
-    vi = vi * beta2 + (one_minus_b2 * gi) * gi;
+    // the plan's update arithmetic (adam_dev.hpp adam_elem): torch's single-tensor Adam,
+    // roundings pinned (no contraction)
+    mi = __builtin_fmaf(one_minus_b1, gi - mi, mi);
+    const float vb = vi * beta2;
+    vi = __builtin_fmaf(one_minus_b2 * gi, gi, vb);
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = p[i] + step_neg * (mi / denom);
+    p[i] = p[i] + (step_neg * mi) / denom;
     m[i] = mi;
     v[i] = vi;
   }

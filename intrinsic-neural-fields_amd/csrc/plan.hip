@@ -53,6 +53,7 @@ struct ParamSeg {
 constexpr int64_t ALIGN = 256;
 // inf_plan::last_chain of a step on the fused fp32 chain (chainf.hip)
 constexpr int CHAIN_F32 = 6;
+constexpr int CHAIN_X3 = 7;  // the split-bf16 register chain (chain3.hip X3) of the bf16x3 mode
 
 }  // namespace
 }  // namespace inf
@@ -84,6 +85,18 @@ struct inf_plan {
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
   int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (igemm.hip), fp32 [bp_max][2H]
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
+  // sharded update (data parallel, inf_plan_shard): the item-major staging layout of
+  // `shard_world` ranks, this rank's items (+ the end-of-step item) as their own table
+  int shard_world = 0, shard_rank = 0;
+  int64_t shard_g = 0, shard_w = 0;  // one rank's chunk: floats of the gradient staging, bytes of the weight staging
+  int n_shard_items = 0;
+  int64_t o_shard_items = 0;
+  float* sh_gsh = nullptr;     // [world][shard_g] local gradients (reduce-scatter input)
+  float* sh_gshard = nullptr;  // [shard_g] this rank's reduced chunk (reduce-scatter output)
+  char* sh_wsh = nullptr;      // [world][shard_w] new weights (all-gather buffer, this rank's chunk in place)
+  // bits 1 / 2 / 4: params / exp_avg / exp_avg_sq are current on this rank's items only
+  // (set by inf_adam_shard, cleared by inf_shard_unpack into that arena)
+  int sharded_state = 0;
   int n_aux_items = 0;
   std::vector<int64_t> o_y, o_yt, o_dZ, o_dZT, o_colsum;  // per hidden layer
   std::vector<int64_t> o_slab;                            // per param segment (weights)
@@ -300,6 +313,7 @@ int build_layout(inf_plan* p) {
   p->o_tables = take(p->table_bytes);
   p->o_tables_b = take(align_up((int64_t)p->segs.size() * sizeof(AdamSeg)));
   p->o_aux_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
+  p->o_shard_items = take(align_up((nitems + 1) * sizeof(AdamItem)));
   int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
   for (const auto& g : p->segs)
     if (g.gemm) max_tiles += ceil_div(g.c_pad, 32) * ceil_div(g.R, 128);
@@ -491,7 +505,7 @@ bool use_split_lgemm(const inf_plan* p, int Bp) {
 
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket) {
   const int H = p->H, s = p->s;
-  if (chain == CHAIN_F32 && use_split_lgemm(p, Bp)) {
+  if ((chain == CHAIN_F32 || chain == CHAIN_X3) && use_split_lgemm(p, Bp)) {
     INF_CHECK_ARG(fuse == nullptr, "split-operand dW: no fused update");
     const int splits = bucket ? p->bucket_splits : p->dw_splits;
     LgemmBatch lb;
@@ -678,10 +692,20 @@ void note_shadow_write(inf_plan* p, const AdamArgs& a, hipStream_t st) {
   }
 }
 
+// A launch that reads the fp32 masters or the Adam state of every parameter: refused while
+// a sharded update left them current on this rank's items only (inf_shard_unpack first).
+int check_unsharded(const inf_plan* p, const char* what) {
+  if (p->sharded_state == 0) return INF_OK;
+  set_error(std::string(what) + ": the optimizer state is sharded (inf_adam_shard); gather it with inf_shard_pack / "
+            "all-gather / inf_shard_unpack of params, exp_avg and exp_avg_sq first");
+  return INF_ERR_STATE;
+}
+
 // Before any launch that reads W / W^T: rewrite every shadow from the fp32 masters if a
 // lazy update may have run since they were last written (always, once one was captured).
 int ensure_rowmajor(inf_plan* p, hipStream_t st) {
   if (!p->rm_stale && !p->rm_captured) return INF_OK;
+  if (int rc = check_unsharded(p, "row-major weight refresh")) return rc;
   AdamArgs a = update_args(p, p->bp_max);
   a.grad_src = GRAD_NONE;
   a.write_shadow = 1;
@@ -693,7 +717,7 @@ int ensure_rowmajor(inf_plan* p, hipStream_t st) {
 // fused chain3 steps in bf16 leave the row-major shadows to ensure_rowmajor
 // (INF_EAGER_SHADOWS=1: every update rewrites all shadows)
 int step_shadow_mode(const inf_plan* p, int chain) {
-  return ((chain == 3 && p->mode == INF_MODE_BF16) || (chain == CHAIN_F32 && p->mode != INF_MODE_BF16)) &&
+  return ((chain == 3 && p->mode == INF_MODE_BF16) || ((chain == CHAIN_F32 || chain == CHAIN_X3) && p->mode != INF_MODE_BF16)) &&
                  std::getenv("INF_EAGER_SHADOWS") == nullptr
              ? 2
              : 1;
@@ -711,7 +735,7 @@ std::vector<AdamSeg> bucket_segs(const inf_plan* p) {
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
   const int parts = chain == 3 ? Bp / chain3_bm(Bp)
-                    : chain == CHAIN_F32 ? Bp / 16
+                    : (chain == CHAIN_F32 || chain == CHAIN_X3) ? Bp / 16
                     : chain ? Bp / chain_partial_rows(chain_bm(Bp))
                             : Bp / 64;
   bool changed = false;
@@ -933,7 +957,8 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
 // layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
 // k_pad > C3_KC (config D): X is streamed in C3_KC-column chunks and phase 0 runs W_y then
 // W_0 over each chunk (W_y x kept in the second accumulator set until the skip layer).
-int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st, const bf16* xpre = nullptr) {
+int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st, const bf16* xpre = nullptr,
+               bool x3 = false) {
   const int H = p->H, L = p->L, s = p->s;
   const int upl = H / 32;
   const int nx = p->k_pad / (32 * upl);  // stream blocks of X
@@ -955,6 +980,10 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     INF_CHECK_ARG(a.enc_in_dim == p->d.in_dim, "encoding width does not match the model's in_dim");
     a.enc_proj = b->enc_proj;
     a.pos = reinterpret_cast<const float*>(b->table);
+  } else if (x3) {
+    INF_CHECK_ARG(b->table != nullptr && b->table_dtype == INF_DTYPE_F32, "chain3 (split-bf16): fp32 table batch required");
+    a.x3 = 1;
+    a.table_f32 = reinterpret_cast<const float*>(b->table);
   } else {
     INF_CHECK_ARG(b->table != nullptr && b->table_dtype == INF_DTYPE_BF16, "chain3: bf16 table batch required");
     a.table = reinterpret_cast<const bf16*>(b->table);
@@ -1087,13 +1116,34 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
-// The fused step of the fp32 parity modes (chainf.hip): eigenfunction tables up to k_pad =
+// The fused step of the bf16x3 parity mode (chain3.hip X3): chain3's
+// register-streamed schedule on bf16 matrix cores with every product split -- hi / lo bf16
+// weight images (the update writes the pair), hi / lo feature and activation tiles, three
+// MFMAs per k block -- from the fp32 table; the dW on lgemm SPLIT over the hi / lo X^T /
+// Y^T / dZ^T images it writes.  16-ray tiles, k_pad <= 1024, batches lgemm's split-K tiles
+// (Bp / dw_splits a multiple of 256); smaller batches take the layered split-bf16 kernels.
+// INF_NO_CHAIN3X3=1: the layered kernels.
+bool use_chain3x3(const inf_plan* p, const inf_batch* b, int Bp) {
+  if (p->mode != INF_MODE_BF16X3 || p->k_pad > C3_KC || chain3_wide(Bp) ||
+      !chain3_supported(p->H, p->L, p->k_pad, Bp) || !chain3_x3_lds_fits(p->H, p->L, p->k_pad))
+    return false;
+  if (b->table == nullptr || b->encoding != INF_ENC_NONE || b->table_dtype != INF_DTYPE_F32 || b->vids == nullptr ||
+      b->rgb == nullptr || !use_split_lgemm(p, Bp))
+    return false;
+  for (int l = 0; l <= p->L - 2; ++l) {
+    const ParamSeg* w = p->weight_seg(l, 0);
+    if (w == nullptr || w->f_off < 0 || (l >= 1 && w->ft_off < 0)) return false;
+  }
+  const ParamSeg* wy = p->weight_seg(p->s, 1);
+  return wy != nullptr && wy->f_off >= 0 && std::getenv("INF_NO_CHAIN3X3") == nullptr;
+}
+
+// The fused step of the fp32 parity mode (chainf.hip): eigenfunction tables up to k_pad =
 // 1024, fp32 fragment images, a dW GEMM over 16-ray blocked operands (K = Bp split
-// dw_splits ways in 32-ray k-tiles).  fp32 mode: exact-f32 dW; bf16x3 mode: the forward
-// and dX chain in exact f32 as well (more accurate than its 6 / 3 split products), the dW
-// GEMM on 3 split-bf16 products (gemm_mode).  INF_NO_CHAINF=1: the layered kernels.
+// dw_splits ways in 32-ray k-tiles), exact-f32 throughout.  (The bf16x3 mode's images are hi /
+// lo bf16 pairs since round 4: chain3 X3, above.)  INF_NO_CHAINF=1: the layered kernels.
 bool use_chainf(const inf_plan* p, const inf_batch* b, int Bp) {
-  if ((p->mode != INF_MODE_FP32 && p->mode != INF_MODE_BF16X3) || !chainf_supported(p->H, p->L, p->k_pad)) return false;
+  if (p->mode != INF_MODE_FP32 || !chainf_supported(p->H, p->L, p->k_pad)) return false;
   if (b->table == nullptr || b->encoding != INF_ENC_NONE || b->table_dtype != INF_DTYPE_F32 || b->vids == nullptr ||
       b->rgb == nullptr)
     return false;
@@ -1401,7 +1451,11 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
   p->ws = (char*)workspace;
   p->ctrl = ctrl;
 
-  // update work list
+  // update work list (a shard layout of an earlier bind is gone with it)
+  INF_CHECK_ARG(p->sharded_state == 0, "bind: the optimizer state is sharded (gather it first)");
+  p->shard_world = 0;
+  p->sh_gsh = p->sh_gshard = nullptr;
+  p->sh_wsh = nullptr;
   p->adam_segs.clear();
   p->adam_items.clear();
   const int L = p->L;
@@ -1425,6 +1479,7 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
       a.WF = g.f_off >= 0 ? p->shadow + g.f_off : nullptr;
       a.WTF = g.ft_off >= 0 ? p->shadow + g.ft_off : nullptr;
       a.wf_acc_order = g.ft_off >= 0 ? 1 : 0;  // hidden layers: fed by the activation tile
+      a.x3 = p->mode == INF_MODE_BF16X3 ? 1 : 0;  // images as hi / lo bf16 pairs (chain3 X3)
       const int flags = (g.C % 4 == 0 && g.off % 4 == 0) ? ITEM_VEC4 : 0;
       for (int r = 0; r < g.R; r += ADAM_TILE_R)
         for (int c = 0; c < g.C; c += ADAM_TILE_C) p->adam_items.push_back(AdamItem{(int32_t)i, r, c, flags});
@@ -1491,6 +1546,7 @@ int inf_plan_set_adam(inf_plan* p, float beta1, float beta2, float eps) {
 
 int inf_sync_shadow(inf_plan* p, inf_stream_t stream) {
   INF_CHECK_ARG(p != nullptr && p->bound, "plan not bound");
+  if (int rc = check_unsharded(p, "sync_shadow")) return rc;
   AdamArgs a = update_args(p, p->bp_max);
   a.grad_src = GRAD_NONE;
   a.write_shadow = 1;
@@ -1534,8 +1590,16 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   }
   const bool apply_adam = (flags & INF_STEP_ADAM) != 0;
   INF_CHECK_ARG((flags & ~(INF_STEP_ADAM | INF_STEP_ADVANCE | INF_STEP_XSLOT0 | INF_STEP_XSLOT1 | INF_STEP_PART1 |
-                           INF_STEP_PART2)) == 0,
+                           INF_STEP_PART2 | INF_STEP_SHARD)) == 0,
                 "train_step: unknown flags");
+  const bool shard = (flags & INF_STEP_SHARD) != 0;
+  INF_CHECK_ARG(!shard || ((flags & (INF_STEP_ADAM | INF_STEP_PART1 | INF_STEP_PART2)) == 0 && p->sh_gsh != nullptr &&
+                           std::getenv("INF_FUSED_UPDATE") == nullptr),
+                "train_step: INF_STEP_SHARD is a gradient-only step of a plan with bound shard buffers "
+                "(not with ADAM / PART1 / PART2 / INF_FUSED_UPDATE)");
+  if (flags & INF_STEP_ADAM) {
+    if (int rc = check_unsharded(p, "train_step with Adam")) return rc;
+  }
   const int part = (flags & INF_STEP_PART1) ? 1 : (flags & INF_STEP_PART2) ? 2 : 0;
   INF_CHECK_ARG(part == 0 || (!apply_adam && (flags & INF_STEP_ADVANCE) == 0 && !((flags & INF_STEP_PART1) &&
                                                                                   (flags & INF_STEP_PART2))),
@@ -1563,6 +1627,12 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   const bool bucketed = part != 0 && use_chain3(p, batch, Bp3) && Bp3 % (256 * p->bucket_splits) == 0 &&
                         std::getenv("INF_FUSED_UPDATE") == nullptr;
   if (part == 1) p->last_part1 = bucketed ? 1 : 0;
+  if (shard && !use_chain3(p, batch, Bp3) && !use_chainf(p, batch, Bp3) && !use_chain3x3(p, batch, Bp3)) {
+    // the other paths read the row-major shadows, rewritten from the fp32 masters, which a
+    // sharded update leaves current on this rank's items only
+    set_error("train_step: INF_STEP_SHARD needs the fused chain (chain3 / chainf) for this batch");
+    return INF_ERR_UNSUPPORTED;
+  }
   if (part == 2 && !bucketed) return INF_OK;  // PART1 reduced the whole gradient
   if (part == 2) {
     INF_CHECK_ARG(p->stepped && p->last_chain == 3 && p->saved_bp == Bp3, "train_step: PART2 without its PART1");
@@ -1584,6 +1654,11 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       a.write_shadow = step_shadow_mode(p, ck);
     } else {
       a.write_grads = 1;
+      if (shard) {  // the reduced local gradient into the item-major staging (reduce-scatter input)
+        a.shard_mode = SHARD_GRAD_OUT;
+        a.gsh = p->sh_gsh;
+        a.g_base = 0;
+      }
     }
     a.loss_part = p->W<double>(p->o_loss);
     a.nloss = nloss_;
@@ -1626,6 +1701,16 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       return launch_update(a, p->mode, st);
     }
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
+  } else if (use_chain3x3(p, batch, Bp3)) {
+    // bf16x3 mode: fused gather + split-bf16 chain -> split-operand dW (-> update below)
+    const int Bp = Bp3;
+    if ((rc = run_chain3(p, batch, Bp, pred, st, nullptr, true))) return rc;
+    if ((rc = run_weight_grads(p, Bp, st, CHAIN_X3))) return rc;
+    p->saved = false;
+    p->saved_batch = batch->batch;
+    p->saved_bp = Bp;
+    ck = CHAIN_X3;
+    nloss = Bp / 16;
   } else if (use_chainf(p, batch, Bp3)) {
     // fp32 mode: fused gather + chain (exact f32 MFMA) -> dW GEMM over its blocked
     // operands (-> update below); the chain leaves per-workgroup loss partials
@@ -1675,6 +1760,7 @@ int inf_adam_ex(inf_plan* p, int step, float lr, int flags, inf_stream_t stream)
     set_error("adam: plan not bound with grads and Adam state");
     return INF_ERR_STATE;
   }
+  if (int rc = check_unsharded(p, "adam")) return rc;
   AdamArgs a = update_args(p, p->bp_max);
   a.grad_src = GRAD_FLAT;
   a.do_adam = 1;
@@ -1686,6 +1772,169 @@ int inf_adam_ex(inf_plan* p, int step, float lr, int flags, inf_stream_t stream)
   a.write_shadow = step_shadow_mode(p, p->last_chain);
   const int rc = launch_update(a, p->mode, (hipStream_t)stream);
   if (rc == INF_OK) note_shadow_write(p, a, (hipStream_t)stream);
+  return rc;
+}
+
+// ---- sharded update (data parallel): reduce-scatter -> Adam on 1/world of the items ->
+// all-gather of the new weights in the GEMM dtype -> every rank rewrites the images ----
+
+int inf_plan_shard(inf_plan* p, int world, int rank, int64_t* grad_floats, int64_t* weight_bytes) {
+  INF_CHECK_ARG(p != nullptr && p->bound, "shard: plan not bound");
+  INF_CHECK_ARG(world >= 1 && rank >= 0 && rank < world && grad_floats != nullptr && weight_bytes != nullptr,
+                "shard: world >= 1, 0 <= rank < world");
+  if (int rc = check_unsharded(p, "shard")) return rc;
+  const int64_t wsz = p->mode == INF_MODE_BF16 ? 2 : 4;  // the update's image dtype (launch_update)
+  auto pay_g = [&](const AdamItem& it) -> int64_t {
+    if (it.seg < 0) return 0;
+    return p->adam_segs[it.seg].matrix ? ADAM_TILE_R * ADAM_TILE_C : ADAM_VEC;
+  };
+  auto pay_w = [&](const AdamItem& it) -> int64_t {
+    if (it.seg < 0) return 0;
+    return p->adam_segs[it.seg].matrix ? ADAM_TILE_R * ADAM_TILE_C * wsz : ADAM_VEC * 4;
+  };
+  int64_t total = 0;
+  for (const auto& it : p->adam_items) total += pay_g(it);
+  // contiguous groups of the item list, cut where the running gradient size passes r / world
+  // of the total; each rank's chunk is the largest group rounded up (256-byte aligned)
+  std::vector<int> group(p->adam_items.size());
+  std::vector<int64_t> gsz(world, 0), wszr(world, 0);
+  int64_t run = 0;
+  int r = 0;
+  for (size_t i = 0; i < p->adam_items.size(); ++i) {
+    const AdamItem& it = p->adam_items[i];
+    while (r + 1 < world && run >= (total * (r + 1) + world - 1) / world) ++r;
+    group[i] = it.seg < 0 ? -1 : r;
+    if (it.seg >= 0) {
+      gsz[r] += pay_g(it);
+      wszr[r] += pay_w(it);
+      run += pay_g(it);
+    }
+  }
+  int64_t Sg = 0, Sw = 0;
+  for (int q = 0; q < world; ++q) {
+    Sg = std::max(Sg, gsz[q]);
+    Sw = std::max(Sw, wszr[q]);
+  }
+  Sg = round_up(std::max<int64_t>(Sg, 64), 64);
+  Sw = round_up(std::max<int64_t>(Sw, 256), 256);
+  INF_CHECK_ARG(Sg * world < (1ll << 31) && Sw * world < (1ll << 31), "shard: staging offsets exceed 32 bits");
+  std::vector<int64_t> lg(world, 0), lw(world, 0);
+  std::vector<AdamItem> own;
+  AdamItem end_item{-1, 0, 0, 0, 0, 0};
+  for (size_t i = 0; i < p->adam_items.size(); ++i) {
+    AdamItem& it = p->adam_items[i];
+    if (group[i] < 0) {
+      it.goff = it.woff = 0;
+      end_item = it;
+      continue;
+    }
+    const int q = group[i];
+    it.goff = (int32_t)(q * Sg + lg[q]);
+    it.woff = (int32_t)(q * Sw + lw[q]);
+    lg[q] += pay_g(it);
+    lw[q] += pay_w(it);
+    if (q == rank) own.push_back(it);
+  }
+  own.push_back(end_item);  // the end-of-step item: the batch advance of a replayed epoch
+  const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
+  INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables + seg_bytes, p->adam_items.data(),
+                        p->adam_items.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  INF_HIP_TRY(hipMemcpy(p->ws + p->o_shard_items, own.data(), own.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  p->n_shard_items = (int)own.size();
+  p->shard_world = world;
+  p->shard_rank = rank;
+  p->shard_g = Sg;
+  p->shard_w = Sw;
+  p->sh_gsh = p->sh_gshard = nullptr;
+  p->sh_wsh = nullptr;
+  *grad_floats = Sg;
+  *weight_bytes = Sw;
+  return INF_OK;
+}
+
+int inf_plan_can_shard(inf_plan* p, const inf_batch* batch) {
+  if (p == nullptr || !p->bound || batch == nullptr || batch->rgb == nullptr || batch->encoding == INF_ENC_PROJECTED)
+    return 0;
+  int Bp3 = 0;
+  if (pad_batch(p, batch->batch, true, &Bp3) != INF_OK) return 0;
+  return (use_chain3(p, batch, Bp3) || use_chainf(p, batch, Bp3) || use_chain3x3(p, batch, Bp3)) &&
+                 std::getenv("INF_FUSED_UPDATE") == nullptr
+             ? 1
+             : 0;
+}
+
+int inf_plan_bind_shard(inf_plan* p, float* grad_staging, float* grad_chunk, void* weight_staging) {
+  INF_CHECK_ARG(p != nullptr && p->shard_world > 0, "bind_shard: inf_plan_shard first");
+  INF_CHECK_ARG(grad_staging != nullptr && grad_chunk != nullptr && weight_staging != nullptr,
+                "bind_shard: three staging buffers required");
+  INF_CHECK_ARG(((uintptr_t)grad_staging % 16) == 0 && ((uintptr_t)grad_chunk % 16) == 0 &&
+                    ((uintptr_t)weight_staging % 16) == 0,
+                "bind_shard: staging buffers must be 16-byte aligned");
+  p->sh_gsh = grad_staging;
+  p->sh_gshard = grad_chunk;
+  p->sh_wsh = (char*)weight_staging;
+  // slots past an item's elements are never written: they must read as zero
+  INF_HIP_TRY(hipMemset(grad_staging, 0, (size_t)(p->shard_g * p->shard_world * 4)));
+  INF_HIP_TRY(hipMemset(grad_chunk, 0, (size_t)(p->shard_g * 4)));
+  INF_HIP_TRY(hipMemset(weight_staging, 0, (size_t)(p->shard_w * p->shard_world)));
+  return INF_OK;
+}
+
+int inf_adam_shard(inf_plan* p, int flags, inf_stream_t stream) {
+  INF_CHECK_ARG((flags & ~INF_STEP_ADVANCE) == 0, "adam_shard: unknown flags");
+  INF_CHECK_ARG(p != nullptr && p->bound && p->sh_gsh != nullptr && p->exp_avg != nullptr && p->exp_avg_sq != nullptr,
+                "adam_shard: plan with Adam state and bound shard buffers required");
+  AdamArgs a = update_args(p, p->bp_max);
+  a.items = p->W<AdamItem>(p->o_shard_items);
+  a.num_items = p->n_shard_items;
+  a.grad_src = GRAD_FLAT;
+  a.shard_mode = SHARD_ADAM;
+  a.gsh = p->sh_gshard;
+  a.g_base = (int64_t)p->shard_rank * p->shard_g;
+  a.wsh = p->sh_wsh;
+  a.w_base = 0;
+  a.do_adam = 1;
+  a.write_shadow = 2;  // this rank's images now; the row-major shadows wait for the gathered masters
+  a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
+  const int rc = launch_update(a, p->mode, (hipStream_t)stream);
+  if (rc == INF_OK) {
+    note_shadow_write(p, a, (hipStream_t)stream);
+    p->sharded_state = 7;
+  }
+  return rc;
+}
+
+int inf_shard_scatter(inf_plan* p, inf_stream_t stream) {
+  INF_CHECK_ARG(p != nullptr && p->bound && p->sh_wsh != nullptr, "shard_scatter: bound shard buffers required");
+  AdamArgs a = update_args(p, p->bp_max);
+  a.grad_src = GRAD_NONE;
+  a.shard_mode = SHARD_SCATTER;
+  a.wsh = p->sh_wsh;
+  a.w_base = 0;
+  a.write_shadow = 2;
+  const int rc = launch_update(a, p->mode, (hipStream_t)stream);
+  if (rc == INF_OK) note_shadow_write(p, a, (hipStream_t)stream);
+  return rc;
+}
+
+int inf_shard_pack(inf_plan* p, const float* arena, float* chunk, inf_stream_t stream) {
+  INF_CHECK_ARG(p != nullptr && p->bound && p->shard_world > 0 && arena != nullptr && chunk != nullptr,
+                "shard_pack: plan with a shard layout, arena and chunk required");
+  return launch_shard_copy(p->W<AdamSeg>(p->o_tables), p->W<AdamItem>(p->o_shard_items), p->n_shard_items, arena,
+                           chunk, (int64_t)p->shard_rank * p->shard_g, 0, (hipStream_t)stream);
+}
+
+int inf_shard_unpack(inf_plan* p, const float* staging, float* arena, inf_stream_t stream) {
+  INF_CHECK_ARG(p != nullptr && p->bound && p->shard_world > 0 && arena != nullptr && staging != nullptr,
+                "shard_unpack: plan with a shard layout, staging and arena required");
+  const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
+  const int rc = launch_shard_copy(p->W<AdamSeg>(p->o_tables), reinterpret_cast<const AdamItem*>(p->ws + p->o_tables + seg_bytes),
+                                   (int)p->adam_items.size(), staging, arena, 0, 1, (hipStream_t)stream);
+  if (rc == INF_OK) {
+    if (arena == p->params) p->sharded_state &= ~1;
+    if (arena == p->exp_avg) p->sharded_state &= ~2;
+    if (arena == p->exp_avg_sq) p->sharded_state &= ~4;
+  }
   return rc;
 }
 
@@ -1818,7 +2067,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       break;
     }
     case INF_STAGE_CHAIN: {
-      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && (use_chain(p) || p->last_chain == CHAIN_F32),
+      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && (use_chain(p) || p->last_chain == CHAIN_F32 || p->last_chain == CHAIN_X3),
                     "chain stage needs a fused training batch");
       // replay on the saved inputs; the step counter it advances is restored by the caller
       const double Lh = p->L;
@@ -1826,6 +2075,14 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
         rc = run_chainf(p, b, Bp, nullptr, st);
         f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
         // fp32 weight images streamed per workgroup (L2 -> CU); rows in; blocked operands out
+        by = (double)(Bp / 16) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * 4.0 +
+             B * (3.0 * p->k_pad * 4.0 + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * 4.0;
+      } else if (p->last_chain == CHAIN_X3) {
+        rc = run_chain3(p, b, Bp, nullptr, st, nullptr, true);
+        // algorithmic FLOPs (the MFMAs issued are three times these: bench.py prices the
+        // mode against a third of the bf16 peak)
+        f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+        // hi / lo bf16 weight images streamed per workgroup; fp32 rows in; hi / lo images out
         by = (double)(Bp / 16) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * 4.0 +
              B * (3.0 * p->k_pad * 4.0 + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * 4.0;
       } else if (p->last_chain == 3) {

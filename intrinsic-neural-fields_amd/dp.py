@@ -50,6 +50,55 @@ def allreduce_grads(flat_grads: torch.Tensor, group=None) -> torch.Tensor:
     return flat_grads
 
 
+def _world(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def _via_host(t: torch.Tensor, group=None) -> bool:
+    """gloo (the one-GPU rehearsal backend) runs the tensor collectives on host copies."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def reduce_scatter_grads(chunk: torch.Tensor, staging: torch.Tensor, group=None) -> torch.Tensor:
+    """Sum the item-major gradient staging [world][chunk] over ranks; rank r keeps chunk r
+    (RCCL reduce-scatter; the sharded step's first collective).  World 1: chunk is staging."""
+    if _world(group) > 1:
+        if _via_host(staging, group):
+            out = torch.empty(chunk.shape, dtype=chunk.dtype)
+            dist.reduce_scatter_tensor(out, staging.cpu(), op=dist.ReduceOp.SUM, group=group)
+            chunk.copy_(out)
+        else:
+            dist.reduce_scatter_tensor(chunk, staging, op=dist.ReduceOp.SUM, group=group)
+    elif chunk.data_ptr() != staging.data_ptr():
+        chunk.copy_(staging[:chunk.numel()])
+    return chunk
+
+
+def all_gather_chunks(staging: torch.Tensor, chunk: torch.Tensor, group=None) -> torch.Tensor:
+    """staging [world][chunk] = every rank's chunk (RCCL all-gather, in place when `chunk` is
+    this rank's slice of `staging`).  World 1: nothing to do."""
+    if _world(group) > 1:
+        if _via_host(staging, group):
+            out = torch.empty(staging.shape, dtype=staging.dtype)
+            dist.all_gather_into_tensor(out, chunk.cpu(), group=group)
+            staging.copy_(out)
+        else:
+            dist.all_gather_into_tensor(staging, chunk, group=group)
+    elif chunk.data_ptr() != staging.data_ptr():
+        staging[:chunk.numel()].copy_(chunk)
+    return staging
+
+
+def gather_sharded_state(plan, group=None):
+    """After sharded steps the fp32 masters and the Adam state are current on each rank's own
+    items only: gather the three arenas (pack this rank's items -> all-gather -> unpack), so
+    every rank again holds all of them bitwise equal (evaluation, checkpoints, replica checks)."""
+    for arena in (plan.params, plan.exp_avg, plan.exp_avg_sq):
+        plan.shard_pack(arena)
+        all_gather_chunks(plan.grad_staging, plan.grad_chunk, group)
+        plan.shard_unpack(arena)
+
+
 def any_rank(flag: bool, device, group=None) -> bool:
     """True on every rank when `flag` is True on at least one (one MAX all-reduce).  Used for
     decisions that change which collectives a rank issues: they must be taken together."""
@@ -144,11 +193,16 @@ class DataParallelEpoch:
     #               all-reduce (runtime.StepPipeline lead 0: the chain reads pre-gathered rows);
     #   bucketed -- the dW GEMM and gradient reduction in two halves (inf_train_step PART1 /
     #               PART2): bucket 1 (Ly and the layers after it) is all-reduced on a side
-    #               stream while the second half's GEMM runs, then bucket 2, then Adam.
+    #               stream while the second half's GEMM runs, then bucket 2, then Adam;
+    #   sharded  -- ZeRO-1 style (include/inf_hip.h): the local gradient in item-major order,
+    #               reduce-scatter, Adam on 1/world of the items, all-gather of the new weights
+    #               in the GEMM dtype (bf16: half the bytes of the fp32 all-gather half of an
+    #               all-reduce), every rank rewrites the weight images; masters and Adam state
+    #               gathered once per epoch.
     # INF_DP_SHAPE picks one; "auto" (default at world > 1 over RCCL) captures every shape,
     # times a few replays of each on the same saved state and keeps the fastest -- the
     # decision is the MAX over ranks of each shape's time, so every rank picks the same one.
-    SHAPES = ("serial", "prefetch", "bucketed")
+    SHAPES = ("serial", "prefetch", "bucketed", "sharded")
 
     def __init__(self, group=None):
         self.group = group
@@ -192,6 +246,30 @@ class DataParallelEpoch:
         allreduce_grads(rt.grads[:split], self.group)
         plan.adam(0, 0.0, advance=True)
 
+    def _step_sharded(self, rt, plan, batch):
+        """One sharded step: reduce-scatter of the item-major gradient, Adam on this rank's
+        items (+ the batch advance), all-gather of the new weights, image rewrite."""
+        plan.train_step(batch, None, apply_adam=False, shard=True)
+        reduce_scatter_grads(plan.grad_chunk, plan.grad_staging, self.group)
+        plan.adam_shard(advance=True)
+        all_gather_chunks(plan.weight_staging, plan.weight_chunk(), self.group)
+        plan.shard_scatter()
+
+    @staticmethod
+    def _can_shard(plan, batch) -> bool:
+        """The sharded step needs a fused chain for the batch (include/inf_hip.h INF_STEP_SHARD)."""
+        return plan.can_shard(batch)
+
+    def _report_shape(self):
+        if self.rank == 0 and getattr(self, "_reported", None) != self.shape:
+            self._reported = self.shape
+            times = f" (ms per step: {self.shape_times})" if self.shape_times else ""
+            print(f"[dp] world {self.world}: step shape {self.shape}{times}", flush=True)
+
+    def _ensure_shard(self, plan):
+        if getattr(plan, "shard_world", 0) != self.world or getattr(plan, "shard_rank", -1) != self.rank:
+            plan.shard(self.world, self.rank)
+
     def _pipelined(self, count, rt, plan, batch):
         self.pipe.run(count, lambda xs: plan.train_step(batch, None, apply_adam=False, xslot=xs),
                       tail_fn=lambda: self._tail_all_reduce(rt, plan))
@@ -202,6 +280,13 @@ class DataParallelEpoch:
         elif shape == "bucketed":
             for _ in range(count):
                 self._step_bucketed(rt, plan, batch)
+        elif shape == "sharded":
+            self._ensure_shard(plan)
+            for _ in range(count):
+                self._step_sharded(rt, plan, batch)
+        elif shape == "serial_fallback":  # sharded asked for, the batch's step has no fused chain
+            for _ in range(count):
+                self._step(rt, plan, batch)
         else:
             for _ in range(count):
                 self._step(rt, plan, batch)
@@ -246,10 +331,14 @@ class DataParallelEpoch:
             if not pipe.start():
                 return None
         self.pipe = pipe
+        if shape == "sharded":
+            self._ensure_shard(plan)  # allocates: before capture
+            if not self._can_shard(plan, batch):
+                return None
         g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g1, stream=s):
-                self._steps("bucketed" if shape == "bucketed" else "serial", 1, rt, plan, batch)
+                self._steps(shape if shape in ("bucketed", "sharded") else "serial", 1, rt, plan, batch)
             if shape == "bucketed" and plan.last_part1_bucketed() != 1:
                 return None  # PART1 reduced the whole gradient: no overlap, not a real shape
             with torch.cuda.graph(gm, stream=s):
@@ -305,10 +394,13 @@ class DataParallelEpoch:
             chosen = names[int(torch.argmin(ms))]
         for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
             dst.copy_(src)
+        if getattr(plan, "shard_world", 0):
+            gather_sharded_state(plan, self.group)  # restored whole on every rank: marks them so
         plan.sync_shadow()
         g1, gm, pipe = graphs[chosen]
         self.shape, self.pipe = chosen, pipe
         self.graph = (g1, gm)
+        self._report_shape()
 
     def run(self, trainer, loader):
         """One epoch; returns (train loss, summed squared error / rays) over ALL ranks' rays,
@@ -367,7 +459,16 @@ class DataParallelEpoch:
             else:
                 plan.set_batch_index(0)
                 shape = os.environ.get("INF_DP_SHAPE", "serial")
-                self._steps("bucketed" if shape == "bucketed" else "serial", full, rt, plan, batch)
+                self.shape = shape if shape in ("bucketed", "sharded") else "serial"
+                if self.shape == "sharded":
+                    self._ensure_shard(plan)
+                    # every rank's plan has the same batch shape, so all take the same answer
+                    if any_rank(not self._can_shard(plan, batch), rt.device, self.group):
+                        self.shape = "serial_fallback"
+                self._report_shape()
+                self._steps(self.shape, full, rt, plan, batch)
+            if self.shape == "sharded":
+                gather_sharded_state(plan, self.group)
             steps = full
         if nb > full:  # partial last batch (drop_last=False), eager
             gb = N - full * B

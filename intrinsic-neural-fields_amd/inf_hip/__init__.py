@@ -21,7 +21,7 @@ LOSS_L2, LOSS_L1, LOSS_CAUCHY = 0, 1, 2
 LOSS_CODES = {"L2": LOSS_L2, "L1": LOSS_L1, "cauchy": LOSS_CAUCHY}
 MODE_CODES = {"fp32": MODE_FP32, "bf16": MODE_BF16, "bf16x3": MODE_BF16X3}
 STAGE_GATHER, STAGE_FWD_GEMM, STAGE_DW_GEMM, STAGE_UPDATE, STAGE_CHAIN = 0, 1, 2, 3, 4
-STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, STEP_PART1, STEP_PART2 = 1, 2, 4, 8, 16, 32  # inf_train_step
+STEP_ADAM, STEP_ADVANCE, STEP_XSLOT0, STEP_XSLOT1, STEP_PART1, STEP_PART2, STEP_SHARD = 1, 2, 4, 8, 16, 32, 64  # inf_train_step
 ENC_NONE, ENC_XYZ, ENC_RFF, ENC_FF, ENC_PROJECTED = 0, 1, 2, 3, 4
 ENC_CODES = {"xyz": ENC_XYZ, "rff": ENC_RFF, "ff": ENC_FF}
 
@@ -104,6 +104,13 @@ _SIGNATURES = {
     "inf_plan_last_step_path": (c_int, [c_void_p]),
     "inf_plan_grad_split": (c_int64, [c_void_p]),
     "inf_plan_last_part1_bucketed": (c_int, [c_void_p]),
+    "inf_plan_shard": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "inf_plan_bind_shard": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "inf_plan_can_shard": (c_int, [c_void_p, c_void_p]),
+    "inf_adam_shard": (c_int, [c_void_p, c_int, c_void_p]),
+    "inf_shard_scatter": (c_int, [c_void_p, c_void_p]),
+    "inf_shard_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "inf_shard_unpack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_plan_weight_generation": (c_int64, [c_void_p]),
     "inf_prefetch_batch": (c_int, [c_void_p, ctypes.POINTER(Batch), c_int, c_void_p]),
     "inf_debug_ranges": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),

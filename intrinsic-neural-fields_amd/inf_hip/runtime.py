@@ -11,7 +11,7 @@ import ctypes
 import torch
 
 from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, ENC_PROJECTED, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
-               MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_PART1, STEP_PART2, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo,
+               MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_PART1, STEP_PART2, STEP_SHARD, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo,
                c_int64, c_void_p,
                check, lib)
 
@@ -398,11 +398,12 @@ class Plan:
         check(lib.inf_backward(self.handle, ptr(dpred), ptr(grads), stream_handle()), "backward")
 
     def train_step(self, b: Batch, pred: torch.Tensor | None, apply_adam: bool, advance: bool = False,
-                   xslot: int | None = None, part: int | None = None):
+                   xslot: int | None = None, part: int | None = None, shard: bool = False):
         """inf_train_step; advance=True also moves ctrl.batch_index on (graph-replayed epochs);
         xslot: the batch's features were gathered into that pre-gather slot (prefetch);
-        part 1 / 2: the bucketed halves of a gradient-only step (grad_split())."""
-        flags = (STEP_ADAM if apply_adam else 0) | (STEP_ADVANCE if advance else 0)
+        part 1 / 2: the bucketed halves of a gradient-only step (grad_split());
+        shard: the reduced local gradient into grad_staging (the sharded step, shard())."""
+        flags = (STEP_ADAM if apply_adam else 0) | (STEP_ADVANCE if advance else 0) | (STEP_SHARD if shard else 0)
         if xslot is not None:
             flags |= STEP_XSLOT0 if xslot == 0 else STEP_XSLOT1
         if part is not None:
@@ -424,6 +425,50 @@ class Plan:
         (inf_adam_ex with INF_STEP_ADVANCE: the data-parallel step's tail)."""
         check(lib.inf_adam_ex(self.handle, int(step), float(lr), STEP_ADVANCE if advance else 0, stream_handle()),
               "adam")
+
+    # ---- sharded optimizer step (data parallel; include/inf_hip.h) -----------------
+    def shard(self, world: int, rank: int):
+        """inf_plan_shard + inf_plan_bind_shard: the item-major staging layout of `world` ranks.
+        Allocates grad_staging [world * shard_g] f32 (the reduce-scatter input), grad_chunk
+        [shard_g] f32 (its output), weight_staging [world * shard_w] bytes (the all-gather
+        buffer; weight_chunk() is this rank's part).  At world 1 the chunks alias the staging,
+        so the collectives vanish."""
+        g, w = c_int64(), c_int64()
+        check(lib.inf_plan_shard(self.handle, int(world), int(rank), ctypes.byref(g), ctypes.byref(w)), "plan_shard")
+        self.shard_world, self.shard_rank = int(world), int(rank)
+        self.shard_g, self.shard_w = int(g.value), int(w.value)
+        with torch.cuda.device(self.device):
+            self.grad_staging = torch.zeros(world * self.shard_g, dtype=torch.float32, device=self.device)
+            self.grad_chunk = self.grad_staging if world == 1 else torch.zeros(self.shard_g, dtype=torch.float32,
+                                                                                device=self.device)
+            self.weight_staging = torch.zeros(world * self.shard_w, dtype=torch.uint8, device=self.device)
+            check(lib.inf_plan_bind_shard(self.handle, ptr(self.grad_staging), ptr(self.grad_chunk),
+                                          ptr(self.weight_staging)), "plan_bind_shard")
+        return self.shard_g, self.shard_w
+
+    def can_shard(self, b: Batch) -> bool:
+        """inf_plan_can_shard: this batch's step takes a fused chain, so it can run sharded."""
+        return bool(lib.inf_plan_can_shard(self.handle, ctypes.byref(b)))
+
+    def weight_chunk(self) -> torch.Tensor:
+        r, n = self.shard_rank, self.shard_w
+        return self.weight_staging[r * n:(r + 1) * n]
+
+    def adam_shard(self, advance: bool = False):
+        """inf_adam_shard: Adam on this rank's items from grad_chunk, new weights into weight_chunk()."""
+        check(lib.inf_adam_shard(self.handle, STEP_ADVANCE if advance else 0, stream_handle()), "adam_shard")
+
+    def shard_scatter(self):
+        """inf_shard_scatter: every weight image and fp32 vector parameter from weight_staging."""
+        check(lib.inf_shard_scatter(self.handle, stream_handle()), "shard_scatter")
+
+    def shard_pack(self, arena: torch.Tensor):
+        """inf_shard_pack: this rank's items of `arena` (params / exp_avg / exp_avg_sq) -> grad_chunk."""
+        check(lib.inf_shard_pack(self.handle, ptr(arena), ptr(self.grad_chunk), stream_handle()), "shard_pack")
+
+    def shard_unpack(self, arena: torch.Tensor):
+        """inf_shard_unpack: every item of grad_staging -> `arena`."""
+        check(lib.inf_shard_unpack(self.handle, ptr(self.grad_staging), ptr(arena), stream_handle()), "shard_unpack")
 
     def render(self, b: Batch, hit: torch.Tensor, pixel_map: torch.Tensor | None, img: torch.Tensor):
         check(lib.inf_render(self.handle, ctypes.byref(b), ptr(hit), ptr(pixel_map), ptr(img), stream_handle()),
@@ -455,8 +500,10 @@ class Plan:
 
     def last_step_path(self) -> str:
         """Kernel path of the last train_step: 'layered', 'chain', 'chain3', 'chain3_chunked',
-        'chain3_wide' (64-ray tiles), 'chain_f32' (the fp32 mode's fused chain)."""
-        return {-1: None, 0: "layered", 2: "chain", 3: "chain3", 4: "chain3_chunked", 5: "chain3_wide", 6: "chain_f32"}[
+        'chain3_wide' (64-ray tiles), 'chain_f32' (the fp32 mode's fused chain), 'chain3_x3' (the
+        bf16x3 mode's split-bf16 chain)."""
+        return {-1: None, 0: "layered", 2: "chain", 3: "chain3", 4: "chain3_chunked", 5: "chain3_wide", 6: "chain_f32",
+                7: "chain3_x3"}[
             int(lib.inf_plan_last_step_path(self.handle))]
 
     def weight_generation(self) -> int:

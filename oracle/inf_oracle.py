@@ -298,16 +298,26 @@ def mlp_backward_bf16(w: dict, cache: dict, dpred: np.ndarray, num_layers: int, 
 def adam_step(p, g, m, v, step: int, lr: float, beta1=0.9, beta2=0.999, eps=1e-8):
     """One Adam update in place; `step` is the post-increment step count.
     m <- lerp(m, g, 1-b1); v <- b2*v + (1-b2)*g*g;
-    p <- p - lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)."""
+    p <- p - lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).
+    torch.optim.Adam's single-tensor CPU kernels op by op (adam.py: lerp_, mul_ + addcmul_,
+    sqrt / bc2_sqrt + eps, addcdiv_), whose roundings tools/adam_bits.py pins: lerp_ and
+    addcmul_ are fused multiply-adds, addcdiv_ is p + (value * m) / denom.  fp32 arrays take
+    the fma as one rounding of the float64 product + sum (exact product, then one rounding)."""
     dt = p.dtype
-    m += dt.type(1 - beta1) * (g - m)
-    v *= dt.type(beta2)
-    v += dt.type(1 - beta2) * g * g
+
+    def fma(a, b, c):
+        if dt == np.float32:
+            return (np.float64(a) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+        return a * b + c
+
+    m[...] = fma(dt.type(1 - beta1), g - m, m)
+    vb = v * dt.type(beta2)
+    v[...] = fma(dt.type(1 - beta2) * g, g, vb)
     bc1 = 1 - beta1 ** step
     bc2_sqrt = (1 - beta2 ** step) ** 0.5
     step_size = lr / bc1
     denom = np.sqrt(v) / dt.type(bc2_sqrt) + dt.type(eps)
-    p += dt.type(-step_size) * (m / denom)
+    p += (dt.type(-step_size) * m) / denom
 
 
 class OracleTrainer:

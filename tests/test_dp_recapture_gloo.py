@@ -223,7 +223,7 @@ def _shape_worker(rank, world, port, out_q):
         def _time_graphs(self, g, plan, full):
             timed.append(g[0])
             # rank 1 finds prefetch fastest, rank 0 bucketed; the MAX over ranks decides
-            return {"serial": 3.0, "prefetch": 1.0 if rank == 1 else 9.0, "bucketed": 2.0 + rank}[g[0]]
+            return {"serial": 3.0, "prefetch": 1.0 if rank == 1 else 9.0, "bucketed": 2.0 + rank, "sharded": 4.0}[g[0]]
 
     log = []
     plan, rt = _Plan(log), _Rt()
@@ -260,8 +260,8 @@ def test_capture_shape_choice_is_collective():
         assert r0[full][0] == r1[full][0], (full, r0[full], r1[full])
     # 16 full batches: prefetch dropped on both ranks (rank 0 could not capture it); times
     # serial 3 / bucketed max(2, 3) = 3 -> the first of the tie, serial
-    assert r0[16][1] == r1[16][1] == ["serial", "bucketed"], (r0[16], r1[16])
+    assert r0[16][1] == r1[16][1] == ["serial", "bucketed", "sharded"], (r0[16], r1[16])
     assert r0[16][0] == "serial"
-    assert set(r0[16][2]) == set(r1[16][2]) == {"serial", "bucketed"}
+    assert set(r0[16][2]) == set(r1[16][2]) == {"serial", "bucketed", "sharded"}
     # 4 full batches (< GRAPH_STEPS = 8): serial, nothing timed
     assert r0[4][0] == "serial" and r0[4][1] == [] and r1[4][1] == []

@@ -33,14 +33,18 @@ def _loaders(B, N, drop_last, k=64, V=500, seed=8):
     return tr, va
 
 
-@pytest.mark.parametrize("mode,drop_last", [("bf16", True), ("fp32", False)])
-def test_dp_epochs_world1_bitwise_single_gpu(tmp_path, mode, drop_last):
+@pytest.mark.parametrize("mode,drop_last,shape", [("bf16", True, "serial"), ("fp32", False, "serial"),
+                                                  ("bf16", True, "sharded"), ("bf16", False, "sharded")])
+def test_dp_epochs_world1_bitwise_single_gpu(tmp_path, mode, drop_last, shape, monkeypatch):
     """Trainer(dp=DataParallelEpoch()) without a process group (world 1): the reduce ->
     (identity) all-reduce -> Adam step shape, graph-replayed, leaves exactly the
-    parameters, Adam state and epoch metrics of the plain fused epochs."""
+    parameters, Adam state and epoch metrics of the plain fused epochs.  The sharded shape
+    (item-major gradient -> Adam on the rank's items -> weight all-gather -> image rewrite,
+    masters gathered at the epoch end, before a partial last batch) too."""
     import config
     import dp
     from trainer import Trainer
+    monkeypatch.setenv("INF_DP_SHAPE", shape)
     B, N = 1024, 9 * 1024 + (0 if drop_last else 300)
     outs = {}
     for tag in ("single", "dp"):
@@ -171,6 +175,46 @@ def test_train_data_parallel_two_ranks_one_gpu_gloo(tmp_path, mode, w_rel, loss_
         assert d.max() <= 2 * lr * 200 and rel <= w_rel, (k, float(d.max()), rel)
     assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
     np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=loss_rtol)
+
+
+@pytest.mark.parametrize("mode", ["bf16", "fp32"])
+def test_sharded_two_ranks_gloo_bitwise_allreduce(tmp_path, mode):
+    """`torchrun --nproc-per-node 2 train.py <cfg> --data_parallel` over gloo on the one GPU,
+    step shape sharded (reduce-scatter of the item-major gradient, Adam on each rank's half
+    of the items, all-gather of the new weights, image rewrite; masters and Adam state
+    gathered every epoch) against shape serial (all-reduce, replicated Adam): the same
+    files, the same weights BIT FOR BIT and the same scalars -- each element's gradient is
+    the same two-term sum and its update the same fp32 arithmetic, on one rank instead of
+    both."""
+    import synthetic_views as S
+    S.build(str(tmp_path), views=(4, 1, 1))
+    cfg = S.intrinsic_config(epochs=2, batch=1024)  # 512 rays per rank: chain3 / chainf steps
+    cfg["model"]["kernels"] = {"mode": mode}
+    results = {}
+    for shape in ("serial", "sharded"):
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", INF_DP_BACKEND="gloo", INF_DP_SHAPE=shape)
+        cfg["training"]["out_dir"] = f"out/{shape}"
+        path = tmp_path / f"{shape}.yaml"
+        with open(path, "w") as fh:
+            yaml.safe_dump(cfg, fh)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(PKG, "train.py"),
+               str(path), "--data_parallel"]
+        r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+        print(shape, r.stdout[-2000:], r.stderr[-3000:])
+        assert r.returncode == 0, shape
+        assert f"[dp] world 2: step shape {shape}" in r.stdout, shape  # not a fallback
+        out = tmp_path / "out" / shape
+        sd = torch.load(out / "model_last_epoch.pt", map_location="cpu", weights_only=True)
+        rows = [json.loads(x) for x in open(out / "logs" / "scalars.jsonl")]
+        results[shape] = (sorted(os.listdir(out)), sd, rows)
+    (fs, ws, rs), (fh_, wh, rh) = results["serial"], results["sharded"]
+    assert fs == fh_
+    for k in ws:
+        assert torch.equal(ws[k], wh[k]), k
+    # the epoch's losses come from each rank's own steps, the val metrics from the gathered
+    # masters: both bit for bit
+    assert [(r["tag"], r["step"], r["value"]) for r in rs] == [(r["tag"], r["step"], r["value"]) for r in rh]
 
 
 def _bucket_rays(k, V, N, seed):
