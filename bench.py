@@ -29,7 +29,8 @@ import torch  # noqa: E402
 # product, so its ceiling in algorithmic FLOPs is a third of the bf16 peak
 PEAK = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}
 HBM_PEAK = 8000.0  # GB/s
-KERNEL_NAMES = {"dw_gemm": "lgemm_kernel (grouped split-K weight-gradient GEMM, fragment-image B operand)",
+KERNEL_NAMES = {"dw_gemm": "lgemm_kernel (grouped weight-gradient GEMM, fragment-image B operand; with the "
+                           "fused update: split-K 1, each block Adam on its own 64x64 tile)",
                 "chain": "chain_kernel (fused forward + loss + dX chain, LDS weight ring)",
                 "chain3": "chain3_kernel (fused gather + forward + loss + dX chain, register-streamed weights)"}
 
@@ -441,8 +442,9 @@ def config_d_bench(args, device, B=4096, steps=40):
     ms, _ = time_steps(tr, steps, 8, 1)
     path = tr.plan.last_step_path()
     st = {"chain3": time_stage(tr.plan, STAGE_CHAIN, reps=10, batch=tr.batch),
-          "dw_gemm": time_stage(tr.plan, STAGE_DW_GEMM, reps=10),
-          "update": time_stage(tr.plan, STAGE_UPDATE, reps=10, layer=1)}
+          "dw_gemm": time_stage(tr.plan, STAGE_DW_GEMM, reps=10)}
+    if not tr.plan.last_step_fused_update():
+        st["update"] = time_stage(tr.plan, STAGE_UPDATE, reps=10, layer=1)
     gms, _, gbytes = time_stage(tr.plan, STAGE_GATHER, reps=10, batch=tr.batch)
     P = tr.plan.info.num_params
     k_pad = tr.plan.in_pad
@@ -978,8 +980,12 @@ def main():
     from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
     # per-kernel times (HIP events around repeated launches of one stage on its saved inputs)
     stages = {}
+    fused_update = tr.plan.last_step_fused_update()
+    # the bf16 step's dW GEMM runs the update inside its launch (lgemm GT: split-K 1, each block
+    # Adam on its own tile): one stage; otherwise the GEMM and the update launch
     stages["dw_gemm"] = time_stage(tr.plan, STAGE_DW_GEMM)
-    stages["update"] = time_stage(tr.plan, STAGE_UPDATE, layer=1)  # Adam + weight images, as in the step
+    if not fused_update:
+        stages["update"] = time_stage(tr.plan, STAGE_UPDATE, layer=1)  # Adam + weight images, as in the step
     chain3 = (args.mode == "bf16" and args.batch <= 8192 and args.hidden in (128, 256)
               and not os.environ.get("INF_NO_CHAIN") and not os.environ.get("INF_NO_CHAIN3"))
     if chain3:

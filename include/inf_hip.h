@@ -350,6 +350,18 @@ int64_t inf_plan_weight_generation(const inf_plan* plan);
  * INF_STEP_PART1 / PART2): bucket 1 = [split, P), bucket 2 = [0, split). */
 int64_t inf_plan_grad_split(const inf_plan* plan);
 
+/* Diagnostics: a copy of a plan buffer -- which = 0: the X^T fragment images the last
+ * fused step wrote; 1 + i / 101 + i: the forward / backward weight fragment image of
+ * parameter segment i.  *bytes: in, the capacity of dst; out, the buffer's size (0 when it
+ * does not exist).  dst NULL: the size only. */
+int inf_debug_buffer(inf_plan* plan, int which, void* dst, int64_t* bytes, inf_stream_t stream);
+
+/* 1 when the last training step ran its parameter update (or gradient reduction) inside
+ * the weight-gradient GEMM launch (bf16 fused chain, lgemm's gradient-tile mode: split-K 1,
+ * each block updating its own 64 x 64 tile), 0 when it launched it separately, -1 before
+ * any step. */
+int inf_plan_last_step_fused_update(const inf_plan* plan);
+
 /* Whether the last INF_STEP_PART1 step really split the gradient: 1 = bucketed (PART2 still
  * to run), 0 = it reduced the whole gradient (not the fused chain3 path, INF_FUSED_UPDATE, or
  * a batch not a multiple of 256 x the bucket splits: PART2 is then a no-op), -1 = no PART1

@@ -32,6 +32,10 @@ struct AdamSeg {
   // fp32 updates (bf16x3 mode): WF / WTF hold hi / lo bf16 image pairs (lo right after hi:
   // + R ldw elements for WF, + R C for WTF) instead of fp32 images -- chain3.hip X3
   int32_t x3;
+  // matrix: the index of its first work item in the update's item table (its items are
+  // contiguous, row-major over the 64 x 32 tiles: item0 + (r / 64) ceil(C / 32) + c / 32)
+  int32_t item0;
+  int32_t pad2_;
 };
 
 // Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = ADAM_VEC elements.

@@ -431,6 +431,73 @@ __device__ __forceinline__ void matrix_items_pipelined(const AdamArgs& a, const 
   }
 }
 
+// NI matrix items whose reduced gradient is an LDS tile (lgemm.hip GT: the dW^T tile of a
+// split-K-1 block -- row m - m0 = input feature, column n - n0 = output feature, the column
+// XOR-swizzled by (row / 4) % 16); item it + 1's parameters and moments load while item it
+// is applied.  The arithmetic of matrix_tile (mt_apply): bitwise the update launch on the
+// same gradient.  Requires VEC4 rows.
+template <typename T, int NI>
+__device__ __forceinline__ void matrix_items_lds(const AdamArgs& a, const AdamSeg& seg, const AdamItem (&items)[NI],
+                                                 Scalars& sc, float (*tile)[ADAM_TILE_R + 1], const float* cs,
+                                                 int cld, int m0, int n0) {
+  constexpr int NR = ADAM_TILE_R / 32;
+  const int tid = threadIdx.x;
+  const int c4 = tid & 7, rb = tid >> 3;
+  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
+  if (a.do_adam && tid == 0) {
+    int t = a.step_host;
+    float lr = a.lr_host;
+    if (t <= 0) {
+      t = a.ctrl->step;
+      lr = a.ctrl->lr;
+    }
+    const double bc1 = 1.0 - pow_int(a.beta1_d, t);
+    const double bc2 = 1.0 - pow_int(a.beta2_d, t);
+    sc.step_neg = (float)(-((double)lr / bc1));
+    sc.bc2_sqrt = (float)sqrt(bc2);
+  }
+  struct Regs {
+    bool ok[NR];
+    int64_t e[NR];
+    float w[NR][4], m[NR][4], v[NR][4];
+  } R[2];
+  auto load = [&](const AdamItem& item, Regs& r) {
+    const int gc = item.c0 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int gr = item.r0 + rb + 32 * i;
+      r.ok[i] = gr < seg.R && gc < seg.C;
+      r.e[i] = seg.off + (int64_t)(r.ok[i] ? gr : 0) * seg.C + (r.ok[i] ? gc : 0);
+      auto ld = [&](const float* base, float (&dst)[4]) {
+        const float4 x = r.ok[i] ? *reinterpret_cast<const float4*>(base + r.e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[0] = x.x, dst[1] = x.y, dst[2] = x.z, dst[3] = x.w;
+      };
+      ld(a.params, r.w[i]);
+      if (adam) {
+        ld(a.exp_avg, r.m[i]);
+        ld(a.exp_avg_sq, r.v[i]);
+      }
+    }
+  };
+  load(items[0], R[0]);
+  if (a.do_adam) lds_barrier();  // sc
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    Regs& r = R[it & 1];
+    if (it + 1 < NI) load(items[it + 1], R[(it + 1) & 1]);
+    float g[NR][4];
+    const int row0 = items[it].c0 + 4 * c4 - m0;  // input features row0 .. row0 + 3 of the tile
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int col = items[it].r0 + rb + 32 * i - n0;  // output feature
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[i][j] = cs[(row0 + j) * cld + (col ^ ((row0 >> 2) & 15))];
+    }
+    lds_barrier();  // the previous item's transposed-image tile reads are done
+    mt_apply<T, true>(a, seg, items[it], sc, tile, r.ok, r.e, r.w, r.m, r.v, g);
+  }
+}
+
 // End-of-step item: loss / SSE partials (one per chain tile) summed in a fixed order, so
 // the epoch loss is bitwise reproducible (unlike per-tile atomics), then the step's sums
 // are stored and added to the epoch sums; optionally the replayed batch index advances.

@@ -47,34 +47,43 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define LG_RA 4
 #endif
 
-template <int BM, int NP = 1>
+template <int BM, int NP = 1, int BN = LG_BN, bool GT = false>
 struct LG {
-  static constexpr int TM = BM / 16, TN = 2;
+  static constexpr int TM = BM / 16, TN = BN / 64;  // a wave owns BN / 4 columns
   static constexpr int D = LG_DEPTH;  // B units in flight per wave (fragment register ring)
   static constexpr int RA = LG_RA;  // A stages (64 deep) in flight in registers
   static_assert((2 * RA) % D == 0, "the B ring index must repeat every RA stages");
   static constexpr int ACH = BM * 8 / 256;  // 16-byte A chunks per thread per stage
   static constexpr int A_STAGE = BM * 128;  // bytes: BM rows x 64 bf16
-  static constexpr int CLD = LG_BN + 4;     // f32 staging row stride
-  // + the fused update's LDS (adam_dev tile + scalars) and a flag word at the end
+  static constexpr int CLD = BN + 4;        // f32 staging row stride
+  // + the fused update's LDS (adam_dev tile + scalars) and a flag word at the end; GT: the
+  // gradient tile stays in LDS while the update items run, so their tile follows it
   // NP operand parts (SPLIT: hi, lo) per stage
-  static constexpr int LDS = std::max(std::max(2 * NP * A_STAGE, BM * CLD * 4), ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
+  static constexpr int CS_BYTES = BM * CLD * 4;
+  static constexpr int ATILE_OFF = GT ? (CS_BYTES + 15) / 16 * 16 : 0;
+  static constexpr int LDS =
+      std::max(std::max(2 * NP * A_STAGE, CS_BYTES), ATILE_OFF + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
   static_assert(ACH >= 1 && BM * 8 % 256 == 0, "A stage must split over 256 threads");
 };
 
 __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM, bool FUSED, bool SPLIT = false>
+// GT (FUSED with LgemmBatch::fused == 2): split-K 1, and each block runs the update items of
+// its own tile on the gradient tile in LDS (adam_dev::matrix_items_lds) -- no slab, no
+// separate update launch; BN 64 keeps 224 blocks at config B.
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false>
 __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
+  static_assert(!GT || FUSED, "the gradient-tile update is a fused mode");
   constexpr int NP = SPLIT ? 2 : 1;
-  using C = LG<BM, NP>;
+  using C = LG<BM, NP, BN, GT>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // ---- fused update: vector / end-of-step items first ----------------------------------
-  float(*const atile)[ADAM_TILE_R + 1] = reinterpret_cast<float(*)[ADAM_TILE_R + 1]>(smem);
-  adam_dev::Scalars& asc = *reinterpret_cast<adam_dev::Scalars*>(smem + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4);
+  float(*const atile)[ADAM_TILE_R + 1] = reinterpret_cast<float(*)[ADAM_TILE_R + 1]>(smem + C::ATILE_OFF);
+  adam_dev::Scalars& asc =
+      *reinterpret_cast<adam_dev::Scalars*>(smem + C::ATILE_OFF + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4);
   if (FUSED && (int)blockIdx.x < batch.n_aux) {
     if ((int)blockIdx.x < batch.n_aux_items)
       adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
@@ -98,7 +107,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   local -= split * tiles;
   const int tm = local / P.tiles_n;
   const int tn = local - tm * P.tiles_n;
-  const int m0 = tm * BM, n0 = tn * LG_BN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(P.Bf), (short)0, 0x7FFFFFFF, 0x00020000);
   const __amdgpu_buffer_rsrc_t rbl =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(SPLIT ? P.Bf_lo : P.Bf), (short)0, 0x7FFFFFFF, 0x00020000);
-  const unsigned boff = (unsigned)((((P.b_row0 + n0) >> 4) + 2 * wc) * 64 + lane) * 16u;
+  const unsigned boff = (unsigned)((((P.b_row0 + n0) >> 4) + TN * wc) * 64 + lane) * 16u;
   const int bstep = P.b_tiles * 1024;  // bytes per unit
   const int kb0 = k_begin >> 5;
 
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   // lane group's 16 columns).  The row-major C / CT epilogue reads rows as vectors: unswizzled
   float* Cs = reinterpret_cast<float*>(smem);
   constexpr int CLD = C::CLD;
-  const bool swz = P.slab != nullptr;
+  const bool swz = P.slab != nullptr || GT;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -239,9 +248,26 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = i * 16 + g4 * 4 + r;
-        Cs[row * CLD + ((wc * 32 + j * 16 + r16) ^ (swz ? (row >> 2) & 15 : 0))] = acc[i][j][r];
+        Cs[row * CLD + ((wc * (16 * TN) + j * 16 + r16) ^ (swz ? (row >> 2) & 15 : 0))] = acc[i][j][r];
       }
   __syncthreads();
+
+  if constexpr (GT) {
+    // the tile's update items (the plan's own work items: shard offsets, flags) on the
+    // gradient tile in LDS
+    const AdamSeg seg = batch.adam.segs[P.adam_seg];
+    constexpr int NI = (BN / ADAM_TILE_R) * (BM / ADAM_TILE_C);
+    const int ncol = (seg.C + ADAM_TILE_C - 1) / ADAM_TILE_C;
+    AdamItem items[NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int r0 = n0 + (it / (BM / ADAM_TILE_C)) * ADAM_TILE_R, c0 = m0 + (it % (BM / ADAM_TILE_C)) * ADAM_TILE_C;
+      items[it] = batch.adam.items[seg.item0 + (r0 / ADAM_TILE_R) * ncol + c0 / ADAM_TILE_C];
+    }
+    adam_dev::matrix_items_lds<bf16, NI>(batch.adam, seg, items, asc, atile, Cs, CLD, m0, n0);
+    if (stl != nullptr) stl[3] = wall_clock64();
+    return;
+  }
 
   if (P.slab != nullptr) {
     // dW^T tile -> slab [n][m]: four consecutive m per 16-byte store, write-through (sc1):
@@ -250,7 +276,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
     constexpr int MQ = BM / 4;
 #pragma unroll 4
-    for (int q = tid; q < LG_BN * MQ; q += 256) {
+    for (int q = tid; q < BN * MQ; q += 256) {
       const int col = q / MQ, mq = q - col * MQ;
       const int cs = col ^ (mq & 15);  // rows mq 4 .. mq 4 + 3 share the swizzle
       const f32x4 v = {Cs[(mq * 4 + 0) * CLD + cs], Cs[(mq * 4 + 1) * CLD + cs], Cs[(mq * 4 + 2) * CLD + cs],
@@ -271,7 +297,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
       // and run the update kernel's own arithmetic (bitwise the same results).
       // Counters never reset: per tile [0] arrivals (S per launch, so ticket / S is this
       // launch's epoch e), [1 + i] the last epoch + 1 that claimed item i (atomic max).
-      constexpr int NI = (LG_BN / ADAM_TILE_R) * (BM / ADAM_TILE_C);
+      constexpr int NI = (BN / ADAM_TILE_R) * (BM / ADAM_TILE_C);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       int* flag = reinterpret_cast<int*>(smem + C::LDS - 16);
@@ -320,7 +346,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
     if (stl != nullptr) stl[3] = wall_clock64();
     return;
   }
-  constexpr int NQ = LG_BN / 4;
+  constexpr int NQ = BN / 4;
 #pragma unroll 4
   for (int q = tid; q < BM * NQ; q += 256) {
     const int row = q / NQ, c4 = q - row * NQ;
@@ -345,7 +371,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   __syncthreads();
   constexpr int MQ = BM / 4;
 #pragma unroll 4
-  for (int q = tid; q < LG_BN * MQ; q += 256) {
+  for (int q = tid; q < BN * MQ; q += 256) {
     const int col = q / MQ, mq = q - col * MQ;
     const bf16x4 h = {(bf16)Cs[(mq * 4 + 0) * CLD + col], (bf16)Cs[(mq * 4 + 1) * CLD + col],
                       (bf16)Cs[(mq * 4 + 2) * CLD + col], (bf16)Cs[(mq * 4 + 3) * CLD + col]};
@@ -353,16 +379,16 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   }
 }
 
-template <int BM, bool FUSED, bool SPLIT = false>
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false>
 int launch_typed(const LgemmBatch& b, hipStream_t stream) {
-  constexpr int lds = LG<BM, SPLIT ? 2 : 1>::LDS;
+  constexpr int lds = LG<BM, SPLIT ? 2 : 1, BN, GT>::LDS;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
-  lgemm_kernel<BM, FUSED, SPLIT><<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256), lds, stream>>>(b);
+  lgemm_kernel<BM, FUSED, SPLIT, BN, GT><<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -372,6 +398,8 @@ int launch_typed(const LgemmBatch& b, hipStream_t stream) {
 int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   INF_CHECK_ARG(bm == 32 || bm == 64, "lgemm: rows per block");
   INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= LGEMM_MAX_PROBLEMS, "lgemm: problem count");
+  const bool gt = b.fused == 2;  // split-K 1, the update on the LDS gradient tile (64 x 64 tiles)
+  const int bn = gt ? 64 : LG_BN;
   int blocks = 0;
   for (int i = 0; i < b.nprob; ++i) {
     LgemmProblem& p = b.p[i];
@@ -379,18 +407,25 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     INF_CHECK_ARG(p.Af != nullptr && p.Bf != nullptr, "lgemm: null operand");
     INF_CHECK_ARG(!b.split || (p.Af_lo != nullptr && p.Bf_lo != nullptr && p.slab != nullptr),
                   "lgemm: split operands need both parts and a slab");
-    INF_CHECK_ARG(p.M > 0 && p.M % bm == 0 && p.N > 0 && p.N % LG_BN == 0, "lgemm: M/N not tile multiples");
+    INF_CHECK_ARG(p.M > 0 && p.M % bm == 0 && p.N > 0 && p.N % bn == 0, "lgemm: M/N not tile multiples");
     INF_CHECK_ARG(p.K > 0 && p.K % (64 * LG_RA * p.splits) == 0, "lgemm: K per split must be a multiple of 64 RA");
     INF_CHECK_ARG(p.a_row0 % 16 == 0 && p.a_row0 + p.M <= 16 * p.a_tiles && p.b_row0 % 16 == 0 &&
                       p.b_row0 + p.N <= 16 * p.b_tiles, "lgemm: operand layout");
     INF_CHECK_ARG(p.splits == 1 || p.slab != nullptr, "lgemm: split-K needs a slab");
-    INF_CHECK_ARG(p.slab != nullptr || p.C != nullptr, "lgemm: no output");
+    INF_CHECK_ARG(p.slab != nullptr || p.C != nullptr || gt, "lgemm: no output");
+    INF_CHECK_ARG(!gt || (p.splits == 1 && p.adam_seg >= 0 && p.adam_vec4), "lgemm: gradient-tile update: split-K 1, 16-byte rows");
     p.tiles_m = p.M / bm;
-    p.tiles_n = p.N / LG_BN;
+    p.tiles_n = p.N / bn;
     p.block_begin = blocks;
     blocks += p.tiles_m * p.tiles_n * p.splits;
   }
   b.total_blocks = blocks;
+  if (gt) {
+    INF_CHECK_ARG(bm == 64 && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.adam.items != nullptr,
+                  "lgemm: gradient-tile update layout");
+    INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: the vector items reduce their slabs");
+    return launch_typed<64, true, false, 64, true>(b, stream);
+  }
   if (b.fused) {
     INF_CHECK_ARG(b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.counters != nullptr, "lgemm: fused update layout");
     for (int i = 0; i < b.nprob; ++i)

@@ -59,6 +59,8 @@ struct LgemmBatch {
   // finish a tile runs the matrix items of that tile on the summed partials; the first
   // n_aux blocks of the grid (a multiple of 8; n_aux_items of them busy) run the vector
   // and end-of-step items.  counters: one int per tile, zero between launches.
+  // fused == 2 ("gradient tile"): split-K 1 with 64 x 64 tiles, each block runs its own
+  // tile's items on the gradient in LDS (no slab, no counters).
   int32_t fused;
   int32_t n_aux, n_aux_items;
   const AdamItem* aux_items;

@@ -73,6 +73,11 @@ struct inf_plan {
   int64_t grad_split = 0;  // bucket 1 = arena [grad_split, P) (Ly and the layers after it)
   int n_items_b1 = 0;      // update work items of bucket 1 (listed first), end-of-step item included
   int last_part1 = -1;     // the last PART1 step: 1 bucketed, 0 reduced the whole gradient
+  // bf16 chain3 steps fuse the update into the dW GEMM: split-K 1, 64 x 64 tiles, each block
+  // applies Adam (or writes the gradient) to its own tile from the LDS gradient tile
+  // (lgemm.hip GT) -- no split-K slabs, no update launch (INF_NO_LGF=1: the slab path)
+  bool lgf = false;
+  bool last_lgf = false;  // the last training step took it
   int train_unit = 128;
   int bp_max = 0;
   int grid_hb = 1;
@@ -252,6 +257,12 @@ int build_layout(inf_plan* p) {
   const bool reg_dw = d.mode == INF_MODE_BF16 || d.mode == INF_MODE_BF16X3;
   if (reg_dw && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
   if (reg_dw && mb <= 4096 && S > 2) S = 2;
+  // the fused gradient-tile update (lgemm.hip GT) of the bf16 chain3 step: split-K 1 over
+  // 64 x 64 tiles whose rows are 16-byte aligned in the arena
+  p->lgf = d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && std::getenv("INF_NO_LGF") == nullptr;
+  for (const auto& g : p->segs)
+    if (g.gemm && (g.C % 4 != 0 || g.off % 4 != 0 || g.c_pad % 64 != 0 || g.R % 64 != 0)) p->lgf = false;
+  if (p->lgf) S = 1;
   // the 64-ray chain tiles' dW through lgemm (shapes fgemm does not tile) stream
   // K = Bp / S rays per block in 256-ray steps: 10,240 rays take 8 splits, not 16
   while (d.mode == INF_MODE_BF16 && mb > CHAIN3_MAX_ROWS && S > 1 && mb % (256 * (int64_t)S) != 0) S /= 2;
@@ -259,6 +270,7 @@ int build_layout(inf_plan* p) {
     const int want = std::atoi(e);
     if (want >= 1 && want <= 16 && (want & (want - 1)) == 0 && mb / want >= 128) S = want;
   }
+  if (S != 1) p->lgf = false;  // INF_DW_SPLITS: the slab path
   p->dw_splits = S;
   p->bucket_splits = S;
   if (d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && 2 * S <= 16 && (mb / (2 * S)) % 256 == 0)
@@ -573,6 +585,8 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     }
     // register-streamed chain: X^T, Y_l^T and dZ_l^T are fragment images (chain3.hip); one
     // lgemm launch computes every dW^T tile into the split-K slabs the update launch reduces
+    // (GT: split-K 1, each block updates its own tile from LDS -- the fused default)
+    const bool gt = fuse != nullptr && p->lgf && splits == 1 && bucket == 0;
     LgemmBatch lb;
     std::memset(&lb, 0, sizeof(lb));
     int ctr = 0;
@@ -598,13 +612,13 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       q.N = g.R;
       q.K = Bp;
       q.splits = splits;
-      q.slab = p->W<float>(p->o_slab[i]);
+      q.slab = gt ? nullptr : p->W<float>(p->o_slab[i]);
       q.slab_ld = g.c_pad;
       q.slab_stride = (int64_t)g.R * g.c_pad;
     }
     lb.stamps = p->lg_stamps;
     if (fuse != nullptr) {
-      lb.fused = 1;
+      lb.fused = gt ? 2 : 1;
       lb.adam = *fuse;
       lb.n_aux_items = p->n_aux_items;
       lb.n_aux = (int)round_up(p->n_aux_items, 8);
@@ -1511,6 +1525,9 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
   p->n_items_b1 = 0;
   for (const auto& it : p->adam_items)
     if (it.seg < 0 || p->segs[it.seg].off >= p->grad_split) ++p->n_items_b1;
+  // each matrix's first item (stable_partition kept a segment's items contiguous and in order)
+  for (int i = (int)p->adam_items.size() - 1; i >= 0; --i)
+    if (p->adam_items[i].seg >= 0) p->adam_segs[p->adam_items[i].seg].item0 = i;
   const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
   INF_CHECK_ARG(seg_bytes + (int64_t)(p->adam_items.size() * sizeof(AdamItem)) <= p->table_bytes, "table size");
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
@@ -1594,7 +1611,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
                 "train_step: unknown flags");
   const bool shard = (flags & INF_STEP_SHARD) != 0;
   INF_CHECK_ARG(!shard || ((flags & (INF_STEP_ADAM | INF_STEP_PART1 | INF_STEP_PART2)) == 0 && p->sh_gsh != nullptr &&
-                           std::getenv("INF_FUSED_UPDATE") == nullptr),
+                           (p->lgf || std::getenv("INF_FUSED_UPDATE") == nullptr)),
                 "train_step: INF_STEP_SHARD is a gradient-only step of a plan with bound shard buffers "
                 "(not with ADAM / PART1 / PART2 / INF_FUSED_UPDATE)");
   if (flags & INF_STEP_ADAM) {
@@ -1683,8 +1700,12 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     ck = 3;
     nloss = Bp / chain3_bm(Bp);
     p->stepped = true;
-    if (std::getenv("INF_FUSED_UPDATE") != nullptr) {
+    p->last_lgf = false;
+    if (!bucketed && (p->lgf || std::getenv("INF_FUSED_UPDATE") != nullptr)) {
+      // the update inside the dW launch: lgf (default, split-K 1: each block its own tile
+      // from LDS) or INF_FUSED_UPDATE (split-K slabs, the last arriving block of a tile)
       p->last_chain = 3;
+      p->last_lgf = p->lgf;
       if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
       const AdamArgs a = step_update(Bp, nloss);
       if ((rc = run_weight_grads(p, Bp, st, 3, &a))) return rc;
@@ -2058,6 +2079,21 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       break;
     }
     case INF_STAGE_DW_GEMM: {
+      if (p->last_lgf) {  // the step's fused dW + update launch (Adam, lr from ctrl: parameters change)
+        if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
+        AdamArgs a = update_args(p, Bp);
+        a.grad_src = GRAD_SLABS;
+        a.do_adam = 1;
+        a.write_shadow = step_shadow_mode(p, 3);
+        rc = run_weight_grads(p, Bp, st, 3, &a);
+        if (rc == INF_OK) note_shadow_write(p, a, st);
+        for (const auto& g : p->segs)
+          if (g.gemm) {
+            f += 2.0 * g.R * g.C * B;
+            by += (double)B * (g.R + g.C) * e;
+          }
+        break;
+      }
       rc = run_weight_grads(p, Bp, st, p->last_chain);
       for (const auto& g : p->segs)
         if (g.gemm) {
@@ -2181,6 +2217,33 @@ int inf_prefetch_batch(inf_plan* p, const inf_batch* b, int slot, inf_stream_t s
 int64_t inf_plan_grad_split(const inf_plan* p) { return p == nullptr ? -1 : p->grad_split; }
 
 int inf_plan_last_part1_bucketed(const inf_plan* p) { return p == nullptr ? -1 : p->last_part1; }
+
+int inf_plan_last_step_fused_update(const inf_plan* p) { return p == nullptr || !p->stepped ? -1 : (p->last_lgf ? 1 : 0); }
+
+int inf_debug_buffer(inf_plan* p, int which, void* dst, int64_t* bytes, inf_stream_t stream) {
+  INF_CHECK_ARG(p != nullptr && p->bound && bytes != nullptr, "debug_buffer: bound plan");
+  const char* src = nullptr;
+  int64_t n = 0;
+  if (which == 0) {
+    src = p->ws + p->o_x0t;
+    n = (int64_t)p->k_pad * p->bp_max * p->esz;
+  } else {
+    const int i = which >= 100 ? which - 101 : which - 1;
+    INF_CHECK_ARG(i >= 0 && i < (int)p->segs.size(), "debug_buffer: segment index");
+    const ParamSeg& g = p->segs[i];
+    const int64_t off = which >= 100 ? g.ft_off : g.f_off;
+    if (off >= 0) {
+      src = p->shadow + off;
+      n = which >= 100 ? (int64_t)p->H * p->H * p->esz : (int64_t)g.R * g.c_pad * p->esz;
+    }
+  }
+  if (dst != nullptr && n > 0) {
+    INF_CHECK_ARG(*bytes >= n, "debug_buffer: destination too small");
+    INF_HIP_TRY(hipMemcpyAsync(dst, src, (size_t)n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  }
+  *bytes = n;
+  return INF_OK;
+}
 
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;

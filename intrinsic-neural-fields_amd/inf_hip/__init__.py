@@ -104,6 +104,8 @@ _SIGNATURES = {
     "inf_plan_last_step_path": (c_int, [c_void_p]),
     "inf_plan_grad_split": (c_int64, [c_void_p]),
     "inf_plan_last_part1_bucketed": (c_int, [c_void_p]),
+    "inf_plan_last_step_fused_update": (c_int, [c_void_p]),
+    "inf_debug_buffer": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "inf_plan_shard": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "inf_plan_bind_shard": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_plan_can_shard": (c_int, [c_void_p, c_void_p]),

@@ -446,6 +446,18 @@ class Plan:
                                           ptr(self.weight_staging)), "plan_bind_shard")
         return self.shard_g, self.shard_w
 
+    def debug_buffer(self, which: int) -> torch.Tensor:
+        """inf_debug_buffer: a uint8 copy of a plan buffer (which 0 = the X^T images of the
+        last fused step, 1 + i / 101 + i = segment i's forward / backward weight image; empty
+        when it has none).  Diagnostics only."""
+        n = c_int64(0)
+        check(lib.inf_debug_buffer(self.handle, int(which), None, ctypes.byref(n), stream_handle()), "debug_buffer")
+        out = torch.empty(max(n.value, 0), dtype=torch.uint8, device=self.device)
+        if n.value:
+            check(lib.inf_debug_buffer(self.handle, int(which), ptr(out), ctypes.byref(n), stream_handle()),
+                  "debug_buffer")
+        return out
+
     def can_shard(self, b: Batch) -> bool:
         """inf_plan_can_shard: this batch's step takes a fused chain, so it can run sharded."""
         return bool(lib.inf_plan_can_shard(self.handle, ctypes.byref(b)))
@@ -514,6 +526,10 @@ class Plan:
     def grad_split(self) -> int:
         """inf_plan_grad_split: gradient bucket 1 = arena [split, P), bucket 2 = [0, split)."""
         return int(lib.inf_plan_grad_split(self.handle))
+
+    def last_step_fused_update(self) -> bool:
+        """inf_plan_last_step_fused_update: the last step's update ran inside the dW GEMM launch."""
+        return int(lib.inf_plan_last_step_fused_update(self.handle)) == 1
 
     def last_part1_bucketed(self) -> int:
         """inf_plan_last_part1_bucketed: 1 if the last part=1 step split the gradient, 0 if it

@@ -431,10 +431,12 @@ def test_bf16_chain_render_matches_layered(monkeypatch):
 
 @pytest.mark.parametrize("apply_adam", [True, False])
 def test_fused_update_bitwise(apply_adam, monkeypatch):
-    """The update fused into the dW GEMM launch (INF_FUSED_UPDATE: the last split-K block
-    of each tile runs the update kernel's own matrix items on the sc1-published partials)
-    leaves exactly the bytes of the separate update launch: parameters, Adam state (or the
-    reduced gradients) and the step's loss sums, over three steps of 4096 rays."""
+    """The split-K slab path (INF_NO_LGF): the update fused into the dW GEMM launch
+    (INF_FUSED_UPDATE: the last split-K block of each tile runs the update kernel's own
+    matrix items on the sc1-published partials) leaves exactly the bytes of the separate
+    update launch: parameters, Adam state (or the reduced gradients) and the step's loss
+    sums, over three steps of 4096 rays."""
+    monkeypatch.setenv("INF_NO_LGF", "1")
     rng = np.random.default_rng(5)
     k, H, L, s = CFG["B"]
     V, B = 3000, 4096
@@ -461,6 +463,50 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
     for a_, b_ in zip(out["separate"][:4], out["fused"][:4]):
         assert np.array_equal(a_, b_)
     assert out["separate"][4] == out["fused"][4]
+
+
+@pytest.mark.parametrize("name,B,apply_adam", [("B", 4096, True), ("B", 4096, False), ("B", 1024, True),
+                                               ("A", 4096, True), ("B", 8192, True)])
+def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
+    """The default bf16 step fuses the update into the dW GEMM (lgemm.hip GT: split-K 1,
+    64 x 64 tiles, each block runs Adam -- or writes the reduced gradient -- on its own tile
+    from the LDS gradient tile).  Against the split-K slab path (INF_NO_LGF: lgemm into 2
+    slabs, the separate update launch): the same chain, so the same loss sums bit for bit;
+    the gradients differ only in the K-sum's order (split-K 2 partials vs one accumulator:
+    1e-6 of each tensor's max, seen ~1e-7) and the Adam steps follow (<= 0.1 % of the
+    elements by up to lr, assert_adam_close), over three steps."""
+    rng = np.random.default_rng(15)
+    k, H, L, s = CFG[name]
+    V = 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (B, 3))).cuda(),
+                         torch.from_numpy(rng.dirichlet([1, 1, 1], B).astype(np.float32)).cuda(),
+                         torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
+    out = {}
+    for tag in ("lgf", "slab"):
+        if tag == "slab":
+            monkeypatch.setenv("INF_NO_LGF", "1")
+        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+        plan.set_lr(1e-3)
+        b = plan.make_batch(source=src, batch=B)
+        sums = []
+        for _ in range(3 if apply_adam else 1):
+            plan.train_step(b, None, apply_adam=apply_adam)
+            assert plan.last_step_path() == "chain3"
+            assert plan.last_step_fused_update() == (tag == "lgf")
+            c = plan.read_ctrl()
+            sums.append((c["loss_sum"], c["sse_sum"]))
+        torch.cuda.synchronize()
+        out[tag] = (arena_to_dict(params, w, *CFG[name][2:]), arena_to_dict(plan.grads, w, *CFG[name][2:]), sums)
+    assert out["lgf"][2][0] == out["slab"][2][0]  # the first step's chain: identical
+    for n in O.layer_names(*CFG[name][2:]):
+        if apply_adam:
+            assert_adam_close(out["lgf"][0][n], out["slab"][0][n], lr=1e-3, steps=3, name=n, atol=1e-6)
+        else:
+            ref = out["slab"][1][n]
+            err = float(np.abs(out["lgf"][1][n] - ref).max() / max(np.abs(ref).max(), 1e-12))
+            assert err < 1e-5, (n, err)
 
 
 def test_dp_step_shape_bitwise_equals_fused_step():

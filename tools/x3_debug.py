@@ -37,3 +37,73 @@ for name, B in (("B", 4096), ("R", 2048)):
         err = np.abs(pred.cpu().numpy() - p_ref)
         print(name, mode, plan.last_step_path(), "RGB err max", float(err.max()), "mean", float(err.mean()),
               "rows>1e-3", int((err.max(1) > 1e-3).sum()), "first bad rows", np.nonzero(err.max(1) > 1e-3)[0][:8].tolist())
+
+# ---- images and X^T: the bf16 plan's vs the bf16x3 plan's hi halves -------------------
+name, B = "B", 4096
+k, H, L, s = CFG[name]
+d = golden(f"g2_forward_{name}.npz")
+w = {kk[2:]: d[kk] for kk in d.files if kk.startswith("w:")}
+rng = np.random.default_rng(31)
+V = 2000
+E = rng.standard_normal((V, k)).astype(np.float32)
+E /= E.max(0) - E.min(0)
+vids = rng.integers(0, V, (B, 3))
+bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+rgb = rng.random((B, 3)).astype(np.float32)
+src = runtime.RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                        torch.from_numpy(rgb).cuda())
+plans = {}
+for mode in ("bf16", "bf16x3"):
+    params = torch.cat([torch.from_numpy(np.ascontiguousarray(w[n])).reshape(-1) for n in O.layer_names(L, s)]).cuda()
+    plan = runtime.Plan(k, H, L, s, mode, "L2", B, params, torch.zeros_like(params), torch.zeros_like(params),
+                        torch.zeros_like(params))
+    plans[mode] = plan
+names = O.layer_names(L, s)
+for i, n in enumerate(names):
+    for fwd in (True, False):
+        a = plans["bf16"].debug_buffer((1 if fwd else 101) + i)
+        b = plans["bf16x3"].debug_buffer((1 if fwd else 101) + i)
+        if a.numel() == 0:
+            continue
+        h = b[:a.numel()]
+        lo = b[a.numel():].view(torch.bfloat16).float()
+        print(n, "fwd" if fwd else "bwd", "bytes", a.numel(), b.numel(), "hi==bf16 image:", bool(torch.equal(a, h)),
+              "mismatch bytes", int((a != h).sum()), "lo |max|", float(lo.abs().max()),
+              "hi |max|", float(h.view(torch.bfloat16).float().abs().max()))
+for mode, plan in plans.items():
+    pred = torch.empty((B, 3), device="cuda")
+    plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
+    print(mode, plan.last_step_path())
+xa = plans["bf16"].debug_buffer(0)
+xb = plans["bf16x3"].debug_buffer(0)
+na = k * 0 + plans["bf16"].in_pad * B * 2
+A = xa[:na].view(torch.bfloat16).float()
+Bh = xb[:na].view(torch.bfloat16).float()
+Bl = xb[na:2 * na].view(torch.bfloat16).float()
+print("X^T images: bf16 |max|", float(A.abs().max()), "x3 hi |max|", float(Bh.abs().max()), "x3 lo |max|",
+      float(Bl.abs().max()), "max |bf16 - x3 hi|", float((A - Bh).abs().max()))
+
+
+def decode_xt(flat, R, Bn):
+    """fragment image (R features x Bn rays, lgemm.hpp layout) -> [ray][feature]"""
+    f = np.arange(R)[None, :]
+    b = np.arange(Bn)[:, None]
+    off = ((b // 32) * (R // 16) + f // 16) * 512 + (f % 16 + 16 * ((b % 32) // 8)) * 8 + b % 8
+    return flat[off]
+
+
+kp = plans["bf16"].in_pad
+xa_d = decode_xt(A.numpy(), kp, B)
+xh_d = decode_xt(Bh.numpy(), kp, B)
+xl_d = decode_xt(Bl.numpy(), kp, B)
+xo = np.zeros((B, kp), np.float32)
+xo[:, :k] = O.gather(E, vids, bary)
+print("bf16 X^T vs oracle max", float(np.abs(xa_d - xo).max()), " x3 hi+lo vs oracle max", float(np.abs(xh_d + xl_d - xo).max()))
+bad = np.abs(xh_d + xl_d - xo) > 1e-3
+print("x3 bad fraction", float(bad.mean()), "bad rays", np.nonzero(bad.any(1))[0][:10].tolist(), "bad features", np.nonzero(bad.any(0))[0][:40].tolist())
+print("ray 0 oracle", np.round(xo[0, :12], 4).tolist())
+print("ray 0 x3    ", np.round((xh_d + xl_d)[0, :12], 4).tolist())
+print("ray 0 bf16  ", np.round(xa_d[0, :12], 4).tolist())
+# is the x3 tile a permutation of the oracle's within a ray?
+for shift in (4, 8, 16, 32, 64, 128, 512):
+    print("shift", shift, float(np.abs((xh_d + xl_d)[:, :kp - shift] - xo[:, shift:]).max()), float(np.abs((xh_d + xl_d)[:, shift:] - xo[:, :kp - shift]).max()))
