@@ -364,7 +364,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       const int nch = BM * cpr;
 #pragma unroll 1
       for (int q0 = tid; q0 < nch; q0 += C3_CT * GR) {
-        u32x4 ev[GR][3][2];
+        // (whole vectors bit-cast at the load: a __builtin_bit_cast of one element of a
+        // vector with a non-constant subscript reads element 0 -- it takes the operand's
+        // address, and a vector element has none)
+        f32x4 ev[GR][3][2];
         float wv[GR][3];
         int okv[GR];
 #pragma unroll
@@ -377,12 +380,12 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
             wv[g][i] = rbary[r * 3 + i];
             if constexpr (BIG) {
               const float* src = a.table_f32 + (int64_t)rvid[r * 4 + i] * k_pad + col0 + ch * 8;
-              ev[g][i][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
-              ev[g][i][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 4));
+              ev[g][i][0] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src)));
+              ev[g][i][1] = __builtin_bit_cast(f32x4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 4)));
             } else {
               const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + col0 + ch * 8) * 4u;
-              ev[g][i][0] = __builtin_amdgcn_raw_buffer_load_b128(rtf, off, 0, 0);
-              ev[g][i][1] = __builtin_amdgcn_raw_buffer_load_b128(rtf, off + 16u, 0, 0);
+              ev[g][i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtf, off, 0, 0));
+              ev[g][i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtf, off + 16u, 0, 0));
             }
           }
         }
@@ -398,9 +401,9 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 #pragma unroll
               for (int u = 0; u < 2; ++u) {
                 const int ee = e + u;
-                const float e0 = __builtin_bit_cast(float, ev[g][0][ee >> 2][ee & 3]);
-                const float e1 = __builtin_bit_cast(float, ev[g][1][ee >> 2][ee & 3]);
-                const float e2 = __builtin_bit_cast(float, ev[g][2][ee >> 2][ee & 3]);
+                const float e0 = ev[g][0][ee >> 2][ee & 3];
+                const float e1 = ev[g][1][ee >> 2][ee & 3];
+                const float e2 = ev[g][2][ee >> 2][ee & 3];
                 const float v = fmaf(wv[g][2], e2, fmaf(wv[g][1], e1, wv[g][0] * e0));
                 x[u] = okv[g] ? v : 0.f;
               }

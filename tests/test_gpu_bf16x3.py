@@ -117,9 +117,12 @@ def test_train_step_rays_bf16x3_matches_oracle():
         np.testing.assert_allclose(pred.cpu().numpy(), p_ref, atol=1e-4)
         assert abs(plan.read_ctrl()["loss_sum"] / (3 * B) - loss) < 1e-5
     got = arena_to_dict(params, w, L, s)
-    # gradients agree to ~1e-5 of each tensor's max (test_backward_bf16x3_golden), so elements
-    # whose gradient is smaller than that may take Adam's opposite step (m / sqrt(v) = +-1 on
-    # step 1): seen 539 of layers.0.0.weight's 262,144 elements (0.2 %) moved by up to lr,
-    # every element within 2 lr steps
+    # unfiltered rays: chain3 X3's forward (three split-bf16 products, 2^-17 operand error)
+    # leaves pre-activations ~1e-6 off, and a 4096-ray batch holds ~66 rays within 1e-6 of a
+    # ReLU kink (test_chainf_unfiltered_rays_config_b), so a few units per step take the
+    # other side; one such flip moves layers.0.0.weight's gradient by up to 7.6e-3 of its
+    # max, and elements whose gradient is below ~1e-2 of the max then take a different Adam
+    # step (m / sqrt(v) ~ +-1 on step 1): measured 7,624 of its 262,144 elements (2.9 %)
+    # beyond 5e-6 (the fp32-forward chain: 539); every element within 2 lr steps
     for n in O.layer_names(L, s):
-        assert_adam_close(got[n], tr.w[n], lr=1e-4, steps=2, name=n, frac=5e-3)
+        assert_adam_close(got[n], tr.w[n], lr=1e-4, steps=2, name=n, frac=5e-2)

@@ -466,15 +466,20 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
 
 
 @pytest.mark.parametrize("name,B,apply_adam", [("B", 4096, True), ("B", 4096, False), ("B", 1024, True),
-                                               ("A", 4096, True), ("B", 8192, True)])
+                                               ("A", 4096, True), ("A", 4096, False), ("B", 8192, True)])
 def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
     """The default bf16 step fuses the update into the dW GEMM (lgemm.hip GT: split-K 1,
     64 x 64 tiles, each block runs Adam -- or writes the reduced gradient -- on its own tile
     from the LDS gradient tile).  Against the split-K slab path (INF_NO_LGF: lgemm into 2
     slabs, the separate update launch): the same chain, so the same loss sums bit for bit;
     the gradients differ only in the K-sum's order (split-K 2 partials vs one accumulator:
-    1e-6 of each tensor's max, seen ~1e-7) and the Adam steps follow (<= 0.1 % of the
-    elements by up to lr, assert_adam_close), over three steps."""
+    1e-6 of each tensor's max, seen ~1e-7) and the Adam steps follow, over three steps:
+    Adam moves every element by ~lr whatever its gradient's size, so an element whose
+    gradient cancels to |g| < sigma / 150 (sigma: the spread of a 4096-ray sum of random-sign
+    terms, ~64x below the sum of their magnitudes) carries a relative rounding difference
+    above 1e-7 * 64 * 150 = 1e-3 into its step -- a > 1e-6 move for ~0.5 % of the elements
+    (0.8 / 150 of a normal sum lands that close to zero; config A measured 32 of 8192).
+    So: <= 1 % of the elements beyond 1e-6, none beyond 2 lr per step."""
     rng = np.random.default_rng(15)
     k, H, L, s = CFG[name]
     V = 3000
@@ -502,7 +507,7 @@ def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
     assert out["lgf"][2][0] == out["slab"][2][0]  # the first step's chain: identical
     for n in O.layer_names(*CFG[name][2:]):
         if apply_adam:
-            assert_adam_close(out["lgf"][0][n], out["slab"][0][n], lr=1e-3, steps=3, name=n, atol=1e-6)
+            assert_adam_close(out["lgf"][0][n], out["slab"][0][n], lr=1e-3, steps=3, name=n, atol=1e-6, frac=1e-2)
         else:
             ref = out["slab"][1][n]
             err = float(np.abs(out["lgf"][1][n] - ref).max() / max(np.abs(ref).max(), 1e-12))

@@ -77,9 +77,9 @@ for mode, plan in plans.items():
 xa = plans["bf16"].debug_buffer(0)
 xb = plans["bf16x3"].debug_buffer(0)
 na = k * 0 + plans["bf16"].in_pad * B * 2
-A = xa[:na].view(torch.bfloat16).float()
-Bh = xb[:na].view(torch.bfloat16).float()
-Bl = xb[na:2 * na].view(torch.bfloat16).float()
+A = xa[:na].view(torch.bfloat16).float().cpu()
+Bh = xb[:na].view(torch.bfloat16).float().cpu()
+Bl = xb[na:2 * na].view(torch.bfloat16).float().cpu()
 print("X^T images: bf16 |max|", float(A.abs().max()), "x3 hi |max|", float(Bh.abs().max()), "x3 lo |max|",
       float(Bl.abs().max()), "max |bf16 - x3 hi|", float((A - Bh).abs().max()))
 
