@@ -236,9 +236,10 @@ class Trainer:
             g2 = gm = None
             if self.dp:
                 gm = self._capture_dp_steps(s)
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2, stream=s):
-                    self.plan.adam(0, 0.0, advance=True)
+                if self.shape not in ("bucketed", "sharded"):  # those step eagerly (step())
+                    g2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g2, stream=s):
+                        self.plan.adam(0, 0.0, advance=True)
             else:
                 # several steps per graph: one replay launch per GRAPH_STEPS steps (an even
                 # number: the pre-gather slots alternate)

@@ -435,8 +435,11 @@ __device__ __forceinline__ void matrix_items_pipelined(const AdamArgs& a, const 
 // split-K-1 block -- row m - m0 = input feature, column n - n0 = output feature, the column
 // XOR-swizzled by (row / 4) % 16); item it + 1's parameters and moments load while item it
 // is applied.  The arithmetic of matrix_tile (mt_apply): bitwise the update launch on the
-// same gradient.  Requires VEC4 rows.
-template <typename T, int NI>
+// same gradient.  An item with seg < 0 (the GEMM's column padding) is skipped.  VEC4:
+// 16-byte aligned arena rows (else element-wise, config R's k = 1023).  (Loading every
+// item's state ahead of the GEMM's main loop instead was measured slower: the dependent
+// item-table loads stall the block's operand prologue, +3 us, for -1.6 us at the tail.)
+template <typename T, int NI, bool VEC4>
 __device__ __forceinline__ void matrix_items_lds(const AdamArgs& a, const AdamSeg& seg, const AdamItem (&items)[NI],
                                                  Scalars& sc, float (*tile)[ADAM_TILE_R + 1], const float* cs,
                                                  int cld, int m0, int n0) {
@@ -466,11 +469,16 @@ __device__ __forceinline__ void matrix_items_lds(const AdamArgs& a, const AdamSe
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int gr = item.r0 + rb + 32 * i;
-      r.ok[i] = gr < seg.R && gc < seg.C;
+      r.ok[i] = item.seg >= 0 && gr < seg.R && gc < seg.C;
       r.e[i] = seg.off + (int64_t)(r.ok[i] ? gr : 0) * seg.C + (r.ok[i] ? gc : 0);
       auto ld = [&](const float* base, float (&dst)[4]) {
-        const float4 x = r.ok[i] ? *reinterpret_cast<const float4*>(base + r.e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[0] = x.x, dst[1] = x.y, dst[2] = x.z, dst[3] = x.w;
+        if constexpr (VEC4) {
+          const float4 x = r.ok[i] ? *reinterpret_cast<const float4*>(base + r.e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+          dst[0] = x.x, dst[1] = x.y, dst[2] = x.z, dst[3] = x.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dst[j] = (r.ok[i] && gc + j < seg.C) ? base[r.e[i] + j] : 0.f;
+        }
       };
       ld(a.params, r.w[i]);
       if (adam) {
@@ -485,6 +493,7 @@ __device__ __forceinline__ void matrix_items_lds(const AdamArgs& a, const AdamSe
   for (int it = 0; it < NI; ++it) {
     Regs& r = R[it & 1];
     if (it + 1 < NI) load(items[it + 1], R[(it + 1) & 1]);
+    if (items[it].seg < 0) continue;  // column padding of the GEMM (block-uniform)
     float g[NR][4];
     const int row0 = items[it].c0 + 4 * c4 - m0;  // input features row0 .. row0 + 3 of the tile
 #pragma unroll
@@ -494,7 +503,7 @@ __device__ __forceinline__ void matrix_items_lds(const AdamArgs& a, const AdamSe
       for (int j = 0; j < 4; ++j) g[i][j] = cs[(row0 + j) * cld + (col ^ ((row0 >> 2) & 15))];
     }
     lds_barrier();  // the previous item's transposed-image tile reads are done
-    mt_apply<T, true>(a, seg, items[it], sc, tile, r.ok, r.e, r.w, r.m, r.v, g);
+    mt_apply<T, VEC4>(a, seg, items[it], sc, tile, r.ok, r.e, r.w, r.m, r.v, g);
   }
 }
 

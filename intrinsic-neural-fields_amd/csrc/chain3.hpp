@@ -107,7 +107,10 @@ struct Chain3Args {
 // tables above this size are read with non-temporal row loads (chain3.hip, igemm.hip)
 constexpr size_t C3_NT_TABLE_BYTES = (size_t)256 << 20;
 constexpr int64_t CHAIN3_MAX_ROWS = 8192;
-constexpr int C3_NR_WIDE = 4;
+#ifndef C3_NR_WIDE_DEF  // experiments (variant libraries only)
+#define C3_NR_WIDE_DEF 4
+#endif
+constexpr int C3_NR_WIDE = C3_NR_WIDE_DEF;
 constexpr int64_t CHAIN3_WIDE_MAX_ROWS = (int64_t)1 << 24;
 // INF_CHAIN3_WIDE=1: wide tiles at any batch that is a multiple of 64 rays (tests compare
 // the two widths on one batch)
@@ -119,7 +122,10 @@ inline int chain3_bm(int64_t rows) { return chain3_wide(rows) ? 16 * C3_NR_WIDE 
 // Feature columns per LDS chunk when the whole 16 x k_pad tile does not fit (k_pad > C3_KC).
 constexpr int C3_KC = 1024;
 // ... and for the wide tiles, which always stream the feature tile in chunks
-constexpr int C3_KC_WIDE = 256;
+#ifndef C3_KC_WIDE_DEF
+#define C3_KC_WIDE_DEF 256
+#endif
+constexpr int C3_KC_WIDE = C3_KC_WIDE_DEF;
 // Weight-stream blocks of a training step: the input layers' k_pad / (32 upl) blocks each,
 // one per hidden layer forward and backward.
 inline int chain3_blocks(int H, int L, int k_pad) { return 2 * (k_pad / H) + 2 * (L - 2); }

@@ -262,9 +262,15 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
       const int r0 = n0 + (it / (BM / ADAM_TILE_C)) * ADAM_TILE_R, c0 = m0 + (it % (BM / ADAM_TILE_C)) * ADAM_TILE_C;
-      items[it] = batch.adam.items[seg.item0 + (r0 / ADAM_TILE_R) * ncol + c0 / ADAM_TILE_C];
+      // a tile of the GEMM's column padding (c_pad > C: config A's k = 64 under a 128-wide
+      // X^T) has no work item: seg -1, skipped
+      items[it] = (c0 < seg.C && r0 < seg.R) ? batch.adam.items[seg.item0 + (r0 / ADAM_TILE_R) * ncol + c0 / ADAM_TILE_C]
+                                             : AdamItem{-1, r0, c0, 0, 0, 0};
     }
-    adam_dev::matrix_items_lds<bf16, NI>(batch.adam, seg, items, asc, atile, Cs, CLD, m0, n0);
+    if (P.adam_vec4)
+      adam_dev::matrix_items_lds<bf16, NI, true>(batch.adam, seg, items, asc, atile, Cs, CLD, m0, n0);
+    else
+      adam_dev::matrix_items_lds<bf16, NI, false>(batch.adam, seg, items, asc, atile, Cs, CLD, m0, n0);
     if (stl != nullptr) stl[3] = wall_clock64();
     return;
   }
@@ -413,7 +419,7 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
                       p.b_row0 + p.N <= 16 * p.b_tiles, "lgemm: operand layout");
     INF_CHECK_ARG(p.splits == 1 || p.slab != nullptr, "lgemm: split-K needs a slab");
     INF_CHECK_ARG(p.slab != nullptr || p.C != nullptr || gt, "lgemm: no output");
-    INF_CHECK_ARG(!gt || (p.splits == 1 && p.adam_seg >= 0 && p.adam_vec4), "lgemm: gradient-tile update: split-K 1, 16-byte rows");
+    INF_CHECK_ARG(!gt || (p.splits == 1 && p.adam_seg >= 0), "lgemm: gradient-tile update: split-K 1");
     p.tiles_m = p.M / bm;
     p.tiles_n = p.N / bn;
     p.block_begin = blocks;

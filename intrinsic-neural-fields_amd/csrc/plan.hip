@@ -75,7 +75,7 @@ struct inf_plan {
   int last_part1 = -1;     // the last PART1 step: 1 bucketed, 0 reduced the whole gradient
   // bf16 chain3 steps fuse the update into the dW GEMM: split-K 1, 64 x 64 tiles, each block
   // applies Adam (or writes the gradient) to its own tile from the LDS gradient tile
-  // (lgemm.hip GT) -- no split-K slabs, no update launch (INF_NO_LGF=1: the slab path)
+  // (lgemm.hip GT) -- no split-K slabs, no update launch (config D; INF_LGF=0/1 forces it)
   bool lgf = false;
   bool last_lgf = false;  // the last training step took it
   int train_unit = 128;
@@ -258,10 +258,18 @@ int build_layout(inf_plan* p) {
   if (reg_dw && mb <= CHAIN3_MAX_ROWS && S > 4) S = 4;
   if (reg_dw && mb <= 4096 && S > 2) S = 2;
   // the fused gradient-tile update (lgemm.hip GT) of the bf16 chain3 step: split-K 1 over
-  // 64 x 64 tiles whose rows are 16-byte aligned in the arena
-  p->lgf = d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS && std::getenv("INF_NO_LGF") == nullptr;
+  // 64 x 64 tiles (arena rows element-wise where they are not 16-byte aligned: config R's
+  // k = 1023; tiles of the column padding c_pad > C skipped)
+  // Default only for the chunked-tile tables (k_pad > C3_KC, config D: dW + update 54.8 ->
+  // 47.5 us, step 145.4 -> 140.8 us).  At config B the 64 x 64 split-K-1 GEMM's longer main
+  // loop (15.2 us vs the 2-split 64 x 128 GEMM's whole 15.7) plus the per-block update tail
+  // (4-6 us) cost what the update launch did (stage 26.7 vs 15.7 + 8.5 us; step 69.4-70.3 vs
+  // 68.1-69.3), configs A / R lose 2-3 us (profiles/r04/lgf_sweep.log).  INF_LGF=0/1 forces it.
+  const char* lgf_env = std::getenv("INF_LGF");
+  p->lgf = d.mode == INF_MODE_BF16 && mb <= CHAIN3_MAX_ROWS &&
+           (lgf_env != nullptr ? std::atoi(lgf_env) != 0 : p->k_pad > C3_KC);
   for (const auto& g : p->segs)
-    if (g.gemm && (g.C % 4 != 0 || g.off % 4 != 0 || g.c_pad % 64 != 0 || g.R % 64 != 0)) p->lgf = false;
+    if (g.gemm && (g.c_pad % 64 != 0 || g.R % 64 != 0)) p->lgf = false;
   if (p->lgf) S = 1;
   // the 64-ray chain tiles' dW through lgemm (shapes fgemm does not tile) stream
   // K = Bp / S rays per block in 256-ray steps: 10,240 rays take 8 splits, not 16

@@ -431,12 +431,12 @@ def test_bf16_chain_render_matches_layered(monkeypatch):
 
 @pytest.mark.parametrize("apply_adam", [True, False])
 def test_fused_update_bitwise(apply_adam, monkeypatch):
-    """The split-K slab path (INF_NO_LGF): the update fused into the dW GEMM launch
+    """The split-K slab path (the default): the update fused into the dW GEMM launch
     (INF_FUSED_UPDATE: the last split-K block of each tile runs the update kernel's own
     matrix items on the sc1-published partials) leaves exactly the bytes of the separate
     update launch: parameters, Adam state (or the reduced gradients) and the step's loss
     sums, over three steps of 4096 rays."""
-    monkeypatch.setenv("INF_NO_LGF", "1")
+    monkeypatch.setenv("INF_LGF", "0")
     rng = np.random.default_rng(5)
     k, H, L, s = CFG["B"]
     V, B = 3000, 4096
@@ -466,20 +466,20 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
 
 
 @pytest.mark.parametrize("name,B,apply_adam", [("B", 4096, True), ("B", 4096, False), ("B", 1024, True),
-                                               ("A", 4096, True), ("A", 4096, False), ("B", 8192, True)])
+                                               ("A", 4096, True), ("A", 4096, False), ("R", 2048, True),
+                                               ("R", 2048, False), ("B", 8192, True)])
 def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
     """The default bf16 step fuses the update into the dW GEMM (lgemm.hip GT: split-K 1,
     64 x 64 tiles, each block runs Adam -- or writes the reduced gradient -- on its own tile
-    from the LDS gradient tile).  Against the split-K slab path (INF_NO_LGF: lgemm into 2
+    from the LDS gradient tile; opt-in, INF_LGF=1).  Against the split-K slab path (lgemm into 2
     slabs, the separate update launch): the same chain, so the same loss sums bit for bit;
-    the gradients differ only in the K-sum's order (split-K 2 partials vs one accumulator:
-    1e-6 of each tensor's max, seen ~1e-7) and the Adam steps follow, over three steps:
-    Adam moves every element by ~lr whatever its gradient's size, so an element whose
-    gradient cancels to |g| < sigma / 150 (sigma: the spread of a 4096-ray sum of random-sign
-    terms, ~64x below the sum of their magnitudes) carries a relative rounding difference
-    above 1e-7 * 64 * 150 = 1e-3 into its step -- a > 1e-6 move for ~0.5 % of the elements
-    (0.8 / 150 of a normal sum lands that close to zero; config A measured 32 of 8192).
-    So: <= 1 % of the elements beyond 1e-6, none beyond 2 lr per step."""
+    the gradients differ only in the K-sum's order (split-K 2-4 partials vs one accumulator:
+    1e-5 of each tensor's max, seen ~1e-7).  With Adam: ONE step, whose move is
+    lr g / (|g| + eps) -- +-lr whatever |g| -- so the two paths agree to rounding except where
+    a gradient at rounding level changes sign (<= 0.1 % of the elements, by <= 2 lr).  (Later
+    steps are not compared: the first step's rounding-level weight differences move
+    pre-activations near a ReLU kink to the other side in the next chain, and Adam turns
+    those one-ray gradient changes into +-lr moves of every small-gradient element.)"""
     rng = np.random.default_rng(15)
     k, H, L, s = CFG[name]
     V = 3000
@@ -490,13 +490,12 @@ def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
                          torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
     out = {}
     for tag in ("lgf", "slab"):
-        if tag == "slab":
-            monkeypatch.setenv("INF_NO_LGF", "1")
+        monkeypatch.setenv("INF_LGF", "1" if tag == "lgf" else "0")
         plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
         plan.set_lr(1e-3)
         b = plan.make_batch(source=src, batch=B)
         sums = []
-        for _ in range(3 if apply_adam else 1):
+        for _ in range(1):
             plan.train_step(b, None, apply_adam=apply_adam)
             assert plan.last_step_path() == "chain3"
             assert plan.last_step_fused_update() == (tag == "lgf")
@@ -507,7 +506,7 @@ def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
     assert out["lgf"][2][0] == out["slab"][2][0]  # the first step's chain: identical
     for n in O.layer_names(*CFG[name][2:]):
         if apply_adam:
-            assert_adam_close(out["lgf"][0][n], out["slab"][0][n], lr=1e-3, steps=3, name=n, atol=1e-6, frac=1e-2)
+            assert_adam_close(out["lgf"][0][n], out["slab"][0][n], lr=1e-3, steps=1, name=n, atol=1e-6, frac=1e-3)
         else:
             ref = out["slab"][1][n]
             err = float(np.abs(out["lgf"][1][n] - ref).max() / max(np.abs(ref).max(), 1e-12))

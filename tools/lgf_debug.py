@@ -1,5 +1,5 @@
 """Diagnostics for the fused dW + update (lgemm GT): one step without Adam, gradients of the
-LGF path vs the split-K slab path (INF_NO_LGF) per layer -- max error, where it sits."""
+LGF path vs the split-K slab path (the default; LGF is INF_LGF=1) per layer -- max error, where it sits."""
 import os
 import sys
 
@@ -22,17 +22,14 @@ for name, B in (("A", 4096), ("B", 8192), ("B", 4096), ("R", 4096)):
                          torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
     out = {}
     for tag in ("lgf", "slab"):
-        if tag == "slab":
-            os.environ["INF_NO_LGF"] = "1"
-        else:
-            os.environ.pop("INF_NO_LGF", None)
+        os.environ["INF_LGF"] = "1" if tag == "lgf" else "0"
         plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
         b = plan.make_batch(source=src, batch=B)
         plan.grads.fill_(float("nan"))
         plan.train_step(b, None, apply_adam=False)
         torch.cuda.synchronize()
         out[tag] = (arena_to_dict(plan.grads, w, L, s), plan.last_step_fused_update(), plan.dw_splits if hasattr(plan, "dw_splits") else None)
-    os.environ.pop("INF_NO_LGF", None)
+    os.environ.pop("INF_LGF", None)
     print(f"== {name} B={B} fused: lgf {out['lgf'][1]} slab {out['slab'][1]}")
     for n in O.layer_names(L, s):
         a, r = out["lgf"][0][n], out["slab"][0][n]
