@@ -950,6 +950,8 @@ int run_chain(inf_plan* p, const inf_batch* b, int Bp, bool train, float* pred, 
 // The large-batch dW GEMM (fgemm.hip) for this padded batch: 64-ray chain tiles and every
 // weight matrix a whole number of 256 x 256 tiles
 bool use_fgemm(const inf_plan* p, int Bp, int splits) {
+  // (the 16-ray chain's 4096-ray step on fgemm measured slower at every split count: 4 / 8 /
+  // 16 splits -> step 86.3 / 80.1 / 81.5 vs 68.7 us on lgemm, profiles/r04/fgemm_narrow_sweep.log)
   if (!chain3_wide(Bp) || std::getenv("INF_NO_FGEMM") != nullptr) return false;
   for (const ParamSeg& g : p->segs)
     if (g.gemm && !fgemm_shape_ok(g.c_pad, g.R, Bp, splits)) return false;
