@@ -580,6 +580,15 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
     const int el = tid & 63, w = tid >> 6;
     const int gi = item.c0 + el;
     const bool ok = gi < seg.C;
+    const int64_t e = seg.off + gi;
+    // wave 0's parameter and Adam state load with the partials (one round trip, not two)
+    const bool pre = w == 0 && ok && a.do_adam && a.grad_src != GRAD_NONE;
+    float pw = 0.f, pm = 0.f, pv = 0.f;
+    if (pre) {
+      pw = a.params[e];
+      pm = a.exp_avg[e];
+      pv = a.exp_avg_sq[e];
+    }
     float g = 0.f;
     if (a.grad_src == GRAD_SLABS) {
       const float* base = seg.slab + (ok ? gi : 0);
@@ -601,7 +610,6 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
     lds_barrier();
     if (w == 0 && ok) {
       g = ((vs[el] + vs[64 + el]) + vs[128 + el]) + vs[192 + el];
-      const int64_t e = seg.off + gi;
       if (a.grad_src == GRAD_FLAT) g = a.shard_mode == SHARD_ADAM ? a.gsh[item.goff - a.g_base + el] : a.grads[e];
       if (a.grad_src != GRAD_NONE) {
         if (a.write_grads) {
@@ -611,7 +619,7 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
             a.grads[e] = g;
         }
         if (a.do_adam) {
-          float pw = a.params[e], m = a.exp_avg[e], v = a.exp_avg_sq[e];
+          float m = pm, v = pv;
           adam_elem(pw, m, v, g, a, sc);
           a.params[e] = pw;
           a.exp_avg[e] = m;

@@ -200,7 +200,10 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     const int t0 = wc * TN;  // the wave's first 16-feature tile
     // fragment ring: D k-blocks (D * TN KiB per wave) in flight
     // X3: hi and lo fragments per k block, half the depth (the same bytes in flight)
-    constexpr int D0 = NR == 1 ? (X3 ? C3_DEPTH / 2 : C3_DEPTH) : C3_DEPTH_WIDE;
+#ifndef C3_X3_DEPTH
+#define C3_X3_DEPTH (C3_DEPTH / 2)
+#endif
+    constexpr int D0 = NR == 1 ? (X3 ? C3_X3_DEPTH : C3_DEPTH) : C3_DEPTH_WIDE;
     constexpr int D = D0 < UPL ? D0 : UPL;
     // every block starts at ring slot 0 (slot = k block % D)
     static_assert(UPL % D == 0, "the fragment ring depth must divide a block's k blocks");
