@@ -120,10 +120,15 @@ inline bool chain3_wide(int64_t rows) {
 }
 inline int chain3_bm(int64_t rows) { return chain3_wide(rows) ? 16 * C3_NR_WIDE : 16; }
 // Feature columns per LDS chunk when the whole 16 x k_pad tile does not fit (k_pad > C3_KC).
-constexpr int C3_KC = 1024;
+#ifndef C3_KC_DEF  // experiments (variant libraries only)
+#define C3_KC_DEF 1024
+#endif
+constexpr int C3_KC = C3_KC_DEF;
 // ... and for the wide tiles, which always stream the feature tile in chunks
+// (512: two chunk gathers per 1024-column tile instead of four, 64 KB of X beside the 64 KB
+// of activation tiles: 65,536 rays 569 -> 559 us, profiles/r04/large_b10_*.log)
 #ifndef C3_KC_WIDE_DEF
-#define C3_KC_WIDE_DEF 256
+#define C3_KC_WIDE_DEF 512
 #endif
 constexpr int C3_KC_WIDE = C3_KC_WIDE_DEF;
 // Weight-stream blocks of a training step: the input layers' k_pad / (32 upl) blocks each,
