@@ -633,6 +633,8 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
       lb.counters = p->W<int32_t>(p->o_counters);
     }
+    // (128 x 128 tiles measured slower at 2 and 4 splits: step 75.3 / 71.6 vs 68.1-69.9 us,
+    // profiles/r04/lgemm_tile_split_sweep.log; so were 4 splits of 64 x 128: 70.5-70.9)
     return launch_lgemm(lb, 64, st);
   }
   // weight gradients: one grouped split-K launch (chunks of GEMM_MAX_PROBLEMS)
