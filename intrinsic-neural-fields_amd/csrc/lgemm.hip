@@ -19,6 +19,12 @@
 // so the compiler's vmcnt waits are exact; the per-stage barrier is an LDS hand-off that
 // never drains vmcnt.
 //
+// KS = 2 (the weight-gradient slab path): two such 4-wave groups per block, each on every
+// other 64-deep stage of the block's K range, their accumulators added in LDS at the end
+// (group 0 + group 1) -- two waves per SIMD, so one wave's MFMAs cover the other's LDS
+// hand-off and barrier waits (a lone wave per SIMD spent its main loop at ~66 GB/s of
+// operands per CU, profiles/r04/lgemm_blocks_slab.log).
+//
 // Epilogues: bias + ReLU into row-major C (bf16 / f32) and a plain transposed copy
 // (input GEMM), or the transposed f32 tile into a split-K slab (weight gradients: the
 // block computes dW^T, the slab holds dW as the update kernel reads it).
@@ -46,12 +52,20 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef LG_RA
 #define LG_RA 4
 #endif
+// two k groups per block (KS = 2): each group keeps half the A stages in flight, so the
+// block's operand prologue is the one-group block's
+#ifndef LG_DEPTH2
+#define LG_DEPTH2 4
+#endif
+#ifndef LG_RA2
+#define LG_RA2 2
+#endif
 
-template <int BM, int NP = 1, int BN = LG_BN, bool GT = false>
+template <int BM, int NP = 1, int BN = LG_BN, bool GT = false, int KS = 1>
 struct LG {
   static constexpr int TM = BM / 16, TN = BN / 64;  // a wave owns BN / 4 columns
-  static constexpr int D = LG_DEPTH;  // B units in flight per wave (fragment register ring)
-  static constexpr int RA = LG_RA;  // A stages (64 deep) in flight in registers
+  static constexpr int D = KS == 2 ? LG_DEPTH2 : LG_DEPTH;  // B units in flight per wave (fragment register ring)
+  static constexpr int RA = KS == 2 ? LG_RA2 : LG_RA;  // A stages (64 deep) in flight in registers
   static_assert((2 * RA) % D == 0, "the B ring index must repeat every RA stages");
   static constexpr int ACH = BM * 8 / 256;  // 16-byte A chunks per thread per stage
   static constexpr int A_STAGE = BM * 128;  // bytes: BM rows x 64 bf16
@@ -61,8 +75,9 @@ struct LG {
   // NP operand parts (SPLIT: hi, lo) per stage
   static constexpr int CS_BYTES = BM * CLD * 4;
   static constexpr int ATILE_OFF = GT ? (CS_BYTES + 15) / 16 * 16 : 0;
+  // KS groups: their own A double buffers, and at the end their own accumulator tiles
   static constexpr int LDS =
-      std::max(std::max(2 * NP * A_STAGE, CS_BYTES), ATILE_OFF + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
+      std::max(std::max(KS * 2 * NP * A_STAGE, KS * CS_BYTES), ATILE_OFF + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4 + 64) + 16;
   static_assert(ACH >= 1 && BM * 8 % 256 == 0, "A stage must split over 256 threads");
 };
 
@@ -71,12 +86,13 @@ __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\
 // GT (FUSED with LgemmBatch::fused == 2): split-K 1, and each block runs the update items of
 // its own tile on the gradient tile in LDS (adam_dev::matrix_items_lds) -- no slab, no
 // separate update launch; BN 64 keeps 224 blocks at config B.
-template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false>
-__global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
+__global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch) {
   static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
   static_assert(!GT || FUSED, "the gradient-tile update is a fused mode");
+  static_assert(KS == 1 || (!FUSED && !SPLIT && !GT), "k-split groups: the plain slab / C epilogues only");
   constexpr int NP = SPLIT ? 2 : 1;
-  using C = LG<BM, NP, BN, GT>;
+  using C = LG<BM, NP, BN, GT, KS>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -109,15 +125,19 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   const int tn = local - tm * P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int tid = threadIdx.x;
+  const int tidb = threadIdx.x;  // thread of the block
+  const int grp = KS == 1 ? 0 : __builtin_amdgcn_readfirstlane(tidb >> 8);  // k group (KS = 2)
+  const int tid = tidb & 255;     // thread of the group
   const int lane = tid & 63;
   const int wc = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g4 = lane >> 4;
 
+  // group g takes the 64-deep stages g, g + KS, ...: its k blocks (units) 32-ray pairs
+  // 2 (KS j + g), + 1 for its stage j; k_begin / kb0 stay the block's
   const int kper = P.K / P.splits;  // multiple of 256
   const int k_begin = split * kper;
-  const int nst = kper / 64;        // A stages, multiple of 4
-  const int nun = kper / 32;        // units
+  const int nst = kper / 64 / KS;   // A stages of this group, a multiple of RA
+  const int nun = 2 * nst;          // units of this group
 
   // ---- A: buffer descriptor at this split's first k block; per-thread chunk offsets:
   // chunk q of a 64-deep stage = k block q / (TM 64), byte (q % (TM 64)) 16 of its TM tiles
@@ -146,31 +166,35 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   const int kb0 = k_begin >> 5;
 
   // (SPLIT: part p = 0 hi, 1 lo; a stage's LDS holds the hi tiles, then the lo tiles)
+  // (st, u: the group's own stage / unit numbers)
   auto loadA = [&](int st, u32x4 (&dst)[NP][ACH]) {
     st = min(st, nst - 1);  // past the end: reload the last stage (never stored)
+    const int gst = KS * st + grp;
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp)
 #pragma unroll
       for (int i = 0; i < ACH; ++i)
-        dst[pp][i] = __builtin_amdgcn_raw_buffer_load_b128(pp ? ral : ra, aoff[i], st * a_step, 0);
+        dst[pp][i] = __builtin_amdgcn_raw_buffer_load_b128(pp ? ral : ra, aoff[i], gst * a_step, 0);
   };
+  char* const agrp = smem + grp * 2 * NP * C::A_STAGE;  // the group's A double buffer
   auto storeA = [&](int buf, const u32x4 (&src)[NP][ACH]) {
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp)
 #pragma unroll
       for (int i = 0; i < ACH; ++i) {
         const int q = tid + 256 * i;
-        *reinterpret_cast<u32x4*>(smem + (buf * NP + pp) * C::A_STAGE + q * 16) = src[pp][i];
+        *reinterpret_cast<u32x4*>(agrp + (buf * NP + pp) * C::A_STAGE + q * 16) = src[pp][i];
       }
   };
   auto loadB = [&](int u, bf16x8 (&dst)[NP][TN]) {
     u = min(u, nun - 1);
+    const int gu = 2 * (KS * (u >> 1) + grp) + (u & 1);
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         dst[pp][j] = __builtin_bit_cast(
-            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(pp ? rbl : rb, boff + j * 1024, (kb0 + u) * bstep, 0));
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(pp ? rbl : rb, boff + j * 1024, (kb0 + gu) * bstep, 0));
   };
 
   f32x4 acc[TM][TN];
@@ -204,7 +228,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
       const int nxt = (ss + 1) % RA;  // compile-time after unrolling
       if (s + 1 < nst) storeA((s + 1) & 1, ar[nxt]);
       loadA(s + 1 + RA, ar[nxt]);
-      const char* As = smem + (s & 1) * NP * C::A_STAGE;
+      const char* As = agrp + (s & 1) * NP * C::A_STAGE;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int slot = (2 * ss + kk) % D;
@@ -238,9 +262,11 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   // column index is XOR-swizzled by row / 4 so those reads spread over the banks (they were
   // 8-way conflicts at CLD = 132; the writes stay conflict-free -- the XOR stays inside a
   // lane group's 16 columns).  The row-major C / CT epilogue reads rows as vectors: unswizzled
+  // KS = 2: each group writes its own tile, then tile 0 += tile 1 (fixed order)
   float* Cs = reinterpret_cast<float*>(smem);
   constexpr int CLD = C::CLD;
   const bool swz = P.slab != nullptr || GT;
+  float* Cg = Cs + grp * (C::CS_BYTES / 4);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -248,9 +274,20 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = i * 16 + g4 * 4 + r;
-        Cs[row * CLD + ((wc * (16 * TN) + j * 16 + r16) ^ (swz ? (row >> 2) & 15 : 0))] = acc[i][j][r];
+        Cg[row * CLD + ((wc * (16 * TN) + j * 16 + r16) ^ (swz ? (row >> 2) & 15 : 0))] = acc[i][j][r];
       }
   __syncthreads();
+  if constexpr (KS == 2) {
+    const float* C1 = Cs + C::CS_BYTES / 4;
+#pragma unroll 4
+    for (int q = tidb; q < BM * CLD / 4; q += 256 * KS) {
+      f32x4 a0 = reinterpret_cast<const f32x4*>(Cs)[q];
+      const f32x4 a1 = reinterpret_cast<const f32x4*>(C1)[q];
+      a0 += a1;
+      reinterpret_cast<f32x4*>(Cs)[q] = a0;
+    }
+    __syncthreads();
+  }
 
   if constexpr (GT) {
     // the tile's update items (the plan's own work items: shard offsets, flags) on the
@@ -282,7 +319,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
     constexpr int MQ = BM / 4;
 #pragma unroll 4
-    for (int q = tid; q < BN * MQ; q += 256) {
+    for (int q = tidb; q < BN * MQ; q += 256 * KS) {
       const int col = q / MQ, mq = q - col * MQ;
       const int cs = col ^ (mq & 15);  // rows mq 4 .. mq 4 + 3 share the swizzle
       const f32x4 v = {Cs[(mq * 4 + 0) * CLD + cs], Cs[(mq * 4 + 1) * CLD + cs], Cs[(mq * 4 + 2) * CLD + cs],
@@ -354,7 +391,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   }
   constexpr int NQ = BN / 4;
 #pragma unroll 4
-  for (int q = tid; q < BM * NQ; q += 256) {
+  for (int q = tidb; q < BM * NQ; q += 256 * KS) {
     const int row = q / NQ, c4 = q - row * NQ;
     const int m = m0 + row, n = n0 + c4 * 4;
     f32x4 v = *reinterpret_cast<const f32x4*>(Cs + row * CLD + c4 * 4);
@@ -377,7 +414,7 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   __syncthreads();
   constexpr int MQ = BM / 4;
 #pragma unroll 4
-  for (int q = tid; q < BN * MQ; q += 256) {
+  for (int q = tidb; q < BN * MQ; q += 256 * KS) {
     const int col = q / MQ, mq = q - col * MQ;
     const bf16x4 h = {(bf16)Cs[(mq * 4 + 0) * CLD + col], (bf16)Cs[(mq * 4 + 1) * CLD + col],
                       (bf16)Cs[(mq * 4 + 2) * CLD + col], (bf16)Cs[(mq * 4 + 3) * CLD + col]};
@@ -385,16 +422,17 @@ __global__ __launch_bounds__(256) void lgemm_kernel(const LgemmBatch batch) {
   }
 }
 
-template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false>
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
 int launch_typed(const LgemmBatch& b, hipStream_t stream) {
-  constexpr int lds = LG<BM, SPLIT ? 2 : 1, BN, GT>::LDS;
+  constexpr int lds = LG<BM, SPLIT ? 2 : 1, BN, GT, KS>::LDS;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
-  lgemm_kernel<BM, FUSED, SPLIT, BN, GT><<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256), lds, stream>>>(b);
+  lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS>
+      <<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256 * KS), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -442,6 +480,12 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
   if (b.split) return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
   if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
+  // the slab / C path: two k groups per block where every block's K range splits into an
+  // even number of 64-deep stages, each a multiple of RA (INF_LGEMM_KS=1: one group)
+  const char* eks = std::getenv("INF_LGEMM_KS");
+  bool ks2 = bm == 64 && (eks == nullptr || std::atoi(eks) != 1);
+  for (int i = 0; i < b.nprob && ks2; ++i) ks2 = (b.p[i].K / b.p[i].splits) % (64 * 2 * LG_RA2) == 0;
+  if (ks2) return launch_typed<64, false, false, LG_BN, false, 2>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }
 

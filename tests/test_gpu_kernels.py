@@ -435,8 +435,10 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
     (INF_FUSED_UPDATE: the last split-K block of each tile runs the update kernel's own
     matrix items on the sc1-published partials) leaves exactly the bytes of the separate
     update launch: parameters, Adam state (or the reduced gradients) and the step's loss
-    sums, over three steps of 4096 rays."""
+    sums, over three steps of 4096 rays.  (The fused launch keeps one k group per block, so
+    the separate path runs the same GEMM here: INF_LGEMM_KS=1.)"""
     monkeypatch.setenv("INF_LGF", "0")
+    monkeypatch.setenv("INF_LGEMM_KS", "1")
     rng = np.random.default_rng(5)
     k, H, L, s = CFG["B"]
     V, B = 3000, 4096
@@ -463,6 +465,38 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
     for a_, b_ in zip(out["separate"][:4], out["fused"][:4]):
         assert np.array_equal(a_, b_)
     assert out["separate"][4] == out["fused"][4]
+
+
+@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
+def test_lgemm_k_groups_match_one_group(name, B, monkeypatch):
+    """The dW GEMM's two k groups per block (lgemm.hip KS = 2, the default where a block's K
+    range splits into whole 512-ray rounds) against one group (INF_LGEMM_KS=1): the same
+    products summed as two interleaved halves then added, so every gradient within 1e-5 of
+    its tensor's max (fp32 reassociation over <= 2048 rays), and the chain's loss sums equal."""
+    monkeypatch.setenv("INF_LGF", "0")
+    rng = np.random.default_rng(23)
+    k, H, L, s = CFG[name]
+    V = 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (B, 3))).cuda(),
+                         torch.from_numpy(rng.dirichlet([1, 1, 1], B).astype(np.float32)).cuda(),
+                         torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
+    out = {}
+    for ks in ("2", "1"):
+        monkeypatch.setenv("INF_LGEMM_KS", ks)
+        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+        b = plan.make_batch(source=src, batch=B)
+        plan.train_step(b, None, apply_adam=False)
+        assert plan.last_step_path() == "chain3"
+        c = plan.read_ctrl()
+        torch.cuda.synchronize()
+        out[ks] = (arena_to_dict(plan.grads, w, L, s), (c["loss_sum"], c["sse_sum"]))
+    assert out["2"][1] == out["1"][1]
+    for n in O.layer_names(L, s):
+        ref = out["1"][0][n]
+        err = float(np.abs(out["2"][0][n] - ref).max() / max(np.abs(ref).max(), 1e-12))
+        assert err < 1e-5, (n, err)
 
 
 @pytest.mark.parametrize("name,B,apply_adam", [("B", 4096, True), ("B", 4096, False), ("B", 1024, True),
