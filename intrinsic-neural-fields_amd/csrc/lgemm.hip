@@ -90,7 +90,7 @@ template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = fals
 __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch) {
   static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
   static_assert(!GT || FUSED, "the gradient-tile update is a fused mode");
-  static_assert(KS == 1 || (!FUSED && !SPLIT && !GT), "k-split groups: the plain slab / C epilogues only");
+  static_assert(KS == 1 || (!FUSED && !GT), "k-split groups: the plain slab / C epilogues only");
   constexpr int NP = SPLIT ? 2 : 1;
   using C = LG<BM, NP, BN, GT, KS>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
@@ -478,13 +478,16 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: fused update reduces the slabs");
   }
   INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
-  if (b.split) return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
-  if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
-  // the slab / C path: two k groups per block where every block's K range splits into an
+  // the slab / C paths: two k groups per block where every block's K range splits into an
   // even number of 64-deep stages, each a multiple of RA (INF_LGEMM_KS=1: one group)
   const char* eks = std::getenv("INF_LGEMM_KS");
-  bool ks2 = bm == 64 && (eks == nullptr || std::atoi(eks) != 1);
+  bool ks2 = bm == 64 && !b.fused && (eks == nullptr || std::atoi(eks) != 1);
   for (int i = 0; i < b.nprob && ks2; ++i) ks2 = (b.p[i].K / b.p[i].splits) % (64 * 2 * LG_RA2) == 0;
+  if (b.split) {
+    if (ks2) return launch_typed<64, false, true, LG_BN, false, 2>(b, stream);
+    return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
+  }
+  if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
   if (ks2) return launch_typed<64, false, false, LG_BN, false, 2>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }
