@@ -336,7 +336,8 @@ int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
  * (csrc/chain3.hip), 4 the same with the feature tile streamed in chunks (k_pad > 1024),
  * 5 the same in 64-ray tiles (batches above 8192 rays), 6 the fused fp32 chain of the
  * fp32 mode (csrc/chainf.hip), 7 the split-bf16 register chain of the bf16x3 mode
- * (csrc/chain3.hip X3); -1 before any step. */
+ * (csrc/chain3.hip X3), 8 the large-batch layer GEMMs (csrc/layer.hip, opt-in
+ * INF_BIG_LAYERED=1); -1 before any step. */
 int inf_plan_last_step_path(const inf_plan* plan);
 
 /* Weight generation: a counter of the launches issued through this plan that may have

@@ -22,6 +22,7 @@
 #include "head.hpp"
 #include "fgemm.hpp"
 #include "igemm.hpp"
+#include "layer.hpp"
 #include "lgemm.hpp"
 #include "rchain.hpp"
 #include "blaslt.hpp"
@@ -54,6 +55,7 @@ constexpr int64_t ALIGN = 256;
 // inf_plan::last_chain of a step on the fused fp32 chain (chainf.hip)
 constexpr int CHAIN_F32 = 6;
 constexpr int CHAIN_X3 = 7;  // the split-bf16 register chain (chain3.hip X3) of the bf16x3 mode
+constexpr int CHAIN_BIG = 8;  // the large-batch layer GEMMs (layer.hip, INF_BIG_LAYERED=1)
 
 }  // namespace
 }  // namespace inf
@@ -741,7 +743,7 @@ int ensure_rowmajor(inf_plan* p, hipStream_t st) {
 // fused chain3 steps in bf16 leave the row-major shadows to ensure_rowmajor
 // (INF_EAGER_SHADOWS=1: every update rewrites all shadows)
 int step_shadow_mode(const inf_plan* p, int chain) {
-  return ((chain == 3 && p->mode == INF_MODE_BF16) || ((chain == CHAIN_F32 || chain == CHAIN_X3) && p->mode != INF_MODE_BF16)) &&
+  return (((chain == 3 || chain == CHAIN_BIG) && p->mode == INF_MODE_BF16) || ((chain == CHAIN_F32 || chain == CHAIN_X3) && p->mode != INF_MODE_BF16)) &&
                  std::getenv("INF_EAGER_SHADOWS") == nullptr
              ? 2
              : 1;
@@ -759,6 +761,7 @@ std::vector<AdamSeg> bucket_segs(const inf_plan* p) {
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
   const int parts = chain == 3 ? Bp / chain3_bm(Bp)
+                    : chain == CHAIN_BIG ? Bp / LY_RAYS
                     : (chain == CHAIN_F32 || chain == CHAIN_X3) ? Bp / 16
                     : chain ? Bp / chain_partial_rows(chain_bm(Bp))
                             : Bp / 64;
@@ -1149,6 +1152,121 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
 // Y^T / dZ^T images it writes.  16-ray tiles, k_pad <= 1024, batches lgemm's split-K tiles
 // (Bp / dw_splits a multiple of 256); smaller batches take the layered split-bf16 kernels.
 // INF_NO_CHAIN3X3=1: the layered kernels.
+// Large batches as layer GEMMs with fused epilogues (layer.hip; opt-in INF_BIG_LAYERED=1):
+// the bf16 eigenfunction-table step of H = 256 MLPs on the 64-ray-tile batches (the dW on
+// fgemm, the update as the fused chain's).
+bool use_big(const inf_plan* p, const inf_batch* b, int Bp) {
+  const char* e = std::getenv("INF_BIG_LAYERED");
+  if (e == nullptr || std::atoi(e) == 0) return false;
+  return p->mode == INF_MODE_BF16 && b->encoding == INF_ENC_NONE && b->table != nullptr &&
+         b->table_dtype == INF_DTYPE_BF16 && b->vids != nullptr && layer_supported(p->H, Bp) && chain3_wide(Bp) &&
+         p->k_pad % LY_KC == 0 && b->num_vertices * (int64_t)p->k_pad * 2 < ((int64_t)1 << 32) &&
+         use_fgemm(p, Bp, p->dw_splits) && p->L - 1 <= CHAIN_MAX_HIDDEN;
+}
+
+int run_big(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
+  const int H = p->H, L = p->L, s = p->s;
+  int rc;
+  // the gather: X (B-operand image) and X^T (the dW's fragment image)
+  XGatherArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.table = reinterpret_cast<const bf16*>(b->table);
+  g.num_vertices = b->num_vertices;
+  g.k_pad = p->k_pad;
+  g.vids = b->vids;
+  g.vid_dtype = b->vid_dtype;
+  g.bary = b->bary;
+  g.ray_idx = b->ray_idx;
+  g.idx_dtype = b->idx_dtype;
+  g.idx_offset = b->idx_offset;
+  g.num_rays = b->num_rays;
+  g.num_src = b->num_source_rays;
+  g.ctrl = p->ctrl;
+  g.offset_from_ctrl = b->offset_from_ctrl;
+  g.batch = b->batch;
+  g.rows = Bp;
+  g.gather_nt = (size_t)b->num_vertices * (size_t)p->k_pad * 2 > C3_NT_TABLE_BYTES;
+  g.X = p->W<bf16>(p->o_x0);
+  g.XT = p->W<bf16>(p->o_x0t);
+  if ((rc = launch_xgather(g, st))) return rc;
+  auto img = [&](const ParamSeg* w, bool fwd) -> const bf16* {
+    const int64_t off = fwd ? w->f_off : w->ft_off;
+    return off >= 0 ? reinterpret_cast<const bf16*>(p->shadow + off) : nullptr;
+  };
+  auto base = [&]() {
+    LayerArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.rows = Bp;
+    a.H = H;
+    return a;
+  };
+  // forward: layer 0 over X, hidden layers over Y_{l-1} (the skip layer also over X), the
+  // last hidden layer with the head, loss and head backward fused
+  for (int l = 0; l <= L - 2; ++l) {
+    LayerArgs a = base();
+    a.mode = l == L - 2 ? LY_MODE_HEAD : LY_MODE_FWD;
+    a.nsrc = 1;
+    a.in[0] = l == 0 ? g.X : p->W<bf16>(p->o_y[l - 1]);
+    a.kin[0] = l == 0 ? p->k_pad : H;
+    a.w[0] = img(p->weight_seg(l, 0), true);
+    a.bias0 = p->params + p->bias_seg(l, 0)->off;
+    if (l == s && l > 0) {
+      a.nsrc = 2;
+      a.in[1] = g.X;
+      a.kin[1] = p->k_pad;
+      a.w[1] = img(p->weight_seg(s, 1), true);
+      a.bias1 = p->params + p->bias_seg(s, 1)->off;
+    }
+    INF_CHECK_ARG(a.w[0] != nullptr && (a.nsrc == 1 || a.w[1] != nullptr), "layered step: fragment image missing");
+    if (a.mode == LY_MODE_FWD) {
+      a.out = p->W<bf16>(p->o_y[l]);
+      a.outT = p->W<bf16>(p->o_yt[l]);
+    } else {
+      a.out = p->W<bf16>(p->o_dZ[L - 2]);
+      a.outT = p->W<bf16>(p->o_dZT[L - 2]);
+      a.colsum = p->W<float>(p->o_colsum[L - 2]);
+      a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
+      a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
+      a.hw_part = p->W<float>(p->o_hw);
+      a.hb_part = p->W<float>(p->o_hb);
+      a.loss_part = p->W<double>(p->o_loss);
+      a.pred = pred;
+      INF_CHECK_ARG(b->rgb != nullptr, "training batch without target colours");
+      a.rgb = b->rgb;
+      a.ray_idx = b->ray_idx;
+      a.idx_dtype = b->idx_dtype;
+      a.idx_offset = b->idx_offset;
+      a.num_rays = b->num_rays;
+      a.num_src = b->num_source_rays;
+      a.offset_from_ctrl = b->offset_from_ctrl;
+      a.batch = b->batch;
+      a.loss = b->loss >= 0 ? b->loss : p->d.loss;
+      INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
+      const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
+      a.inv_count = (float)(1.0 / (double)cnt);
+      a.ctrl = p->ctrl;
+      a.count_step = 1;
+    }
+    if ((rc = launch_layer(a, st))) return rc;
+  }
+  // dX: dZ_{l-1} = (W_l^T dZ_l) * (Y_{l-1} > 0), l = L-2 .. 1 (the skip layer through Lx)
+  for (int l = L - 2; l >= 1; --l) {
+    LayerArgs a = base();
+    a.mode = LY_MODE_BWD;
+    a.nsrc = 1;
+    a.in[0] = p->W<bf16>(p->o_dZ[l]);
+    a.kin[0] = H;
+    a.w[0] = img(p->weight_seg(l, 0), false);
+    INF_CHECK_ARG(a.w[0] != nullptr, "layered step: transposed fragment image missing");
+    a.mask_in = p->W<bf16>(p->o_y[l - 1]);
+    a.out = p->W<bf16>(p->o_dZ[l - 1]);
+    a.outT = p->W<bf16>(p->o_dZT[l - 1]);
+    a.colsum = p->W<float>(p->o_colsum[l - 1]);
+    if ((rc = launch_layer(a, st))) return rc;
+  }
+  return INF_OK;
+}
+
 bool use_chain3x3(const inf_plan* p, const inf_batch* b, int Bp) {
   if (p->mode != INF_MODE_BF16X3 || p->k_pad > C3_KC || chain3_wide(Bp) ||
       !chain3_supported(p->H, p->L, p->k_pad, Bp) || !chain3_x3_lds_fits(p->H, p->L, p->k_pad))
@@ -1694,7 +1812,17 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
     return a;
   };
-  if (use_chain3(p, batch, Bp3)) {
+  if (!bucketed && !shard && xslot < 0 && use_big(p, batch, Bp3)) {
+    // large batch as layer GEMMs (layer.hip) -> the 64-ray tiles' dW GEMM (-> update below)
+    const int Bp = Bp3;
+    if ((rc = run_big(p, batch, Bp, pred, st))) return rc;
+    if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
+    p->saved = false;
+    p->saved_batch = batch->batch;
+    p->saved_bp = Bp;
+    ck = CHAIN_BIG;
+    nloss = Bp / LY_RAYS;
+  } else if (use_chain3(p, batch, Bp3)) {
     // fused gather + chain -> dW GEMM (-> update below).  INF_FUSED_UPDATE=1: the update
     // runs inside the dW launch instead (each tile's last split-K block applies Adam to
     // it, the first blocks do the biases and the end-of-step sums; bitwise the same) --
@@ -2106,7 +2234,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
           }
         break;
       }
-      rc = run_weight_grads(p, Bp, st, p->last_chain);
+      rc = run_weight_grads(p, Bp, st, p->last_chain == CHAIN_BIG ? 3 : p->last_chain);
       for (const auto& g : p->segs)
         if (g.gemm) {
           f += 2.0 * g.R * g.C * B;
@@ -2115,7 +2243,8 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
       break;
     }
     case INF_STAGE_CHAIN: {
-      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr && (use_chain(p) || p->last_chain == CHAIN_F32 || p->last_chain == CHAIN_X3),
+      INF_CHECK_ARG(b != nullptr && b->rgb != nullptr &&
+                        (use_chain(p) || p->last_chain == CHAIN_F32 || p->last_chain == CHAIN_X3 || p->last_chain == CHAIN_BIG),
                     "chain stage needs a fused training batch");
       // replay on the saved inputs; the step counter it advances is restored by the caller
       const double Lh = p->L;
@@ -2133,6 +2262,10 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
         // hi / lo bf16 weight images streamed per workgroup; fp32 rows in; hi / lo images out
         by = (double)(Bp / 16) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * 4.0 +
              B * (3.0 * p->k_pad * 4.0 + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * 4.0;
+      } else if (p->last_chain == CHAIN_BIG) {
+        rc = run_big(p, b, Bp, nullptr, st);
+        f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
+        by = B * (3.0 * p->k_pad * e + 24.0) + B * (2.0 * p->k_pad + 4.0 * (2.0 * Lh - 3) * H) * e;
       } else if (p->last_chain == 3) {
         rc = run_chain3(p, b, Bp, nullptr, st);
         f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);

@@ -588,15 +588,20 @@ def test_dp_step_shape_bitwise_equals_fused_step():
         assert f[5] == d[5]
 
 
-@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("A", 4096), ("R", 2048), ("B", 65536)])
-def test_bf16_chain3_matches_bf16_oracle(name, B):
+@pytest.mark.parametrize("name,B,big", [("B", 4096, False), ("B", 1024, False), ("A", 4096, False), ("R", 2048, False),
+                                        ("B", 65536, False), ("B", 65536, True), ("B", 16384, True)])
+def test_bf16_chain3_matches_bf16_oracle(name, B, big, monkeypatch):
     """The fused bf16 step (csrc/chain3.hip + lgemm.hip) against an independent restatement
     of the bf16 mode's arithmetic (oracle.inf_oracle.mlp_forward_bf16 / mlp_backward_bf16:
     bf16 weights and activations, fp32 accumulation, the rounding points of the chain's
     epilogues) -- not against the builder's own layered bf16 kernels.  What is left is the
     fp32 summation order, which can flip a bf16 rounding now and then.  65,536 rays is the
     bench's large-batch line: chain3's 64-ray tiles (the feature tile streamed in 256-column
-    chunks, W_y x a separate fp32 sum) and the 256 x 256-tile dW GEMM (fgemm.hip)."""
+    chunks, W_y x a separate fp32 sum) and the 256 x 256-tile dW GEMM (fgemm.hip).  big: the
+    same batch on the layer GEMMs (layer.hip, INF_BIG_LAYERED=1): 128-ray workgroups, the skip
+    layer's two sources in one accumulator, the head fused into the last layer's epilogue."""
+    if big:
+        monkeypatch.setenv("INF_BIG_LAYERED", "1")
     rng = np.random.default_rng(77)
     k, H, L, s = CFG[name]
     w0 = weights(golden(f"g2_forward_{name}.npz"))
@@ -611,8 +616,10 @@ def test_bf16_chain3_matches_bf16_oracle(name, B):
     plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
     pred = torch.empty((B, 3), device="cuda")
     plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
-    assert plan.last_step_path() == ("chain3_wide" if B > 8192 else "chain3"), plan.last_step_path()
+    assert plan.last_step_path() == ("layer_big" if big else "chain3_wide" if B > 8192 else "chain3"), plan.last_step_path()
     c = plan.read_ctrl()
+    if big:
+        assert c["step"] == 1  # the head workgroup counts the step, as chain3's store wave does
     p = pred.cpu().numpy()
     g = arena_to_dict(plan.grads, w, L, s)
     p_ref, cache = O.mlp_forward_bf16(w0, O.gather_bf16(E, vids, bary), L, s)
