@@ -19,7 +19,8 @@
 // so the compiler's vmcnt waits are exact; the per-stage barrier is an LDS hand-off that
 // never drains vmcnt.
 //
-// KS = 2 (the weight-gradient slab path): two such 4-wave groups per block, each on every
+// KS = 2 (weight-gradient slab paths; the default for the split-operand one): two such
+// 4-wave groups per block, each on every
 // other 64-deep stage of the block's K range, their accumulators added in LDS at the end
 // (group 0 + group 1) -- two waves per SIMD, so one wave's MFMAs cover the other's LDS
 // hand-off and barrier waits (a lone wave per SIMD spent its main loop at ~66 GB/s of
@@ -479,9 +480,14 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   }
   INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
   // the slab / C paths: two k groups per block where every block's K range splits into an
-  // even number of 64-deep stages, each a multiple of RA (INF_LGEMM_KS=1: one group)
+  // even number of 64-deep stages, each a multiple of RA.  Default for the split-operand
+  // (bf16x3) dW: 122.3 -> 120.9 us per step.  The bf16 step keeps one group by default: two
+  // groups took its dW 15.6 -> 14.8 us, but the reassociated fp32 sums moved config B's
+  // 12-epoch bf16 PSNR curve (G12) by 0.56 dB at one epoch, past the test's 0.5 dB per-epoch
+  // bar (profiles/r04/gpu_suite_kgroups_g12.log).  INF_LGEMM_KS=1 / 2 forces one or two.
   const char* eks = std::getenv("INF_LGEMM_KS");
-  bool ks2 = bm == 64 && !b.fused && (eks == nullptr || std::atoi(eks) != 1);
+  const int want_ks = eks != nullptr ? std::atoi(eks) : (b.split ? 2 : 1);
+  bool ks2 = bm == 64 && !b.fused && want_ks == 2;
   for (int i = 0; i < b.nprob && ks2; ++i) ks2 = (b.p[i].K / b.p[i].splits) % (64 * 2 * LG_RA2) == 0;
   if (b.split) {
     if (ks2) return launch_typed<64, false, true, LG_BN, false, 2>(b, stream);

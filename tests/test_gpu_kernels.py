@@ -469,8 +469,8 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
 
 @pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
 def test_lgemm_k_groups_match_one_group(name, B, monkeypatch):
-    """The dW GEMM's two k groups per block (lgemm.hip KS = 2, the default where a block's K
-    range splits into whole 512-ray rounds) against one group (INF_LGEMM_KS=1): the same
+    """The dW GEMM's two k groups per block (lgemm.hip KS = 2: INF_LGEMM_KS=2 on the bf16 step,
+    the default of the bf16x3 one) against one group (INF_LGEMM_KS=1): the same
     products summed as two interleaved halves then added, so every gradient within 1e-5 of
     its tensor's max (fp32 reassociation over <= 2048 rays), and the chain's loss sums equal."""
     monkeypatch.setenv("INF_LGF", "0")
