@@ -3,6 +3,7 @@ wave 0 of the first and the last workgroup, plus the stage's HIP-event time.
 
     python tools/chain3_timing.py [batch] [k] [hidden] [layers] [skip]
     C3T_RFF=1: the input is the RFF encoding (k = 2 * k_rff + 3) of interpolated positions
+    C3T_MODE=bf16x3: the split-bf16 chain (chain3.hip X3) instead of the bf16 one
 """
 import ctypes
 import os
@@ -20,7 +21,7 @@ B, k, H, L, s = [int(x) for x in (sys.argv[1:] + ["4096", "1024", "256", "8", "4
 rng = np.random.default_rng(0)
 P = H * k + H + (L - 3) * (H * H + H) + (H * H + H + H * k + H) + 3 * H + 3
 params = torch.from_numpy((rng.standard_normal(P) * 0.03).astype(np.float32)).cuda()
-plan = runtime.Plan(k, H, L, s, "bf16", "L2", B, params, grads=torch.zeros_like(params),
+plan = runtime.Plan(k, H, L, s, os.environ.get("C3T_MODE", "bf16"), "L2", B, params, grads=torch.zeros_like(params),
                     exp_avg=torch.zeros_like(params), exp_avg_sq=torch.zeros_like(params))
 V, N = 50000, B
 if os.environ.get("C3T_RFF"):
