@@ -292,7 +292,41 @@ class Trainer:
                 n -= 1
 
 
-def time_steps(tr, steps, warmup, world):
+# The GPU raises its clocks over the first ~25 ms of sustained load: from a cold start the
+# headline step replays at ~70 us for ~6 ms and settles at ~65 us after ~27 ms (the 65,536-ray
+# step: ~540 -> ~479 us after ~40 ms; tools/step_ramp.py, profiles/r04/step_ramp_*.log).  A
+# short window (the driver's 5 warmup + 20 timed steps span 1.7 ms) would time that ramp, not
+# the sustained rate a training run sees, so every timed leg first replays its own step,
+# untimed, for SETTLE_MS of GPU time -- the count is reported in the line (clock_settle).
+SETTLE_MS = float(os.environ.get("INF_BENCH_SETTLE_MS", "60"))
+SETTLED = {}
+
+
+def settle(tr, world, tag=None):
+    """Untimed replays of `tr`'s step for about SETTLE_MS ms (a probe of 8 steps sizes it;
+    ranks agree on the count, since data-parallel replays carry collectives)."""
+    if SETTLE_MS <= 0:
+        return 0
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    tr.run(8)
+    e1.record()
+    torch.cuda.synchronize()
+    per = max(e0.elapsed_time(e1) / 8, 1e-3)
+    n = min(int(SETTLE_MS / per) + 1, 100000)
+    if world > 1:
+        t = torch.tensor([n], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        n = int(t[0])
+    tr.run(n)
+    if tag is not None:
+        SETTLED[tag] = n + 8
+    return n + 8
+
+
+def time_steps(tr, steps, warmup, world, tag=None):
+    settle(tr, world, tag)
     tr.run(warmup)
     if world > 1:
         torch.distributed.barrier()
@@ -922,6 +956,7 @@ def main():
 
     dp_mode = world > 1 or bool(os.environ.get("INF_BENCH_DP"))
     dp_shapes = None
+    chosen = None
     if dp_mode:
         # the data-parallel step in each of its shapes (dp.py picks the fastest the same way),
         # and the gradient all-reduce alone; `value` is the fastest shape's
@@ -930,7 +965,7 @@ def main():
         for shape in [x for x in os.environ.get("INF_DP_SHAPES", "serial,prefetch,bucketed,sharded").split(",") if x]:
             tr = Trainer(args, device, args.batch, rank, world, shape=shape)
             tr.capture()
-            ms_s, wall_s = time_steps(tr, args.steps, args.warmup, world)
+            ms_s, wall_s = time_steps(tr, args.steps, args.warmup, world, tag="dp_" + shape)
             tr.gather_state()
             dp_shapes[shape] = {"ms_per_step": ms_s, "value": world * args.batch / (ms_s * 1e-3),
                                 "allreduce_in_graph": tr.ar_in_graph, "prefetch_active": bool(tr.prefetch)}
@@ -974,7 +1009,7 @@ def main():
     else:
         tr = Trainer(args, device, args.batch, rank, world)
         tr.capture()
-        ms, wall_ms = time_steps(tr, args.steps, args.warmup, world)
+        ms, wall_ms = time_steps(tr, args.steps, args.warmup, world, tag="headline")
     tr_ar_in_graph = tr.ar_in_graph
     value = world * args.batch / (ms * 1e-3)
 
@@ -1110,6 +1145,10 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "clock_settle": {"ms": SETTLE_MS, "steps": SETTLED.get("headline", SETTLED.get("dp_" + str(chosen))),
+                             "note": "untimed replays of the same step before the W warmup steps: the GPU's "
+                                     "clocks ramp over ~25 ms of load (tools/step_ramp.py); "
+                                     "INF_BENCH_SETTLE_MS=0 disables"},
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "weak",
