@@ -541,8 +541,10 @@ __device__ inline void finish_step(const AdamArgs& a) {
 
 // One work item (adam.hpp AdamItem) on 256 threads: a matrix tile, a vector chunk or the
 // end-of-step item.  `tile` and `sc` are the caller's LDS.
-// VT: vector-partial loads in flight per thread; PB, SC1: matrix_tile
-template <typename T, int VT = 64, int PB = 8, bool SC1 = false>
+// VT: vector-partial loads in flight per thread; PB, SC1: matrix_tile; VEC_ONLY: the caller
+// runs vector / end-of-step items only (the dW GEMM's leading blocks, lgemm.hip AUX): the
+// matrix path is not compiled into it
+template <typename T, int VT = 64, int PB = 8, bool SC1 = false, bool VEC_ONLY = false>
 __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& item, float (*tile)[ADAM_TILE_R + 1],
                                             Scalars& sc) {
   if (item.seg < 0) {
@@ -569,10 +571,12 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
   if (a.do_adam) lds_barrier();
 
   if (seg.matrix) {
-    if (item.pad & ITEM_VEC4)
-      matrix_tile<T, true, PB, SC1>(a, seg, item, sc, tile);
-    else
-      matrix_tile<T, false, PB, SC1>(a, seg, item, sc, tile);
+    if constexpr (!VEC_ONLY) {
+      if (item.pad & ITEM_VEC4)
+        matrix_tile<T, true, PB, SC1>(a, seg, item, sc, tile);
+      else
+        matrix_tile<T, false, PB, SC1>(a, seg, item, sc, tile);
+    }
   } else {
     // vector chunk: ADAM_VEC (64) consecutive elements; wave w sums the partials w, w + 4,
     // ... (one coalesced 256-byte load per partial, up to 64 in flight: one round trip for

@@ -87,11 +87,14 @@ __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\
 // GT (FUSED with LgemmBatch::fused == 2): split-K 1, and each block runs the update items of
 // its own tile on the gradient tile in LDS (adam_dev::matrix_items_lds) -- no slab, no
 // separate update launch; BN 64 keeps 224 blocks at config B.
-template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
+// AUX (LgemmBatch::aux_only): the first n_aux blocks run the update's vector / end-of-step
+// items, the rest the plain slab GEMM (the matrix items follow in the update launch).
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1, bool AUX = false>
 __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch) {
   static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
   static_assert(!GT || FUSED, "the gradient-tile update is a fused mode");
   static_assert(KS == 1 || (!FUSED && !GT), "k-split groups: the plain slab / C epilogues only");
+  static_assert(!AUX || (!FUSED && !SPLIT), "vector items beside the plain bf16 slab GEMM");
   constexpr int NP = SPLIT ? 2 : 1;
   using C = LG<BM, NP, BN, GT, KS>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
@@ -101,12 +104,19 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
   float(*const atile)[ADAM_TILE_R + 1] = reinterpret_cast<float(*)[ADAM_TILE_R + 1]>(smem + C::ATILE_OFF);
   adam_dev::Scalars& asc =
       *reinterpret_cast<adam_dev::Scalars*>(smem + C::ATILE_OFF + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4);
-  if (FUSED && (int)blockIdx.x < batch.n_aux) {
-    if ((int)blockIdx.x < batch.n_aux_items)
-      adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
-    return;
+  if constexpr (FUSED || AUX) {
+    if ((int)blockIdx.x < batch.n_aux) {
+      // (the update kernel's vector sum order either way: partial w, w + 4, ... per wave)
+      if ((int)blockIdx.x < batch.n_aux_items) {
+        if constexpr (AUX)
+          adam_dev::update_item<bf16, 64, 4, false, true>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
+        else
+          adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
+      }
+      return;
+    }
   }
-  const int gblk = (int)blockIdx.x - (FUSED ? batch.n_aux : 0);  // n_aux % 8 == 0: same XCD order
+  const int gblk = (int)blockIdx.x - ((FUSED || AUX) ? batch.n_aux : 0);  // n_aux % 8 == 0: same XCD order
   unsigned long long* const stl =
       (batch.stamps != nullptr && threadIdx.x == 0) ? batch.stamps + 8 * (size_t)gblk : nullptr;
   if (stl != nullptr) stl[0] = wall_clock64();
@@ -423,17 +433,17 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
   }
 }
 
-template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1, bool AUX = false>
 int launch_typed(const LgemmBatch& b, hipStream_t stream) {
   constexpr int lds = LG<BM, SPLIT ? 2 : 1, BN, GT, KS>::LDS;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS, AUX>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
-  lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS>
-      <<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256 * KS), lds, stream>>>(b);
+  lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS, AUX>
+      <<<dim3((unsigned)(b.total_blocks + ((FUSED || AUX) ? b.n_aux : 0))), dim3(256 * KS), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -479,6 +489,7 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: fused update reduces the slabs");
   }
   INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
+  INF_CHECK_ARG(!(b.aux_only && (b.fused || b.split)), "lgemm: vector-item blocks: plain bf16 slab GEMM only");
   // the slab / C paths: two k groups per block where every block's K range splits into an
   // even number of 64-deep stages, each a multiple of RA.  Default for the split-operand
   // (bf16x3) dW: 122.3 -> 120.9 us per step.  The bf16 step keeps one group by default: two
@@ -494,6 +505,13 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
   }
   if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
+  if (b.aux_only) {
+    INF_CHECK_ARG(bm == 64 && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.aux_items != nullptr,
+                  "lgemm: vector-item blocks layout");
+    for (int i = 0; i < b.nprob; ++i) INF_CHECK_ARG(b.p[i].slab != nullptr, "lgemm: vector-item blocks: slab path only");
+    return ks2 ? launch_typed<64, false, false, LG_BN, false, 2, true>(b, stream)
+               : launch_typed<64, false, false, LG_BN, false, 1, true>(b, stream);
+  }
   if (ks2) return launch_typed<64, false, false, LG_BN, false, 2>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }

@@ -92,6 +92,10 @@ struct inf_plan {
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
   int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (igemm.hip), fp32 [bp_max][2H]
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
+  // the matrix items alone (the update launch after a dW GEMM that ran the vector items)
+  int64_t o_mat_items = 0;
+  int n_mat_items = 0;
+  bool last_aux_dw = false;  // the last training step ran its vector items in the dW launch
   // sharded update (data parallel, inf_plan_shard): the item-major staging layout of
   // `shard_world` ranks, this rank's items (+ the end-of-step item) as their own table
   int shard_world = 0, shard_rank = 0;
@@ -335,6 +339,7 @@ int build_layout(inf_plan* p) {
   p->o_tables = take(p->table_bytes);
   p->o_tables_b = take(align_up((int64_t)p->segs.size() * sizeof(AdamSeg)));
   p->o_aux_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
+  p->o_mat_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
   p->o_shard_items = take(align_up((nitems + 1) * sizeof(AdamItem)));
   int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
   for (const auto& g : p->segs)
@@ -475,7 +480,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
 bool use_fgemm(const inf_plan* p, int Bp, int splits);
 bool use_split_lgemm(const inf_plan* p, int Bp);
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr,
-                     int bucket = 0);
+                     int bucket = 0, const AdamArgs* aux = nullptr);
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
@@ -525,8 +530,10 @@ bool use_split_lgemm(const inf_plan* p, int Bp) {
   return true;
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket) {
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket,
+                     const AdamArgs* aux) {
   const int H = p->H, s = p->s;
+  INF_CHECK_ARG(aux == nullptr || (fuse == nullptr && bucket == 0 && chain == 3), "dW vector items: the chain3 slab path");
   if ((chain == CHAIN_F32 || chain == CHAIN_X3) && use_split_lgemm(p, Bp)) {
     INF_CHECK_ARG(fuse == nullptr, "split-operand dW: no fused update");
     const int splits = bucket ? p->bucket_splits : p->dw_splits;
@@ -569,6 +576,7 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     // large batches (the 64-ray chain tiles): 256 x 256 output tiles over the same images
     // (fgemm.hip), when every matrix is a whole number of them
     if (fuse == nullptr && use_fgemm(p, Bp, splits)) {
+      INF_CHECK_ARG(aux == nullptr, "dW vector items: lgemm only");
       FgemmBatch fb;
       std::memset(&fb, 0, sizeof(fb));
       fb.K = Bp;
@@ -634,6 +642,13 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       lb.n_aux = (int)round_up(p->n_aux_items, 8);
       lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
       lb.counters = p->W<int32_t>(p->o_counters);
+    } else if (aux != nullptr) {
+      // the update's vector / end-of-step items in the GEMM's leading blocks (lgemm.hpp aux_only)
+      lb.aux_only = 1;
+      lb.adam = *aux;
+      lb.n_aux_items = p->n_aux_items;
+      lb.n_aux = (int)round_up(p->n_aux_items, 8);
+      lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
     }
     // (128 x 128 tiles measured slower at 2 and 4 splits: step 75.3 / 71.6 vs 68.1-69.9 us,
     // profiles/r04/lgemm_tile_split_sweep.log; so were 4 splits of 64 x 128: 70.5-70.9)
@@ -1674,6 +1689,12 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
     if (it.seg < 0 || !p->adam_segs[it.seg].matrix) aux.push_back(it);
   p->n_aux_items = (int)aux.size();
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_aux_items, aux.data(), aux.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  std::vector<AdamItem> mat;
+  for (const auto& it : p->adam_items)
+    if (it.seg >= 0 && p->adam_segs[it.seg].matrix) mat.push_back(it);
+  p->n_mat_items = (int)mat.size();
+  if (!mat.empty())
+    INF_HIP_TRY(hipMemcpy(p->ws + p->o_mat_items, mat.data(), mat.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
   INF_HIP_TRY(hipMemset(p->ws + p->o_counters, 0, (size_t)(p->o_ws_end - p->o_counters)));
   // padded shadow columns/rows must read as zero
   INF_HIP_TRY(hipMemset(p->shadow, 0, p->shadow_bytes));
@@ -1793,6 +1814,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     return launch_update(a, p->mode, st);
   }
   // the update launch's arguments for a step whose gradient partials are complete
+  p->last_aux_dw = false;
   auto step_update = [&](int Bp_, int nloss_) {
     AdamArgs a = update_args(p, Bp_);
     a.grad_src = GRAD_SLABS;
@@ -1860,6 +1882,28 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       a.segs = p->W<AdamSeg>(p->o_tables_b);
       a.num_items = p->n_items_b1;
       return launch_update(a, p->mode, st);
+    }
+    // INF_AUX_DW=1: the vector / end-of-step items in the dW launch's leading blocks (on the
+    // CUs its 224 blocks leave idle at 4096 rays), the matrix items alone in the update
+    // launch -- bitwise the same step (test_aux_dw_bitwise), measured neutral: the update
+    // 10.1 -> 9.8 us, the dW launch 14.5 -> 14.9 us under rocprof, steps 64.4-64.6 vs
+    // 64.7-64.9 us (profiles/r04/aux_dw/), so opt-in
+    const char* aux_env = std::getenv("INF_AUX_DW");
+    const bool aux_dw = (aux_env != nullptr ? std::atoi(aux_env) != 0 : false) && apply_adam && !shard &&
+                        p->mode == INF_MODE_BF16 && p->n_mat_items > 0 && !use_fgemm(p, Bp, p->dw_splits);
+    p->last_aux_dw = aux_dw;
+    if (aux_dw) {
+      ck = 3;
+      p->last_chain = 3;
+      if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
+      const AdamArgs a = step_update(Bp, nloss);
+      if ((rc = run_weight_grads(p, Bp, st, 3, nullptr, 0, &a))) return rc;
+      AdamArgs m = a;
+      m.items = p->W<AdamItem>(p->o_mat_items);
+      m.num_items = p->n_mat_items;
+      if ((rc = launch_update(m, p->mode, st))) return rc;
+      note_shadow_write(p, m, st);
+      return INF_OK;
     }
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
   } else if (use_chain3x3(p, batch, Bp3)) {

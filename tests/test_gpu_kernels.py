@@ -468,6 +468,41 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
 
 
 @pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
+def test_aux_dw_bitwise(name, B, monkeypatch):
+    """The update's vector / end-of-step items run by the dW GEMM's leading blocks
+    (INF_AUX_DW=1: lgemm.hip AUX, the matrix items alone in the update launch) leave exactly
+    the bytes of the default split: parameters, Adam state and the step's loss sums over
+    three steps (config R: k = 1023, element-wise arena rows)."""
+    monkeypatch.setenv("INF_LGF", "0")
+    rng = np.random.default_rng(31)
+    k, H, L, s = CFG[name]
+    V = 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (B, 3))).cuda(),
+                         torch.from_numpy(rng.dirichlet([1, 1, 1], B).astype(np.float32)).cuda(),
+                         torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
+    out = {}
+    for tag in ("0", "1"):
+        monkeypatch.setenv("INF_AUX_DW", tag)
+        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+        plan.set_lr(1e-3)
+        b = plan.make_batch(source=src, batch=B)
+        sums = []
+        for _ in range(3):
+            plan.train_step(b, None, apply_adam=True)
+            c = plan.read_ctrl()
+            sums.append((c["loss_sum"], c["sse_sum"], c["batch_index"]))
+        assert plan.last_step_path() == "chain3"
+        torch.cuda.synchronize()
+        out[tag] = (params.cpu().numpy().copy(), plan.exp_avg.cpu().numpy().copy(),
+                    plan.exp_avg_sq.cpu().numpy().copy(), sums)
+    for a_, b_ in zip(out["0"][:3], out["1"][:3]):
+        assert np.array_equal(a_, b_)
+    assert out["0"][3] == out["1"][3]
+
+
+@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
 def test_lgemm_k_groups_match_one_group(name, B, monkeypatch):
     """The dW GEMM's two k groups per block (lgemm.hip KS = 2: INF_LGEMM_KS=2 on the bf16 step,
     the default of the bf16x3 one) against one group (INF_LGEMM_KS=1): the same
