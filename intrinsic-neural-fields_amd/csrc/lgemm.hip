@@ -454,7 +454,11 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   INF_CHECK_ARG(bm == 32 || bm == 64, "lgemm: rows per block");
   INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= LGEMM_MAX_PROBLEMS, "lgemm: problem count");
   const bool gt = b.fused == 2;  // split-K 1, the update on the LDS gradient tile (64 x 64 tiles)
-  const int bn = gt ? 64 : LG_BN;
+  // (INF_LGF_BN=128: 64 x 128 gradient tiles -- config D's dW + update 44.8 -> 49.8 us, step
+  // 128.7 -> 133.4 us: half the blocks at 2.4 -> 1.2 per CU, each a longer chain)
+  const char* e_gbn = std::getenv("INF_LGF_BN");
+  const int gt_bn = e_gbn != nullptr && std::atoi(e_gbn) == 128 ? 128 : 64;
+  const int bn = gt ? gt_bn : LG_BN;
   int blocks = 0;
   for (int i = 0; i < b.nprob; ++i) {
     LgemmProblem& p = b.p[i];
@@ -479,7 +483,7 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     INF_CHECK_ARG(bm == 64 && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.adam.items != nullptr,
                   "lgemm: gradient-tile update layout");
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: the vector items reduce their slabs");
-    return launch_typed<64, true, false, 64, true>(b, stream);
+    return gt_bn == 128 ? launch_typed<64, true, false, 128, true>(b, stream) : launch_typed<64, true, false, 64, true>(b, stream);
   }
   if (b.fused) {
     INF_CHECK_ARG(b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.counters != nullptr, "lgemm: fused update layout");
