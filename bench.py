@@ -298,7 +298,7 @@ class Trainer:
 # short window (the driver's 5 warmup + 20 timed steps span 1.7 ms) would time that ramp, not
 # the sustained rate a training run sees, so every timed leg first replays its own step,
 # untimed, for SETTLE_MS of GPU time -- the count is reported in the line (clock_settle).
-SETTLE_MS = float(os.environ.get("INF_BENCH_SETTLE_MS", "60"))
+SETTLE_MS = float(os.environ.get("INF_BENCH_SETTLE_MS", "100"))
 SETTLED = {}
 
 
