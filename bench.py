@@ -247,6 +247,12 @@ class Trainer:
                 with torch.cuda.graph(gm, stream=s):
                     self.i = 0
                     self._steps(self.GRAPH_STEPS)
+                # and a 4-step graph for the tail of a timed window (the driver's K = 20 is
+                # 8 + 8 + 4): a replay launch boundary costs ~6 us over a step inside a graph
+                self.g4 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g4, stream=s):
+                    self.i = 0
+                    self._steps(4)
         torch.cuda.current_stream().wait_stream(s)
         self.graphs = (g1, g2, gm)
         self.plan.set_batch_index(0)
@@ -281,12 +287,17 @@ class Trainer:
     def run(self, n):
         """n training steps (multi-step graph replays where they fit the epoch)."""
         gm = self.graphs[2] if self.graphs is not None else None
+        g4 = getattr(self, "g4", None) if gm is not None else None
         while n > 0:
             self._wrap()
             if gm is not None and n >= self.GRAPH_STEPS and self.i + self.GRAPH_STEPS <= self.nb and self.i % 2 == 0:
                 gm.replay()
                 self.i += self.GRAPH_STEPS
                 n -= self.GRAPH_STEPS
+            elif g4 is not None and n >= 4 and self.i + 4 <= self.nb and self.i % 2 == 0:
+                g4.replay()
+                self.i += 4
+                n -= 4
             else:
                 self.step()
                 n -= 1
@@ -302,7 +313,7 @@ SETTLE_MS = float(os.environ.get("INF_BENCH_SETTLE_MS", "100"))
 SETTLED = {}
 
 
-def settle(tr, world, tag=None):
+def settle(tr, world, warmup=0, tag=None):
     """Untimed replays of `tr`'s step for about SETTLE_MS ms (a probe of 8 steps sizes it;
     ranks agree on the count, since data-parallel replays carry collectives)."""
     if SETTLE_MS <= 0:
@@ -320,13 +331,17 @@ def settle(tr, world, tag=None):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         n = int(t[0])
     tr.run(n)
+    # end where the W warmup steps leave the timed window on a graph boundary of the epoch
+    # (production replays GRAPH_STEPS-step graphs; single-step replays cost ~6 us more each)
+    extra = (-(tr.i + warmup)) % tr.GRAPH_STEPS
+    tr.run(extra)
     if tag is not None:
-        SETTLED[tag] = n + 8
-    return n + 8
+        SETTLED[tag] = n + 8 + extra
+    return n + 8 + extra
 
 
 def time_steps(tr, steps, warmup, world, tag=None):
-    settle(tr, world, tag)
+    settle(tr, world, warmup, tag)
     tr.run(warmup)
     if world > 1:
         torch.distributed.barrier()
