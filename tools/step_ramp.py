@@ -46,10 +46,13 @@ def show(tag, t):
     marks = []
     for i, x in enumerate(t):
         cum += x * tr.GRAPH_STEPS
-        if i in (0, 1, 2, 3, 5, 10, 20, 50, 100, 200, 400, len(t) - 1):
+        if i in (0, 1, 2, 3, 5, 10, 20, 50, 100, 200, 400, 800, 1600, 3200, 6400, len(t) - 1):
             marks.append(f"#{i} @{cum / 1e3:.1f}ms {x:.2f}")
     tail = sorted(t[len(t) // 2:])[len(t) // 4]
     print(f"{tag}: us/step per replay: " + ", ".join(marks) + f"; median of 2nd half {tail:.2f}")
+    # medians of consecutive windows of 100 replays (~50 ms at 4096 rays)
+    w = [sorted(t[j:j + 100])[50] for j in range(0, len(t) - 99, 100)]
+    print(f"   per-100-replay medians: " + " ".join(f"{x:.1f}" for x in w))
 
 
 show("cold", trajectory(R))
