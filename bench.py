@@ -1161,8 +1161,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "clock_settle": {"ms": SETTLE_MS, "steps": SETTLED.get("headline", SETTLED.get("dp_" + str(chosen))),
-                             "note": "untimed replays of the same step before the W warmup steps: the GPU's "
-                                     "clocks ramp over ~25 ms of load (tools/step_ramp.py); "
+                             "note": "untimed replays of the same step before the W warmup steps (the GPU's "
+                                     "clocks ramp over ~25 ms of load, tools/step_ramp.py), ending so "
+                                     "that the timed window starts on an 8-step graph boundary; "
                                      "INF_BENCH_SETTLE_MS=0 disables"},
             "ms_per_step": ms,
             "higher_is_better": True,
