@@ -240,19 +240,21 @@ class Trainer:
                     g2 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g2, stream=s):
                         self.plan.adam(0, 0.0, advance=True)
-            else:
-                # several steps per graph: one replay launch per GRAPH_STEPS steps (an even
-                # number: the pre-gather slots alternate)
-                gm = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gm, stream=s):
-                    self.i = 0
-                    self._steps(self.GRAPH_STEPS)
-                # and a 4-step graph for the tail of a timed window (the driver's K = 20 is
-                # 8 + 8 + 4): a replay launch boundary costs ~6 us over a step inside a graph
-                self.g4 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.g4, stream=s):
-                    self.i = 0
-                    self._steps(4)
+            elif not self.prefetch:
+                # the production trainer's graph set (trainer.GRAPH_SIZES: 32, 8, 4, 2, 1 steps
+                # per replay launch; a launch boundary costs ~5-8 us of idle GPU): n steps replay
+                # as trainer.graph_replays(n) -- the driver's K = 20 from an epoch start is
+                # 8 + 8 + 4, exactly what trainer.py replays for an epoch of 20 batches
+                from trainer import GRAPH_SIZES
+                self.gset = {}
+                for n in GRAPH_SIZES:
+                    if n <= self.nb:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=s):
+                            self.i = 0
+                            self._steps(n)
+                        self.gset[n] = g
+                gm = self.gset.get(self.GRAPH_STEPS)
         torch.cuda.current_stream().wait_stream(s)
         self.graphs = (g1, g2, gm)
         self.plan.set_batch_index(0)
@@ -285,19 +287,26 @@ class Trainer:
         self.i += 1
 
     def run(self, n):
-        """n training steps (multi-step graph replays where they fit the epoch)."""
+        """n training steps: single-GPU, the production trainer's graph replays
+        (trainer.graph_replays over what is left of the epoch); data-parallel shapes,
+        GRAPH_STEPS-step graphs where they fit the epoch, else single steps."""
+        gset = getattr(self, "gset", None) if self.graphs is not None else None
+        if gset:
+            from trainer import graph_replays
+            while n > 0:
+                self._wrap()
+                for g in graph_replays(min(n, self.nb - self.i), tuple(gset)):
+                    gset[g].replay()
+                    self.i += g
+                    n -= g
+            return
         gm = self.graphs[2] if self.graphs is not None else None
-        g4 = getattr(self, "g4", None) if gm is not None else None
         while n > 0:
             self._wrap()
             if gm is not None and n >= self.GRAPH_STEPS and self.i + self.GRAPH_STEPS <= self.nb and self.i % 2 == 0:
                 gm.replay()
                 self.i += self.GRAPH_STEPS
                 n -= self.GRAPH_STEPS
-            elif g4 is not None and n >= 4 and self.i + 4 <= self.nb and self.i % 2 == 0:
-                g4.replay()
-                self.i += 4
-                n -= 4
             else:
                 self.step()
                 n -= 1
@@ -331,9 +340,11 @@ def settle(tr, world, warmup=0, tag=None):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         n = int(t[0])
     tr.run(n)
-    # end where the W warmup steps leave the timed window on a graph boundary of the epoch
-    # (production replays GRAPH_STEPS-step graphs; single-step replays cost ~6 us more each)
-    extra = (-(tr.i + warmup)) % tr.GRAPH_STEPS
+    # end where the W warmup steps leave the timed window at an epoch start (single-GPU: the
+    # window then replays what trainer.py replays for an epoch of K batches) or on a graph
+    # boundary of the data-parallel shapes' GRAPH_STEPS-step graphs
+    period = tr.nb if getattr(tr, "gset", None) else tr.GRAPH_STEPS
+    extra = (-(tr.i + warmup)) % period
     tr.run(extra)
     if tag is not None:
         SETTLED[tag] = n + 8 + extra
@@ -343,6 +354,7 @@ def settle(tr, world, warmup=0, tag=None):
 def time_steps(tr, steps, warmup, world, tag=None):
     settle(tr, world, warmup, tag)
     tr.run(warmup)
+    tr._wrap()  # an epoch wrap due at the window's start (set_batch_index) happens before it
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -487,7 +499,7 @@ def config_d_bench(args, device, B=4096, steps=40):
     from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
     a = copy.copy(args)
     a.k, a.verts, a.no_graph = 4096, 500_000, False
-    tr = Trainer(a, device, B, 0, 1, nb=8)
+    tr = Trainer(a, device, B, 0, 1)
     tr.capture()
     ms, _ = time_steps(tr, steps, 8, 1)
     path = tr.plan.last_step_path()
@@ -522,7 +534,7 @@ def _secondary_train(args, device, B, steps, **over):
     for kk, v in over.items():
         setattr(a, kk, v)
     a.no_graph = False
-    tr = Trainer(a, device, B, 0, 1, nb=8)
+    tr = Trainer(a, device, B, 0, 1)
     tr.capture()
     ms, _ = time_steps(tr, steps, 4, 1)
     P = tr.plan.info.num_params
@@ -830,13 +842,18 @@ PSNR_RUNS = {
     "g13_train_curve_B_L2.npz": ("reference synthetic run G13 on config B's MLP (k=1024 8x256 skip 4, L2, lr 1e-4, "
                                  "12 epochs)",
                                  {"k": 1024, "num_layers": 8, "mlp_hidden_dim": 256, "skip_layer_idx": 4}, "L2"),
+    # the reference's own shipped configuration (intrinsic_cat.yaml:24-37), k = the fixture's list of 1023 indices
+    "g16_train_curve_R.npz": ("reference synthetic run G16 on config R exactly (k=list(1023) 6x128 skip 3, L1, lr 1e-4, "
+                              "batch 4096, 12 epochs)",
+                              {"k": "k_list", "num_layers": 6, "mlp_hidden_dim": 128, "skip_layer_idx": 3}, "L1"),
 }
 
 
 def psnr_vs_ref(mode, fixture="g8_train_curve.npz"):
     """'PSNR vs ref' of BASELINE.json's metric: the reference's own 12-epoch synthetic
-    training runs (tests/golden/g8_train_curve.npz and, on the benchmarked MLP,
-    g13_train_curve_B_L2.npz, produced by importing the reference; no dataset is available
+    training runs (tests/golden/g8_train_curve.npz, on the benchmarked MLP
+    g13_train_curve_B_L2.npz, and on the reference's own cat configuration
+    g16_train_curve_R.npz; produced by importing the reference; no dataset is available
     offline) re-run through this framework's Trainer (trainer.py mirror, fused HIP steps)
     -- validation epoch-PSNR curve against the reference's."""
     import tempfile
@@ -846,6 +863,8 @@ def psnr_vs_ref(mode, fixture="g8_train_curve.npz"):
     from trainer import Trainer
     workload, mkeys, loss = PSNR_RUNS[fixture]
     d = np.load(os.path.join(ROOT, "tests", "golden", fixture))
+    if mkeys["k"] == "k_list":
+        mkeys = dict(mkeys, k=[int(x) for x in d["k_list"]])
     with tempfile.TemporaryDirectory() as out:
         cfg = {"seed": 0, "data": {"img_height": 8, "img_width": 8},
                "model": dict(mkeys, kernels={"mode": mode}),

@@ -116,8 +116,9 @@ typedef struct inf_batch {
 typedef struct inf_ctrl {
   int32_t step;        /* Adam step count t (post-increment semantics of torch Adam) */
   int32_t batch_index; /* batch number inside the current epoch                     */
-  float lr;            /* learning rate (ReduceLROnPlateau may change it)            */
   int32_t prefetch_index; /* batch number the next inf_prefetch_batch gathers        */
+  int32_t reserved;
+  double lr;           /* learning rate, a double as torch's param_group["lr"]       */
   double loss_sum;     /* sum of element losses of the last step                     */
   double sse_sum;      /* sum of squared errors of the last step                     */
   double epoch_loss;   /* accumulated over the epoch (host resets)                   */
@@ -192,7 +193,7 @@ int inf_ff_encode(int64_t n, int d, const float* x, const float* bands, int k, i
 /* torch.optim.Adam (config.py:108) step `step` (1-based) of one parameter tensor that is
  * not in a plan arena: the plan update's arithmetic (adam_dev.hpp adam_elem). */
 int inf_adam_dense(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int step,
-                   float lr, float beta1, float beta2, float eps, inf_stream_t stream);
+                   double lr, double beta1, double beta2, double eps, inf_stream_t stream);
 
 /* ---- plan: one TextureField (model.py:12-112) + its training step ---------------- */
 typedef struct inf_plan inf_plan;
@@ -208,8 +209,11 @@ int inf_plan_param_layout(const inf_plan* plan, int64_t* offsets, int64_t* numel
  * (grads/exp_avg/exp_avg_sq may be NULL for inference-only plans). */
 int inf_plan_bind(inf_plan* plan, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
                   void* shadow, void* workspace, inf_ctrl* ctrl);
-/* Adam hyper-parameters (torch.optim.Adam defaults: 0.9, 0.999, 1e-8; config.py:108). */
-int inf_plan_set_adam(inf_plan* plan, float beta1, float beta2, float eps);
+/* Adam hyper-parameters (torch.optim.Adam defaults: 0.9, 0.999, 1e-8; config.py:108), as
+ * the Python doubles torch holds them: the update derives its fp32 constants the way torch's
+ * CPU kernels do (1 - beta1, beta2, 1 - beta2 and eps rounded to float from the double;
+ * the bias corrections and lr / (1 - beta1^t) in double). */
+int inf_plan_set_adam(inf_plan* plan, double beta1, double beta2, double eps);
 
 /* Re-derive the packed GEMM weights from the fp32 parameters (after init,
  * load_state_dict, or any host-side parameter edit). */
@@ -269,12 +273,12 @@ int inf_prefetch_batch(inf_plan* plan, const inf_batch* batch, int slot, inf_str
  * lr -- lr = 0 leaves the parameters unchanged, as torch does); step <= 0: both are read
  * from ctrl (graph-replayed steps, where the fused step has already advanced
  * ctrl->step). */
-int inf_adam(inf_plan* plan, int step, float lr, inf_stream_t stream);
+int inf_adam(inf_plan* plan, int step, double lr, inf_stream_t stream);
 
 /* inf_adam with flags: INF_STEP_ADVANCE also advances ctrl->batch_index by one in the same
  * launch (the data-parallel step's tail: all-reduce -> Adam + advance, instead of a
  * separate inf_ctrl_advance launch).  flags = 0 is inf_adam. */
-int inf_adam_ex(inf_plan* plan, int step, float lr, int flags, inf_stream_t stream);
+int inf_adam_ex(inf_plan* plan, int step, double lr, int flags, inf_stream_t stream);
 
 /* Render slice (renderer.py:112-146): forward of `batch` and placement of each
  * predicted colour at image row pixel_map[hit[b]] (hit = hit_ray_idxs; pixel_map maps

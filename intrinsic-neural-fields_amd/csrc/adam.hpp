@@ -77,7 +77,7 @@ struct AdamArgs {
   int32_t do_adam;
   int32_t write_shadow;
   int32_t step_host;    // > 0: use this t and lr_host, else ctrl->step and ctrl->lr
-  float lr_host;        // used as given (0 included) when step_host > 0
+  double lr_host;       // used as given (0 included) when step_host > 0
   inf_ctrl* ctrl;
   // end-of-step item (AdamItem.seg < 0): fixed-order sum of the fused chain's per-tile
   // loss / SSE partials into ctrl, and the batch-index advance of a replayed epoch

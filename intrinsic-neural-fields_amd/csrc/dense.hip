@@ -11,6 +11,8 @@
 //   inf_colsum:        out[n] (+)= sum_m X[m ldx + n]            (bias gradients)
 //   inf_view_angle:    acos(cos_sim(-d, normals[face]))          (model.py:164-169, 179-185)
 //   inf_ff_encode:     FourierFeatEnc of 1- or 3-wide inputs     (layers.py:6-25)
+#include <cmath>
+
 #include "common.hpp"
 
 namespace inf {
@@ -212,28 +214,21 @@ __global__ void adam_dense_kernel(int64_t n, float* __restrict__ p, const float*
   }
 }
 
-double pow_int_host(double b, int t) {
-  double r = 1.0;
-  while (t > 0) {
-    if (t & 1) r *= b;
-    b *= b;
-    t >>= 1;
-  }
-  return r;
-}
 }  // namespace
 
 extern "C" int inf_adam_dense(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                              int step, float lr, float beta1, float beta2, float eps, inf_stream_t stream) {
+                              int step, double lr, double beta1, double beta2, double eps, inf_stream_t stream) {
   INF_CHECK_ARG(n >= 0 && step >= 1, "adam_dense: bad arguments");
   if (n == 0) return INF_OK;
   INF_CHECK_ARG(param != nullptr && grad != nullptr && exp_avg != nullptr && exp_avg_sq != nullptr,
                 "adam_dense: null argument");
-  const double bc1 = 1.0 - pow_int_host((double)beta1, step);
-  const double bc2 = 1.0 - pow_int_host((double)beta2, step);
+  // torch's scalars (Python doubles: beta ** step, lr / bc1, sqrt(bc2)), each rounded to
+  // float where its CPU kernel takes it
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
   adam_dense_kernel<<<blocks_for(n), 256, 0, (hipStream_t)stream>>>(
-      n, param, grad, exp_avg, exp_avg_sq, (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), eps,
-      (float)(-((double)lr / bc1)), (float)sqrt(bc2));
+      n, param, grad, exp_avg, exp_avg_sq, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+      (float)(-(lr / bc1)), (float)std::sqrt(bc2));
   INF_LAUNCH_CHECK();
   return INF_OK;
 }

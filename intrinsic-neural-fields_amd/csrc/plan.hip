@@ -128,7 +128,7 @@ struct inf_plan {
 
   std::vector<AdamSeg> adam_segs;
   std::vector<AdamItem> adam_items;
-  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+  double beta1 = 0.9, beta2 = 0.999, eps = 1e-8;  // torch holds them as Python doubles
 
   // saved forward
   int saved_batch = 0, saved_bp = 0;
@@ -705,10 +705,12 @@ AdamArgs update_args(inf_plan* p, int Bp) {
   a.ctrl = p->ctrl;
   a.beta1_d = p->beta1;
   a.beta2_d = p->beta2;
-  a.one_minus_b1 = (float)(1.0 - (double)p->beta1);
-  a.beta2 = p->beta2;
-  a.one_minus_b2 = (float)(1.0 - (double)p->beta2);
-  a.eps = p->eps;
+  // the fp32 constants torch's CPU kernels use: the double expressions rounded once
+  // (lerp_ weight 1 - beta1, mul_ beta2, addcmul_ value 1 - beta2, add_ eps)
+  a.one_minus_b1 = (float)(1.0 - p->beta1);
+  a.beta2 = (float)p->beta2;
+  a.one_minus_b2 = (float)(1.0 - p->beta2);
+  a.eps = (float)p->eps;
   (void)Bp;
   return a;
 }
@@ -1522,7 +1524,7 @@ int forward_impl(inf_plan* p, const inf_batch* b, float* pred, bool save, bool l
 extern "C" {
 
 const char* inf_last_error(void) { return g_last_error.c_str(); }
-int inf_abi_version(void) { return 2; }
+int inf_abi_version(void) { return 3; }  // 3: double lr / Adam constants, inf_ctrl 56 bytes
 
 int inf_gather(const void* table, int table_dtype, int64_t num_vertices, int k, int64_t table_ld, const void* vids,
                int vid_dtype, const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, int batch,
@@ -1593,6 +1595,25 @@ int inf_plan_param_layout(const inf_plan* p, int64_t* offsets, int64_t* numels, 
     offsets[i] = p->segs[i].off;
     numels[i] = (int64_t)p->segs[i].R * p->segs[i].C;
   }
+  return INF_OK;
+}
+
+// The item subsets the fused dW + update reads (lgemm.hip): the vector and end-of-step
+// items its leading blocks run, and the matrix items.  Copies of p->adam_items: re-uploaded
+// whenever those change (bind, and inf_plan_shard's staging offsets goff / woff, which the
+// fused update's SHARD_GRAD_OUT items write through).
+static int upload_item_subsets(inf_plan* p) {
+  std::vector<AdamItem> aux;
+  for (const auto& it : p->adam_items)
+    if (it.seg < 0 || !p->adam_segs[it.seg].matrix) aux.push_back(it);
+  p->n_aux_items = (int)aux.size();
+  INF_HIP_TRY(hipMemcpy(p->ws + p->o_aux_items, aux.data(), aux.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  std::vector<AdamItem> mat;
+  for (const auto& it : p->adam_items)
+    if (it.seg >= 0 && p->adam_segs[it.seg].matrix) mat.push_back(it);
+  p->n_mat_items = (int)mat.size();
+  if (!mat.empty())
+    INF_HIP_TRY(hipMemcpy(p->ws + p->o_mat_items, mat.data(), mat.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
   return INF_OK;
 }
 
@@ -1683,18 +1704,7 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
     const std::vector<AdamSeg> tb = bucket_segs(p);
     INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables_b, tb.data(), tb.size() * sizeof(AdamSeg), hipMemcpyHostToDevice));
   }
-  // the vector and end-of-step items, run by the dW GEMM's first blocks when it fuses the update
-  std::vector<AdamItem> aux;
-  for (const auto& it : p->adam_items)
-    if (it.seg < 0 || !p->adam_segs[it.seg].matrix) aux.push_back(it);
-  p->n_aux_items = (int)aux.size();
-  INF_HIP_TRY(hipMemcpy(p->ws + p->o_aux_items, aux.data(), aux.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
-  std::vector<AdamItem> mat;
-  for (const auto& it : p->adam_items)
-    if (it.seg >= 0 && p->adam_segs[it.seg].matrix) mat.push_back(it);
-  p->n_mat_items = (int)mat.size();
-  if (!mat.empty())
-    INF_HIP_TRY(hipMemcpy(p->ws + p->o_mat_items, mat.data(), mat.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  if (int rc = upload_item_subsets(p)) return rc;
   INF_HIP_TRY(hipMemset(p->ws + p->o_counters, 0, (size_t)(p->o_ws_end - p->o_counters)));
   // padded shadow columns/rows must read as zero
   INF_HIP_TRY(hipMemset(p->shadow, 0, p->shadow_bytes));
@@ -1703,9 +1713,9 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
   return INF_OK;
 }
 
-int inf_plan_set_adam(inf_plan* p, float beta1, float beta2, float eps) {
+int inf_plan_set_adam(inf_plan* p, double beta1, double beta2, double eps) {
   INF_CHECK_ARG(p != nullptr, "null plan");
-  INF_CHECK_ARG(beta1 >= 0.f && beta1 < 1.f && beta2 >= 0.f && beta2 < 1.f && eps >= 0.f, "Adam hyper-parameters");
+  INF_CHECK_ARG(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0, "Adam hyper-parameters");
   p->beta1 = beta1;
   p->beta2 = beta2;
   p->eps = eps;
@@ -1957,9 +1967,9 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   return INF_OK;
 }
 
-int inf_adam(inf_plan* p, int step, float lr, inf_stream_t stream) { return inf_adam_ex(p, step, lr, 0, stream); }
+int inf_adam(inf_plan* p, int step, double lr, inf_stream_t stream) { return inf_adam_ex(p, step, lr, 0, stream); }
 
-int inf_adam_ex(inf_plan* p, int step, float lr, int flags, inf_stream_t stream) {
+int inf_adam_ex(inf_plan* p, int step, double lr, int flags, inf_stream_t stream) {
   INF_CHECK_ARG((flags & ~INF_STEP_ADVANCE) == 0, "adam: unknown flags");
   if (p == nullptr || !p->bound || p->grads == nullptr || p->exp_avg == nullptr || p->exp_avg_sq == nullptr) {
     set_error("adam: plan not bound with grads and Adam state");
@@ -2044,6 +2054,7 @@ int inf_plan_shard(inf_plan* p, int world, int rank, int64_t* grad_floats, int64
   const int64_t seg_bytes = align_up(p->adam_segs.size() * sizeof(AdamSeg));
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables + seg_bytes, p->adam_items.data(),
                         p->adam_items.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
+  if (int rc = upload_item_subsets(p)) return rc;  // the fused dW + update's copies carry goff too
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_shard_items, own.data(), own.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
   p->n_shard_items = (int)own.size();
   p->shard_world = world;

@@ -51,13 +51,13 @@ class Batch(ctypes.Structure):
 
 
 class Ctrl(ctypes.Structure):
-    _fields_ = [("step", c_int32), ("batch_index", c_int32), ("lr", c_float), ("prefetch_index", c_int32),
-                ("loss_sum", c_double), ("sse_sum", c_double), ("epoch_loss", c_double),
+    _fields_ = [("step", c_int32), ("batch_index", c_int32), ("prefetch_index", c_int32), ("reserved", c_int32),
+                ("lr", c_double), ("loss_sum", c_double), ("sse_sum", c_double), ("epoch_loss", c_double),
                 ("epoch_sse", c_double)]
 
 
 CTRL_BYTES = ctypes.sizeof(Ctrl)
-assert CTRL_BYTES == 48
+assert CTRL_BYTES == 56
 
 _SIGNATURES = {
     "inf_last_error": (ctypes.c_char_p, []),
@@ -80,8 +80,8 @@ _SIGNATURES = {
     "inf_dense_act_bwd": (c_int, [c_int64, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "inf_colsum": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "inf_view_angle": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
-    "inf_adam_dense": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float,
-                               c_float, c_void_p]),
+    "inf_adam_dense": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_double, c_double, c_double,
+                               c_double, c_void_p]),
     "inf_ff_encode": (c_int, [c_int64, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p]),
     "inf_uv_fill_holes": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "inf_masked_sse": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
@@ -90,13 +90,13 @@ _SIGNATURES = {
     "inf_plan_get_info": (c_int, [c_void_p, ctypes.POINTER(PlanInfo)]),
     "inf_plan_param_layout": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64), c_int]),
     "inf_plan_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "inf_plan_set_adam": (c_int, [c_void_p, c_float, c_float, c_float]),
+    "inf_plan_set_adam": (c_int, [c_void_p, c_double, c_double, c_double]),
     "inf_sync_shadow": (c_int, [c_void_p, c_void_p]),
     "inf_forward": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_int, c_void_p]),
     "inf_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_train_step": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_int, c_void_p]),
-    "inf_adam": (c_int, [c_void_p, c_int, c_float, c_void_p]),
-    "inf_adam_ex": (c_int, [c_void_p, c_int, c_float, c_int, c_void_p]),
+    "inf_adam": (c_int, [c_void_p, c_int, c_double, c_void_p]),
+    "inf_adam_ex": (c_int, [c_void_p, c_int, c_double, c_int, c_void_p]),
     "inf_render": (c_int, [c_void_p, ctypes.POINTER(Batch), c_void_p, c_void_p, c_void_p, c_void_p]),
     "inf_projected_rows": (c_int64, [c_int64]),
     "inf_project_table": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),

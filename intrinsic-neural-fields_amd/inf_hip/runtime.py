@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import (CTRL_BYTES, ENC_CODES, ENC_NONE, ENC_PROJECTED, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
+from . import (CTRL_BYTES, Ctrl, ENC_CODES, ENC_NONE, ENC_PROJECTED, DTYPE_BF16, DTYPE_F32, DTYPE_I32, DTYPE_I64, INF_OK, LOSS_CODES, MODE_BF16,
                MODE_CODES, Batch, STEP_ADAM, STEP_ADVANCE, STEP_PART1, STEP_PART2, STEP_SHARD, STEP_XSLOT0, STEP_XSLOT1, MlpDesc, PlanInfo,
                c_int64, c_void_p,
                check, lib)
@@ -260,6 +260,10 @@ class Plan:
             if t is not None and (t.numel() != self.info.num_params or t.device != self.device):
                 raise ValueError("optimizer arenas must match the parameter arena")
         self.grads, self.exp_avg, self.exp_avg_sq = grads, exp_avg, exp_avg_sq
+        # inf_plan_bind resets the C side's shard layout and buffers: forget ours with it, so
+        # a sharded step after a rebind re-shards (dp._ensure_shard) instead of failing
+        self.shard_world = self.shard_rank = 0
+        self.grad_staging = self.grad_chunk = self.weight_staging = None
         with torch.cuda.device(self.device):
             check(lib.inf_plan_bind(self.handle, ptr(self.params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq),
                                     ptr(self.shadow), ptr(self.workspace), ptr(self.ctrl)), "plan_bind")
@@ -288,23 +292,22 @@ class Plan:
         return self.ctrl.view(torch.float64)
 
     def set_lr(self, lr: float):
-        self.ctrl_f32[2].fill_(float(lr))
+        self.ctrl_f64[Ctrl.lr.offset // 8].fill_(float(lr))
 
     def set_step(self, step: int):
-        self.ctrl_i32[0].fill_(int(step))
+        self.ctrl_i32[Ctrl.step.offset // 4].fill_(int(step))
 
     def set_batch_index(self, i: int):
-        self.ctrl_i32[1].fill_(int(i))
+        self.ctrl_i32[Ctrl.batch_index.offset // 4].fill_(int(i))
 
     def set_prefetch_index(self, i: int):
-        self.ctrl_i32[3].fill_(int(i))
+        self.ctrl_i32[Ctrl.prefetch_index.offset // 4].fill_(int(i))
 
     def reset_epoch_sums(self):
-        self.ctrl_f64[4:6].zero_()
+        self.ctrl_f64[Ctrl.epoch_loss.offset // 8:Ctrl.epoch_sse.offset // 8 + 1].zero_()
 
     def read_ctrl(self) -> dict:
         raw = bytes(self.ctrl.cpu().numpy().tobytes())
-        from . import Ctrl
         c = Ctrl.from_buffer_copy(raw)
         return {f: getattr(c, f) for f, _ in Ctrl._fields_}
 

@@ -63,9 +63,27 @@ def _summary_writer(log_dir):
         return _JsonlWriter(log_dir)
 
 
+# Steps per captured graph of a replayed epoch: the epoch's full batches replay as the
+# greedy decomposition of their count into these sizes (32-step graphs, then 8, 4, 2, 1).
+# Each replay launch costs ~5-8 us of idle GPU at its boundary (tools/launch_window.py:
+# 61.7 us per step inside a graph, 69.8 us as single-step replays), so long epochs replay
+# the largest graph and an epoch's remainder takes at most four launches, not up to 7.
+GRAPH_SIZES = (32, 8, 4, 2, 1)
+
+
+def graph_replays(n, sizes=GRAPH_SIZES):
+    """The graph sizes, in replay order, that cover n consecutive steps."""
+    out = []
+    for g in sizes:
+        while n >= g:
+            out.append(g)
+            n -= g
+    return out
+
+
 class _FusedEpoch:
-    """Replays captured fused steps (GRAPH_STEPS per graph launch, then single steps) over
-    the full batches of an epoch; the batch index advances on the device.  The gather runs
+    """Replays captured fused steps (graphs of GRAPH_SIZES steps) over the full batches of
+    an epoch; the batch index advances on the device.  The gather runs
     inside the fused chain by default; INF_PREFETCH=1 moves the next batch's gather to a
     side stream (runtime.StepPipeline: each step then reads pre-gathered feature rows),
     which measured slower on one GPU (see StepPipeline)."""
@@ -112,18 +130,16 @@ class _FusedEpoch:
             optim.sync_runtime_state(model, rt, plan, group)
             plan.reset_epoch_sums()
             plan.set_batch_index(0)
-            g1, gm = self.graph
+            graphs = self.graph
             if self.pipe is not None and self.pipe.start():
                 for _ in range(full // self.GRAPH_STEPS):
-                    gm.replay()
+                    graphs[self.GRAPH_STEPS].replay()
                 b = self._batch
                 self.pipe.run(full % self.GRAPH_STEPS,
                               lambda xs: plan.train_step(b, None, apply_adam=True, advance=True, xslot=xs))
             else:
-                for _ in range(full // self.GRAPH_STEPS):
-                    gm.replay()
-                for _ in range(full % self.GRAPH_STEPS):
-                    g1.replay()
+                for n in graph_replays(full):
+                    graphs[n].replay()
             optim.after_fused_steps(model, rt, group, full)
             done = full
             total = full * B
@@ -154,23 +170,26 @@ class _FusedEpoch:
             self.pipe = None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g1, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        full = loader.N // B
+        # only the sizes this epoch replays (an epoch of 20 batches needs no 32-step graph)
+        sizes = sorted(set(graph_replays(full))) if self.pipe is None else [self.GRAPH_STEPS]
+        graphs = {}
         with torch.cuda.stream(s):
-            # the step's update launch also advances ctrl.batch_index (INF_STEP_ADVANCE)
-            with torch.cuda.graph(g1, stream=s):
-                plan.train_step(b, None, apply_adam=True, advance=True)
-            with torch.cuda.graph(gm, stream=s):  # GRAPH_STEPS steps per replay launch
-                if self.pipe is not None:
-                    self.pipe.run(self.GRAPH_STEPS,
-                                  lambda xs: plan.train_step(b, None, apply_adam=True, advance=True, xslot=xs))
-                else:
-                    for _ in range(self.GRAPH_STEPS):
-                        plan.train_step(b, None, apply_adam=True, advance=True)
+            for n in sizes:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):  # n steps per replay launch
+                    if self.pipe is not None:
+                        self.pipe.run(n, lambda xs: plan.train_step(b, None, apply_adam=True, advance=True, xslot=xs))
+                    else:
+                        # the step's update launch also advances ctrl.batch_index (INF_STEP_ADVANCE)
+                        for _ in range(n):
+                            plan.train_step(b, None, apply_adam=True, advance=True)
+                graphs[n] = g
         torch.cuda.current_stream().wait_stream(s)
         for dst, src in zip((plan.params, plan.exp_avg, plan.exp_avg_sq, plan.ctrl), saved):
             dst.copy_(src)
         plan.sync_shadow()
-        self.graph = (g1, gm)
+        self.graph = graphs
 
 
 class Trainer:

@@ -31,12 +31,16 @@ Fixtures:
   g14_bake_{grid,jitter}.npz         texel search + barycentrics + hole filling
                                      (get_tris_fast, bary_matched, uv_fill_holes)  bake_texture_field.py:96-264,360-397
   g15_raygen.npz                     create_ray_origins_and_directions         mesh.py:171-207
+  g12_spread.npz                     G12's curve under other fp32 summation orders (threads, DataParallel, f64)
+  g16_train_curve_R.npz              config R exactly (intrinsic_cat.yaml:24-37: k = list(1023), 6x128, skip 3,
+                                     L1, lr 1e-4, batch 4096): 12-epoch curve + its summation-order spread
 
 Run:  python tests/golden/make_golden.py
 """
 import copy
 import os
 import sys
+import tempfile
 import types
 
 sys.dont_write_bytecode = True
@@ -658,6 +662,126 @@ def g8_spread():
     save("g8_spread.npz", ref=np.asarray(d["val_psnr"], np.float64), **curves)
 
 
+class _Bf16Forward(torch.nn.Module):
+    """The reference's module under torch's CPU bf16 autocast (its GEMMs on bf16 operands,
+    fp32 accumulation and fp32 parameters / optimizer): how far the reference itself moves
+    when run in bf16 -- the spread a bf16 implementation's PSNR bar is derived from."""
+
+    def __init__(self, fwd):
+        super().__init__()
+        self.fwd = fwd
+
+    def forward(self, batch):
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            return self.fwd(batch).float()
+
+
+def _curve_spread(d, mcfg, loss_type, tag_note="", bf16=False):
+    """The reference's own val-PSNR curve on fixture `d`'s inputs under other fp32 summation
+    orders -- 1 / 3 / 8 CPU threads, nn.DataParallel's scatter over 2 and 4 replicas, and
+    float64 -- the spread a per-epoch PSNR bar is derived from (g8_spread's recipe); with
+    bf16=True also under CPU bf16 autocast (1 / 3 / 8 threads, DataParallel over 2 and 4)."""
+    B, lr = int(d["batch"]), float(d["lr"])
+    cfg = {"model": mcfg, "training": {"lr": lr, "loss_type": loss_type}}
+    curves = {}
+    variants = [("threads1", 1, 1, torch.float32), ("threads3", 3, 1, torch.float32),
+                ("threads8", 8, 1, torch.float32), ("dp2", 8, 2, torch.float32),
+                ("dp4", 8, 4, torch.float32), ("f64", 8, 1, torch.float64)]
+    if bf16:
+        variants += [("bf16_threads1", 1, 1, torch.bfloat16), ("bf16_threads3", 3, 1, torch.bfloat16),
+                     ("bf16_threads8", 8, 1, torch.bfloat16), ("bf16_dp2", 8, 2, torch.bfloat16),
+                     ("bf16_dp4", 8, 4, torch.bfloat16)]
+    for tag, threads, chunks, dt in variants:
+        torch.set_num_threads(threads)
+        torch.manual_seed(0)
+        model, _ = ref_config.get_model_and_optim(cfg, None, "cpu")
+        model = model.to(torch.float64 if dt == torch.float64 else torch.float32)
+        optim = torch.optim.Adam(model.parameters(), lr=lr)  # config.py:108 on the cast model
+        fwd = _ChunkedForward(model, chunks) if chunks > 1 or dt == torch.float64 else model
+        if dt == torch.bfloat16:
+            fwd = _Bf16Forward(fwd)
+        tr = _bare_trainer(fwd, optim, ref_config.get_loss_fn(cfg))
+        t = torch.from_numpy
+        Et = t(d["E"])
+        train_ld = ref_loader.RayDataLoader(Et, "efuncs", t(d["tr_vids"]), t(d["tr_bary"]), t(d["tr_rgb"]),
+                                            None, None, B, False, True, device="cpu")
+        tr.val_data_loader = ref_loader.RayDataLoader(Et, "efuncs", t(d["va_vids"]), t(d["va_bary"]),
+                                                      t(d["va_rgb"]), None, None, B, False, False, device="cpu")
+        val = []
+        for epoch in range(len(d["val_psnr"])):
+            for b in train_ld:  # shuffle=False: the fixture's deterministic batch order
+                tr._train_step(b)
+            val.append(tr.evaluate(epoch)[1])
+        curves[tag] = np.array(val, np.float64)
+        print(tag_note, tag, np.round(curves[tag] - d["val_psnr"], 4).tolist())
+    torch.set_num_threads(8)
+    return curves
+
+
+def g12_spread():
+    """G12's spread: how far the reference's own G12 curve (config B's
+    MLP, L1, lr 2e-4) moves under other fp32 summation orders -> g12_spread.npz.  The G12
+    test derives its per-epoch bar from it instead of a chosen 0.5 dB."""
+    d = np.load(os.path.join(OUT, "g12_train_curve_B.npz"))
+    curves = _curve_spread(d, model_cfg("B"), "L1", "g12", bf16=True)
+    save("g12_spread.npz", ref=np.asarray(d["val_psnr"], np.float64), **curves)
+
+
+def g16_train_curve_R():
+    """The reference's own shipped configuration, exactly (configs/texture_reconstruction/
+    intrinsic_cat.yaml:24-37): k = list(1023) eigenfunction indices (runs 0-255, 1793-2303,
+    3840-4095 of a V x 4096 table), 6 x 128 MLP, skip 3, L1, Adam lr 1e-4, batch 4096 --
+    12 epochs of G8's synthetic texture reconstruction (no dataset offline), the
+    val-PSNR curve (trainer.py:164-187,232-283), plus its summation-order spread
+    (_curve_spread) in the same file."""
+    rng = np.random.default_rng(16)
+    V = 1000
+    full = rng.standard_normal((V, 4096)).astype(np.float32)
+    with tempfile.TemporaryDirectory() as td:  # the loader's own column select + rescale
+        path = os.path.join(td, "efuncs.npy")
+        np.save(path, full)
+        E = ref_mesh.load_first_k_eigenfunctions(path, K_LIST_1023, rescale_strategy="standard").numpy()
+    del full
+    proj = rng.standard_normal((16, 3)).astype(np.float32) * 2.0
+    vert_rgb = 1.0 / (1.0 + np.exp(-(E[:, :16] * 4.0) @ proj))
+
+    def rays(n):
+        vids, bary = synthetic_rays(rng, V, n, include_edges=False)
+        rgb = np.einsum("ni,nic->nc", bary, vert_rgb[vids]).astype(np.float32)
+        return vids.astype(np.int32), bary, rgb  # int32 ids, as dataset.py stores them
+    tr_v, tr_b, tr_rgb = rays(65536)
+    va_v, va_b, va_rgb = rays(8192)
+    batch, lr = 4096, 1e-4  # intrinsic_cat.yaml:32-33
+    cfg = {"model": model_cfg("R"), "training": {"lr": lr, "loss_type": "L1"}}
+    torch.set_num_threads(8)
+    torch.manual_seed(0)
+    model, optim = ref_config.get_model_and_optim(cfg, None, "cpu")
+    tr = _bare_trainer(model, optim, ref_config.get_loss_fn(cfg))
+    Et = torch.from_numpy(E)
+    t = lambda a: torch.from_numpy(a.astype(np.int64) if a.dtype == np.int32 else a)
+    train_ld = ref_loader.RayDataLoader(Et, "efuncs", t(tr_v), t(tr_b), t(tr_rgb), None, None, batch, False, True,
+                                        device="cpu")
+    tr.val_data_loader = ref_loader.RayDataLoader(Et, "efuncs", t(va_v), t(va_b), t(va_rgb), None, None, batch,
+                                                  False, False, device="cpu")
+    val_psnr, train_psnr = [], []
+    for epoch in range(12):
+        acc_l2, total = 0.0, 0
+        for b in train_ld:  # shuffle=False: deterministic batch order
+            loss, pred = tr._train_step(b)
+            acc_l2 += torch.nn.functional.mse_loss(pred, b["expected_rgbs"], reduction="sum").item()
+            total += b["expected_rgbs"].shape[0]
+        train_psnr.append(ref_metrics.epoch_psnr(acc_l2 / total))
+        val_psnr.append(tr.evaluate(epoch)[1])
+    d = dict(E=E, tr_vids=tr_v, tr_bary=tr_b, tr_rgb=tr_rgb, va_vids=va_v, va_bary=va_b, va_rgb=va_rgb,
+             val_psnr=np.array(val_psnr), train_psnr=np.array(train_psnr), lr=np.float32(lr), batch=np.int64(batch),
+             k_list=np.array(K_LIST_1023, np.int64))
+    print("g16 val psnr", np.round(d["val_psnr"], 3).tolist())
+    dd = dict(d)
+    dd["tr_vids"], dd["va_vids"] = tr_v.astype(np.int64), va_v.astype(np.int64)
+    spread = _curve_spread(dd, model_cfg("R"), "L1", "g16", bf16=True)
+    save("g16_train_curve_R.npz", **d, **{"spread_" + k: v for k, v in spread.items()})
+
+
 def _uv_grid(nu, nv, jitter, rng):
     """A UV triangulation of the unit square's [0.02, 0.98]^2 (a torus's seamed grid, as
     tests/synthetic_views.py bakes), interior vertices jittered by `jitter` cells."""
@@ -750,3 +874,5 @@ if __name__ == "__main__":
         g13_train_curve_B_L2()
         g14_bake()
         g15_raygen()
+        g12_spread()
+        g16_train_curve_R()

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(inf_hip.lib, name), name
         assert name in inf_hip.EXPORTED, f"{name} has no ctypes signature"
-    assert inf_hip.lib.inf_abi_version() == 2
+    assert inf_hip.lib.inf_abi_version() == 3
 
 
 def reference_layout(k, H, L, s):
@@ -87,3 +87,12 @@ def test_plan_rejects_invalid_architectures(bad):
     rc = inf_hip.lib.inf_plan_create(ctypes.byref(desc), 64, ctypes.byref(h))
     assert rc == -1
     assert b"invalid argument" in inf_hip.lib.inf_last_error()
+
+
+def test_ctrl_layout_matches_header():
+    """inf_ctrl (include/inf_hip.h): the ctypes mirror's field offsets are the C layout (int32
+    step / batch_index / prefetch_index / reserved, then double lr and the four sums)."""
+    from inf_hip import Ctrl
+    assert [(f, getattr(Ctrl, f).offset) for f, _ in Ctrl._fields_] == [
+        ("step", 0), ("batch_index", 4), ("prefetch_index", 8), ("reserved", 12), ("lr", 16), ("loss_sum", 24),
+        ("sse_sum", 32), ("epoch_loss", 40), ("epoch_sse", 48)]

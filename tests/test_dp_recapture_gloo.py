@@ -29,7 +29,7 @@ class _Plan:
         self.params = torch.zeros(P)
         self.exp_avg = torch.zeros(P)
         self.exp_avg_sq = torch.zeros(P)
-        self.ctrl = torch.zeros(48, dtype=torch.uint8)
+        self.ctrl = torch.zeros(56, dtype=torch.uint8)
 
     def make_batch(self, **kw):
         return kw

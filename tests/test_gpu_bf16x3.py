@@ -1,7 +1,9 @@
-"""The split-bf16 parity mode (INF_MODE_BF16X3): fp32 buffers and kernels
-of the fp32 mode, every GEMM inner product from bf16 parts of its operands on bf16 matrix
-cores (plan.hip gemm_mode: the forward GEMMs on six products of a three-part split,
-~2^-24 relative; the backward ones on three of a two-part split, ~2^-16).  Held to the north_star's exact bar against the
+"""The split-bf16 parity mode (INF_MODE_BF16X3): fp32 master weights,
+every GEMM inner product from bf16 parts of its operands on bf16 matrix cores.  The fused
+step (chain3.hip X3) runs the forward and the dX chain on THREE products of a TWO-part split
+(hi hi + hi lo + lo hi, operands hi + bf16(x - hi): 2^-17 relative representation error) and
+the dW GEMM likewise (lgemm SPLIT); the layered fallback (plan.hip gemm_mode) uses the same
+two-part split.  Held to the north_star's exact bar against the
 reference's own fixtures (G2 forward, G3 gradients / one Adam step, G4 20 Adam steps) and
 the fp32 oracle on device-resident rays: predicted RGB within 1e-4 abs, reduced gradients
 within 1e-4 of each tensor's max, Adam weights as the fp32 mode's tests hold them (a
@@ -123,6 +125,8 @@ def test_train_step_rays_bf16x3_matches_oracle():
     # other side; one such flip moves layers.0.0.weight's gradient by up to 7.6e-3 of its
     # max, and elements whose gradient is below ~1e-2 of the max then take a different Adam
     # step (m / sqrt(v) ~ +-1 on step 1): measured 7,624 of its 262,144 elements (2.9 %)
-    # beyond 5e-6 (the fp32-forward chain: 539); every element within 2 lr steps
+    # beyond 5e-6 (the fp32-forward chain: 539); every element within 2 lr steps.  The bar
+    # sits near that measurement (4 %) so a regression inside a loose envelope
+    # still shows
     for n in O.layer_names(L, s):
-        assert_adam_close(got[n], tr.w[n], lr=1e-4, steps=2, name=n, frac=5e-2)
+        assert_adam_close(got[n], tr.w[n], lr=1e-4, steps=2, name=n, frac=4e-2)

@@ -234,6 +234,10 @@ def test_trainer_g8_training_curve(tmp_path, mode, layered, monkeypatch):
         np.testing.assert_allclose(val[:5], d["val_psnr"][:5], atol=1e-3)
         tol = g8_reference_spread()
         assert 0.05 <= tol < 0.2
+        if layered:
+            # the layered kernels track the reference's float64 curve (0.023 dB seen): held
+            # near that, below the spread, so a regression inside it still shows
+            tol = 0.05
     else:
         tol = 0.2
     print(mode, "layered" if layered else "fused", np.round(np.array(val) - d["val_psnr"], 4).tolist(), "bar", tol)
@@ -272,19 +276,80 @@ def test_trainer_g12_curve_config_b(tmp_path):
         curves[mode] = np.array(_val_curve(out))
     ref = d["val_psnr"]
     print({m: np.round(c - ref, 3).tolist() for m, c in curves.items()})
-    # The first epochs follow the reference's trajectory (fp32: 0.002 dB through epoch 3 on
-    # both fp32 paths, then 0.005 (layered kernels) / 0.030 dB (fused fp32 chain) at epochs
-    # 4-5; bf16 0.02 dB); later the trajectories drift apart the same way in both modes (fp32
-    # too: summation-order differences grow through training, ±0.33 dB seen at epochs 5-11),
-    # so the rest is held statistically: every epoch within 0.5 dB, the mean of the last
-    # four within 0.2 dB (0.08 seen in both modes).
-    for mode, early in (("fp32", 0.05), ("bf16", 0.2)):
+    # This L1 run is chaotic: the reference ITSELF, with only its fp32 summation order
+    # changed (1 / 3 / 8 threads, DataParallel over 2 / 4 replicas, float64), moves by up to
+    # 0.545 dB per epoch, and under CPU bf16 autocast by up to 0.39 (g12_spread.npz).  So each
+    # epoch's bar is derived from that spread (g12_reference_envelope), not chosen: fp32 from
+    # the fp32 variants, bf16 from all of them; the early epochs, where the variants agree to
+    # < 3e-3 dB (fp32) / 0.02 dB (bf16), keep a floor of 0.005 / 0.02 dB; a systematic error
+    # would also move the mean of the last four epochs (0.2 dB bar; the variants: <= 0.16).
+    for mode, floor in (("fp32", 0.005), ("bf16", 0.02)):
         c = curves[mode]
-        if mode == "fp32":
-            np.testing.assert_allclose(c[:3], ref[:3], atol=0.005, err_msg=mode)
-        np.testing.assert_allclose(c[:5], ref[:5], atol=early, err_msg=mode)
-        np.testing.assert_allclose(c, ref, atol=0.5, err_msg=mode)
+        bar = np.maximum(g12_reference_envelope(bf16=mode == "bf16"), floor)
+        err = np.abs(c - ref)
+        print(mode, "bar", np.round(bar, 3).tolist())
+        assert (err <= bar).all(), (mode, np.round(err, 3).tolist())
         assert abs(float(np.mean(c[-4:] - ref[-4:]))) < 0.2, mode
+
+
+def g12_reference_envelope(bf16=False):
+    """Per-epoch PSNR bar of the G12 run, derived from the reference's own spread
+    (tests/golden/make_golden.py g12_spread -> g12_spread.npz): at epoch e, 1.5 x the largest
+    |variant - reference| seen at any epoch <= e (a chaotic divergence does not shrink, and
+    the max of a few samples understates the spread's tail) over the fp32 summation-order
+    variants, and with bf16=True also the reference run under CPU bf16 autocast."""
+    s = golden("g12_spread.npz")
+    vs = [v for v in s.files if v != "ref" and (bf16 or not v.startswith("bf16"))]
+    env = np.max([np.abs(s[v] - s["ref"]) for v in vs], axis=0)
+    return 1.5 * np.maximum.accumulate(env)
+
+
+def g16_reference_spread(bf16=False):
+    """The reference's config-R run (g16_train_curve_R.npz) moved by other fp32 summation
+    orders (1 / 3 / 8 threads, DataParallel 2 / 4, float64): at most 0.0016 dB over 12
+    epochs -- not chaotic; bf16=True: under CPU bf16 autocast, at most 0.007 dB."""
+    d = golden("g16_train_curve_R.npz")
+    vs = [v for v in d.files if v.startswith("spread_") and v.startswith("spread_bf16") == bf16]
+    return max(float(np.abs(d[v] - d["val_psnr"]).max()) for v in vs)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16x3", "bf16"])
+def test_trainer_g16_curve_config_r(tmp_path, mode):
+    """The reference's own shipped configuration, exactly (intrinsic_cat.yaml:24-37: k =
+    list(1023) eigenfunction indices, padded to 1024 with zero columns; 6 x 128, skip 3; L1;
+    Adam lr 1e-4; batch 4096): 12 epochs of the reference's synthetic texture reconstruction
+    (G16, made by importing the reference; the cat dataset is not available offline) through
+    trainer.Trainer.  The run is not chaotic -- the reference's own fp32 summation-order
+    variants stay within 0.0016 dB of it, its CPU bf16 autocast within 0.007 dB
+    (g16_reference_spread) -- so every epoch is held to a bar derived from that spread:
+    10 x the fp32 spread for the fp32 and bf16x3 parity modes (0.016 dB), 10 x the bf16
+    spread for bf16 (0.07 dB; this implementation rounds at other points than autocast),
+    with a 0.01 dB floor."""
+    import config
+    from ray_dataloader import RayDataLoader
+    from trainer import Trainer
+    d = golden("g16_train_curve_R.npz")
+    tol = max(10 * g16_reference_spread(bf16=mode == "bf16"), 0.01)
+    assert tol < 0.1  # the bar measures arithmetic, not chaos
+    k = [int(x) for x in d["k_list"]]
+    cfg = {"seed": 0, "data": {"img_height": 8, "img_width": 8},
+           "model": {"k": k, "num_layers": 6, "mlp_hidden_dim": 128, "skip_layer_idx": 3, "kernels": {"mode": mode}},
+           "training": {"out_dir": str(tmp_path), "batch_size": int(d["batch"]), "lr": float(d["lr"]),
+                        "loss_type": "L1", "render_every": 1000, "print_every": 1000, "epochs": 12,
+                        "checkpoint_every": 1000}}
+    E = torch.from_numpy(d["E"])
+    t = lambda a: torch.from_numpy(a)
+    train = RayDataLoader(E, "efuncs", t(d["tr_vids"]), t(d["tr_bary"]), t(d["tr_rgb"]), None, None, int(d["batch"]),
+                          False, True, device="cuda")
+    val = RayDataLoader(E, "efuncs", t(d["va_vids"]), t(d["va_bary"]), t(d["va_rgb"]), None, None, int(d["batch"]),
+                        False, False, device="cuda")
+    torch.manual_seed(0)
+    model, optim = config.get_model_and_optim(cfg, None, "cuda")
+    model.kernel_mode = mode
+    Trainer(model, optim, config.get_loss_fn(cfg), None, {"train": train, "val": val}, None, cfg, "cuda").train()
+    c = np.array(_val_curve(tmp_path))
+    print(mode, np.round(c - d["val_psnr"], 4).tolist(), "bar", tol)
+    np.testing.assert_allclose(c, d["val_psnr"], atol=tol)
 
 
 @pytest.mark.parametrize("mode,tol", [("fp32", 0.05), ("bf16", 0.2)])

@@ -538,9 +538,10 @@ def test_lgemm_k_groups_match_one_group(name, B, monkeypatch):
                                                ("A", 4096, True), ("A", 4096, False), ("R", 2048, True),
                                                ("R", 2048, False), ("B", 8192, True)])
 def test_lgf_update_matches_slab_path(name, B, apply_adam, monkeypatch):
-    """The default bf16 step fuses the update into the dW GEMM (lgemm.hip GT: split-K 1,
-    64 x 64 tiles, each block runs Adam -- or writes the reduced gradient -- on its own tile
-    from the LDS gradient tile; opt-in, INF_LGF=1).  Against the split-K slab path (lgemm into 2
+    """The fused dW + update (lgemm.hip GT, "LGF": split-K 1, 64 x 64 tiles, each block runs
+    Adam -- or writes the reduced gradient -- on its own tile from the LDS gradient tile; the
+    default for k > 1024 (config D, tests/test_gpu_config_d_adam.py), forced here at A / R / B
+    with INF_LGF=1).  Against the split-K slab path (lgemm into 2
     slabs, the separate update launch): the same chain, so the same loss sums bit for bit;
     the gradients differ only in the K-sum's order (split-K 2-4 partials vs one accumulator:
     1e-5 of each tensor's max, seen ~1e-7).  With Adam: ONE step, whose move is

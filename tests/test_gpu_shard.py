@@ -41,11 +41,16 @@ def _assert_same(a, b, what):
         assert np.array_equal(x, y), (what, n, int((x != y).sum()))
 
 
-@pytest.mark.parametrize("name,mode,B", [("B", "bf16", 4096), ("R", "bf16", 2048), ("B", "fp32", 1024)])
-def test_sharded_step_world1_bitwise(name, mode, B):
+@pytest.mark.parametrize("name,mode,B,lgf", [("B", "bf16", 4096, "0"), ("R", "bf16", 2048, "0"),
+                                             ("B", "fp32", 1024, "0"), ("B", "bf16", 4096, "1")])
+def test_sharded_step_world1_bitwise(name, mode, B, lgf, monkeypatch):
     """World 1 (chunks alias the staging, no collective): sharded steps == the all-reduce DP
     step shape (gradient -> Adam + advance) bit for bit: masters and Adam state after the
-    epoch-end gather, the weight images, the loss sums and the ctrl block's counters."""
+    epoch-end gather, the weight images, the loss sums and the ctrl block's counters.
+    lgf "1": the gradient-only step on the fused dW + update path (INF_LGF=1, config D's
+    default), whose leading blocks write the bias items into the staging through their own
+    copy of the work items (that copy kept pre-shard offsets)."""
+    monkeypatch.setenv("INF_LGF", lgf)
     nb = 3
     src, perm = _rays(name, nb * B, seed=33)
     out = {}
@@ -76,14 +81,17 @@ def test_sharded_step_world1_bitwise(name, mode, B):
     assert s[1:] == h[1:] and s[2] == nb
 
 
-@pytest.mark.parametrize("world,name,mode", [(2, "B", "bf16"), (3, "B", "bf16"), (4, "R", "bf16"), (2, "A", "fp32")])
-def test_sharded_step_emulated_ranks_bitwise(world, name, mode):
+@pytest.mark.parametrize("world,name,mode,lgf", [(2, "B", "bf16", "0"), (3, "B", "bf16", "0"), (4, "R", "bf16", "0"),
+                                                (2, "A", "fp32", "0"), (2, "B", "bf16", "1"), (3, "B", "bf16", "1")])
+def test_sharded_step_emulated_ranks_bitwise(world, name, mode, lgf, monkeypatch):
     """`world` ranks emulated on one GPU: rank r trains on its torch.chunk shard of every
     global batch (loss normalised by the global 3 B).  The all-reduce path (sum of the ranks'
     flat gradients -> replicated Adam) and the sharded path (sum of the item-major staging
     buffers -> rank r's chunk -> Adam on its items -> concatenated weight chunks -> every
     rank's images) leave the same bytes on every rank, after three steps and the
-    epoch-end gather.  world 3 / 4: uneven item groups."""
+    epoch-end gather.  world 3 / 4: uneven item groups.  lgf "1": the fused dW + update
+    path (INF_LGF=1) writing the staging."""
+    monkeypatch.setenv("INF_LGF", lgf)
     import dp
     nb, B = 3, 2048
     src, perm = _rays(name, nb * B, seed=44)

@@ -3,7 +3,8 @@ per 8-step replay, HIP events around each, over ~0.5 s of back-to-back replays, 
 after 1 s idle.  Shows how long the GPU takes to reach its sustained step time (what a short
 timed window, e.g. 5 warmup + 20 timed steps, sees instead).
 
-    python tools/step_ramp.py [batch] [replays]
+    python tools/step_ramp.py [batch] [replays] [nb] [-- bench args, e.g. --k 64 --layers 4 --hidden 128
+                                                  --skip 2 --verts 20000 for config A]
 """
 import os
 import sys
@@ -15,12 +16,16 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-R = int(sys.argv[2]) if len(sys.argv) > 2 else 800
-sys.argv = [sys.argv[0]]
+argv = sys.argv[1:]
+rest = argv[argv.index("--") + 1:] if "--" in argv else []
+pos = argv[:argv.index("--")] if "--" in argv else argv
+B = int(pos[0]) if len(pos) > 0 else 4096
+R = int(pos[1]) if len(pos) > 1 else 800
+NB = int(pos[2]) if len(pos) > 2 else 32
+sys.argv = [sys.argv[0]] + rest
 args = bench.parse()
 dev = torch.device("cuda", 0)
-tr = bench.Trainer(args, dev, B, 0, 1)
+tr = bench.Trainer(args, dev, B, 0, 1, nb=NB)
 tr.capture()
 gm = tr.graphs[2]
 
