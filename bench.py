@@ -511,6 +511,29 @@ def config_d_bench(args, device, B=4096, steps=40):
     P = tr.plan.info.num_params
     k_pad = tr.plan.in_pad
     row_bytes = B * 3 * k_pad * 2
+    # the reference's own product (mesh.py:313-324 with the loader's index select): the
+    # B x k feature matrix, row-major only (inf_gather -> gather_rows_kernel), of the same
+    # rays from the same packed bf16 table, into bf16 and into fp32 (the reference's dtype)
+    from inf_hip import runtime as RT
+    Tb = tr.src.table_for(tr.plan)
+    ref_gather = {}
+    for name, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        X = torch.empty((B, k_pad), dtype=dt, device=device)
+        RT.gather(Tb, tr.src.vids, tr.src.bary, ray_idx=tr.perm, offset=0, batch=B, out=X)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            RT.gather(Tb, tr.src.vids, tr.src.bary, ray_idx=tr.perm, offset=0, batch=B, out=X)
+        e1.record()
+        torch.cuda.synchronize()
+        ms_g = e0.elapsed_time(e1) / 20
+        out_bytes = X.numel() * X.element_size()
+        ref_gather[name] = {"ms": ms_g, "table_gbs": row_bytes / (ms_g * 1e-3) / 1e9,
+                            "table_hbm_frac": row_bytes / (ms_g * 1e-3) / 1e9 / HBM_PEAK,
+                            "hbm_gbs": (row_bytes + out_bytes + B * 32) / (ms_g * 1e-3) / 1e9,
+                            "hbm_frac": (row_bytes + out_bytes + B * 32) / (ms_g * 1e-3) / 1e9 / HBM_PEAK}
+        del X
     out = {"config": "human_dense D: k=4096 8x256 skip 4, L2, Adam lr 1e-4, V=500000, bf16 table 4.1 GB",
            "rays_per_step": B, "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s", "path": path,
            "roofline": step_roofline(4096, a.hidden, a.layers, B, P, ms),
@@ -520,7 +543,10 @@ def config_d_bench(args, device, B=4096, steps=40):
                              "table_gbs": row_bytes / (gms * 1e-3) / 1e9,
                              "table_hbm_frac": row_bytes / (gms * 1e-3) / 1e9 / HBM_PEAK,
                              "note": "standalone gather (X and X^T written) of the step's rays; inside the "
-                                     "fused chain the rows go straight to LDS"}}
+                                     "fused chain the rows go straight to LDS"},
+           "reference_gather": dict(ref_gather, note="inf_gather of the step's rays: the B x k feature matrix of "
+                                                     "mesh.py:313-324, row-major only (table rows read once, one "
+                                                     "output write); hbm_gbs counts rows + output + ray records")}
     del tr
     torch.cuda.empty_cache()
     return out

@@ -10,6 +10,8 @@
 // read by the same lanes so their FMAs stay in registers.  The row-major tile is stored
 // straight from registers; the transposed copy (used by the weight-gradient GEMMs) goes
 // through a padded LDS tile so both stores are coalesced.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace inf {
@@ -176,6 +178,120 @@ __global__ __launch_bounds__(GT_THREADS) void gather_kernel(
   store_tile<OutT, VEC>(acc, tile, out, ld_out, rows_out, out_t, ld_out_t);
 }
 
+// Row-major output only (no transposed copy): the reference's own product, the B x k
+// feature matrix (mesh.py:313-324; inf_gather, the render's feature-gather path, the
+// pre-gather slots).  A work item is (ray b, 16-byte chunk c of the table row); consecutive
+// threads take consecutive chunks of one ray, so a wave reads whole 1 KiB runs of each of
+// the three vertex rows and its ray records are wave-uniform (broadcast) loads.  Each thread
+// takes G items (their records first, then all 3 G row chunks) and writes each output chunk
+// whole.  Same arithmetic as gather_kernel: b0 e0, + b1 e1, + b2 e2 (fma).  Measured at
+// config D (4096 rays x 3 rows of a 4.1 GB bf16 table, k = 4096, bf16 output;
+// profiles/r05/gather_variants.txt): G = 1 22.2 us (4.5 TB/s of rows, 6.1 TB/s with the
+// output), G = 2 22.9, G = 4 26.1, G = 8 33.1; non-temporal row loads +4 us; the 64 x 64
+// tile kernel 25.2 us -- more, smaller workgroups keep the HBM queues fuller than deep
+// per-thread batches.
+constexpr int GR_ROWS_ITEMS = 1;
+typedef unsigned int g_u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename TabT, typename OutT, int G, bool NT>
+__global__ __launch_bounds__(GT_THREADS) void gather_rows_kernel(
+    const TabT* __restrict__ table, int64_t V, int k, int64_t table_ld, const void* __restrict__ vids, int vid_dtype,
+    const float* __restrict__ bary, const void* __restrict__ ray_idx, int idx_dtype, int64_t idx_offset,
+    const int32_t* __restrict__ ctrl_batch_index, int64_t num_rays, int64_t num_src, int batch,
+    OutT* __restrict__ out, int64_t ld_out, unsigned nchunk, unsigned total) {
+  constexpr int EPC = 16 / sizeof(TabT);  // table elements per 16-byte chunk
+  int64_t offset = idx_offset;
+  if (ctrl_batch_index != nullptr) offset += (int64_t)(*ctrl_batch_index) * batch;
+  const unsigned stride = gridDim.x * GT_THREADS;
+  const unsigned i0 = blockIdx.x * GT_THREADS * G + threadIdx.x;
+  unsigned bi[G], ci[G];
+  bool live[G];
+  int64_t v0[G], v1[G], v2[G];
+  float w0[G], w1[G], w2[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const unsigned i = i0 + g * GT_THREADS;
+    bi[g] = i / nchunk;
+    ci[g] = i - bi[g] * nchunk;
+    live[g] = false;
+    v0[g] = v1[g] = v2[g] = 0;
+    w0[g] = w1[g] = w2[g] = 0.f;
+    if (i < total && (int)bi[g] < batch && (int)(ci[g] * EPC) < k) {
+      const int64_t row = source_row(ray_idx, idx_dtype, offset, (int)bi[g], num_rays, num_src);
+      if (row >= 0) {
+        v0[g] = vid_at(vids, vid_dtype, 3 * row + 0);
+        v1[g] = vid_at(vids, vid_dtype, 3 * row + 1);
+        v2[g] = vid_at(vids, vid_dtype, 3 * row + 2);
+        w0[g] = bary[3 * row + 0];
+        w1[g] = bary[3 * row + 1];
+        w2[g] = bary[3 * row + 2];
+        // an out-of-range vertex id reads as a zero feature row (never outside the table)
+        live[g] = (uint64_t)v0[g] < (uint64_t)V && (uint64_t)v1[g] < (uint64_t)V && (uint64_t)v2[g] < (uint64_t)V;
+      }
+    }
+  }
+  g_u32x4 e[G][3];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t c = (int64_t)ci[g] * EPC;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) e[g][j] = g_u32x4{0u, 0u, 0u, 0u};
+    if (live[g]) {
+      const g_u32x4* p0 = reinterpret_cast<const g_u32x4*>(table + v0[g] * table_ld + c);
+      const g_u32x4* p1 = reinterpret_cast<const g_u32x4*>(table + v1[g] * table_ld + c);
+      const g_u32x4* p2 = reinterpret_cast<const g_u32x4*>(table + v2[g] * table_ld + c);
+      if constexpr (NT) {  // rows read once: keep them out of the caches
+        e[g][0] = __builtin_nontemporal_load(p0);
+        e[g][1] = __builtin_nontemporal_load(p1);
+        e[g][2] = __builtin_nontemporal_load(p2);
+      } else {
+        e[g][0] = *p0;
+        e[g][1] = *p1;
+        e[g][2] = *p2;
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const unsigned i = i0 + g * GT_THREADS;
+    if (i >= total) continue;
+    float x[EPC];
+    if constexpr (sizeof(TabT) == 4) {
+      // whole vectors bit-cast (a bit_cast of one subscripted element compiles to a load of
+      // element 0 -- DESIGN.md section 7, round 4)
+      const f32x4 a = __builtin_bit_cast(f32x4, e[g][0]), b = __builtin_bit_cast(f32x4, e[g][1]),
+                  d = __builtin_bit_cast(f32x4, e[g][2]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = fmaf(w2[g], d[q], fmaf(w1[g], b[q], w0[g] * a[q]));
+    } else {
+      const bf16x8 a = __builtin_bit_cast(bf16x8, e[g][0]), b = __builtin_bit_cast(bf16x8, e[g][1]),
+                   d = __builtin_bit_cast(bf16x8, e[g][2]);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = fmaf(w2[g], (float)d[q], fmaf(w1[g], (float)b[q], w0[g] * (float)a[q]));
+    }
+    if (!live[g]) {
+#pragma unroll
+      for (int q = 0; q < EPC; ++q) x[q] = 0.f;
+    }
+    OutT* dst = out + (int64_t)bi[g] * ld_out + (int64_t)ci[g] * EPC;
+    if constexpr (sizeof(OutT) == 4) {
+#pragma unroll
+      for (int q = 0; q < EPC; q += 4) *reinterpret_cast<f32x4*>(dst + q) = f32x4{x[q], x[q + 1], x[q + 2], x[q + 3]};
+    } else if constexpr (EPC == 8) {
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (bf16)x[q];
+      *reinterpret_cast<bf16x8*>(dst) = o;
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (bf16)x[q];
+      *reinterpret_cast<bf16x4*>(dst) = o;
+    }
+  }
+  (void)stride;
+}
+
 template <typename TabT, typename OutT>
 int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const void* vids, int vid_dtype,
                  const float* bary, const void* ray_idx, int idx_dtype, int64_t idx_offset, const int32_t* ctrl_bi,
@@ -185,7 +301,34 @@ int launch_typed(const void* table, int64_t V, int k, int64_t table_ld, const vo
   const bool vec = (k % 16 == 0) && (table_ld % 16 == 0) && (ld_out % 16 == 0) &&
                    (out_t == nullptr || ld_out_t % 16 == 0) && ((uintptr_t)table % 16 == 0) &&
                    ((uintptr_t)out % 16 == 0) && ((uintptr_t)out_t % 16 == 0);
-  if (vec) {
+  constexpr int EPC = 16 / sizeof(TabT);
+  const int64_t nchunk = ld_out / EPC, total = (int64_t)rows_out * nchunk;
+  if (vec && out_t == nullptr && total < ((int64_t)1 << 31) && std::getenv("INF_GATHER_TILES") == nullptr) {
+    // row-major only: whole-row chunks (gather_rows_kernel); INF_GATHER_TILES=1 keeps the
+    // 64 x 64 tile kernel (A/B)
+    static const int gsel = [] {
+      const char* e = std::getenv("INF_GATHER_G");
+      return e != nullptr ? std::atoi(e) : GR_ROWS_ITEMS;
+    }();
+    // INF_GATHER_NT=1: non-temporal row loads (measured slower, even for tables above the MALL)
+    const char* ent = std::getenv("INF_GATHER_NT");
+    const bool nt = ent != nullptr && std::atoi(ent) != 0;
+#define INF_GR_LAUNCH(G_, NT_)                                                                                   \
+  gather_rows_kernel<TabT, OutT, G_, NT_><<<dim3((unsigned)ceil_div(total, (int64_t)GT_THREADS * G_)), GT_THREADS, 0, \
+                                            stream>>>((const TabT*)table, V, k, table_ld, vids, vid_dtype, bary,        \
+                                                      ray_idx, idx_dtype, idx_offset, ctrl_bi, num_rays, num_src, batch, \
+                                                      (OutT*)out, ld_out, (unsigned)nchunk, (unsigned)total)
+    if (gsel == 1) {
+      if (nt) INF_GR_LAUNCH(1, true); else INF_GR_LAUNCH(1, false);
+    } else if (gsel == 8) {
+      if (nt) INF_GR_LAUNCH(8, true); else INF_GR_LAUNCH(8, false);
+    } else if (gsel == 2) {
+      if (nt) INF_GR_LAUNCH(2, true); else INF_GR_LAUNCH(2, false);
+    } else {
+      if (nt) INF_GR_LAUNCH(4, true); else INF_GR_LAUNCH(4, false);
+    }
+#undef INF_GR_LAUNCH
+  } else if (vec) {
     gather_kernel<TabT, OutT, true><<<grid, GT_THREADS, 0, stream>>>(
         (const TabT*)table, V, k, table_ld, vids, vid_dtype, bary, ray_idx, idx_dtype, idx_offset, ctrl_bi, num_rays,
         num_src, batch, (OutT*)out, ld_out, rows_out, (OutT*)out_t, ld_out_t);

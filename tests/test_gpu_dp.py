@@ -206,7 +206,7 @@ def test_train_data_parallel_two_ranks_within_summation_order_spread(tmp_path, m
     difference flips a bf16 weight image, so two runs that differ ONLY in summation order
     part over the epochs -- the bar is therefore derived, not chosen: a second single-process
     run whose weight-gradient GEMM sums in another order (fp32: INF_DW_SPLITS=2, split-K 2
-    instead of one accumulator; bf16: INF_LGEMM_KS=2, two interleaved k groups per block)
+    instead of one accumulator; bf16: INF_LGEMM_KS=1, one k group per block instead of two)
     measures how far a pure summation-order change moves this run, and the world-2 run
     (whose only difference is the order of two half-batch gradients) must stay within 10x
     that spread, in weights (relative L2) and in every logged scalar.  A sharding /
@@ -219,7 +219,7 @@ def test_train_data_parallel_two_ranks_within_summation_order_spread(tmp_path, m
     base = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", INF_DP_BACKEND="gloo")
     for key in ("INF_DW_SPLITS", "INF_LGEMM_KS"):
         base.pop(key, None)
-    knob = {"INF_DW_SPLITS": "2"} if mode == "fp32" else {"INF_LGEMM_KS": "2"}
+    knob = {"INF_DW_SPLITS": "2"} if mode == "fp32" else {"INF_LGEMM_KS": "1"}
     single = _run_train(tmp_path, cfg, "single", base, 0)
     reorder = _run_train(tmp_path, cfg, "single_reordered", dict(base, **knob), 0)
     dp2 = _run_train(tmp_path, cfg, "dp2", base, 2)

@@ -80,6 +80,47 @@ def test_gather_bf16_table_and_index():
     np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-5)
 
 
+@pytest.mark.parametrize("tab,out_dt,k,ld", [(torch.float32, torch.float32, 64, 64), (torch.bfloat16, torch.float32, 1024, 1024),
+                                             (torch.bfloat16, torch.bfloat16, 4096, 4096), (torch.float32, torch.bfloat16, 96, 128),
+                                             (torch.bfloat16, torch.bfloat16, 1024, 1152)])
+def test_gather_rows_kernel_matches_tile_kernel(tab, out_dt, k, ld, monkeypatch):
+    """The row-major gather (gather_rows_kernel: whole-row 16-byte chunks, the default when
+    no transposed copy is asked for) against the 64 x 64 tile kernel (INF_GATHER_TILES=1):
+    the same fma order, so bit for bit -- including out-of-range vertex ids and ray-index
+    values (zero rows), columns k..ld-1 and rows past the batch (written as zero)."""
+    rng = np.random.default_rng(12)
+    V, N, B, rows = 500, 3000, 1000, 1040
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32)).to(tab).cuda()
+    vids = rng.integers(0, V, (N, 3))
+    vids[::97, 2] = V + 3
+    bary = torch.from_numpy(rng.dirichlet([1, 1, 1], N).astype(np.float32)).cuda()
+    perm = torch.randperm(N)
+    perm[::131] = N + 9
+    vids_t, perm_t = torch.from_numpy(vids).cuda(), perm.cuda()
+    outs = {}
+    for tag in ("rows", "tiles"):
+        if tag == "tiles":
+            monkeypatch.setenv("INF_GATHER_TILES", "1")
+        out = torch.full((rows, ld), 7.0, dtype=out_dt, device="cuda")
+        from inf_hip import DTYPE_I64, check, lib, runtime as R
+        check(lib.inf_gather(R.ptr(E), R.dtype_code(E), V, k, E.stride(0), R.ptr(vids_t), R.dtype_code(vids_t),
+                             R.ptr(bary), R.ptr(perm_t), DTYPE_I64, 100, B, N, R.ptr(out), R.dtype_code(out), ld,
+                             rows, None, 0, R.stream_handle()), "gather")
+        outs[tag] = out.float().cpu().numpy()
+    assert np.array_equal(outs["rows"], outs["tiles"])
+    assert (outs["rows"][B:] == 0).all() and (outs["rows"][:, k:] == 0).all()
+    idx = perm[100:100 + B].numpy()
+    ok = idx < N
+    vv = np.minimum(np.where(ok[:, None], vids[np.minimum(idx, N - 1)], 0), V - 1)
+    ref = O.gather(E.float().cpu().numpy(), vv, bary.cpu().numpy()[np.minimum(idx, N - 1)])
+    bad = ~ok | (vids[np.minimum(idx, N - 1)] >= V).any(1)
+    ref[bad] = 0
+    if out_dt == torch.float32:
+        np.testing.assert_allclose(outs["rows"][:B, :k], ref, atol=1e-5)
+    else:  # one bf16 rounding of the fp32 sum: half an ulp, 2^-9 relative
+        np.testing.assert_allclose(outs["rows"][:B, :k], ref, rtol=2 ** -8, atol=1e-6)
+
+
 @pytest.mark.parametrize("name", ["A", "R", "B"])
 def test_forward_fp32_golden(name):
     d = golden(f"g2_forward_{name}.npz")
@@ -504,8 +545,8 @@ def test_aux_dw_bitwise(name, B, monkeypatch):
 
 @pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
 def test_lgemm_k_groups_match_one_group(name, B, monkeypatch):
-    """The dW GEMM's two k groups per block (lgemm.hip KS = 2: INF_LGEMM_KS=2 on the bf16 step,
-    the default of the bf16x3 one) against one group (INF_LGEMM_KS=1): the same
+    """The dW GEMM's two k groups per block (lgemm.hip KS = 2, the default since round 5)
+    against one group (INF_LGEMM_KS=1): the same
     products summed as two interleaved halves then added, so every gradient within 1e-5 of
     its tensor's max (fp32 reassociation over <= 2048 rays), and the chain's loss sums equal."""
     monkeypatch.setenv("INF_LGF", "0")
