@@ -92,6 +92,12 @@ struct Chain3Args {
   float inv_count;
   inf_ctrl* ctrl;
   int32_t count_step;
+  // chain4 (large batches, csrc/chain4.hip): the fragment images by role -- W_0, W_y, the
+  // hidden layers' forward images wf[1 .. L-2] (Lx at the skip layer) and backward wb[..]
+  const bf16* w0_img;
+  const bf16* wy_img;
+  const bf16* wf[CHAIN_MAX_HIDDEN];
+  const bf16* wb[CHAIN_MAX_HIDDEN];
   // diagnostics: wall-clock stamps (100 MHz) of wave 0 of the first and the last
   // workgroup: [2][nphase * 5 + 6] = entry, {phase start, MFMAs done, epilogue done} ...,
   // end, weight prologue issued, feature tile written, barrier 0 passed, {after B1} ...,
@@ -155,5 +161,19 @@ inline int chain3_kc(int k_pad, int64_t rows) {
 }
 
 int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream);
+
+// chain4.hip: the large-batch step on 128-ray workgroups of four waves (one per SIMD, the
+// whole register file each), the 8-layer H = 256 field (configs B / C / D / E) above
+// CHAIN3_MAX_ROWS.  Opt-in (INF_CHAIN4=1): measured slower than chain3's 64-ray tiles at
+// 65536 rays (533 vs 344 us of chain; tools/chain4_timing.py)
+constexpr int C4_BM = 128;
+constexpr int C4_KC = 128;  // feature columns gathered per chunk
+constexpr int C4_STAMPS = 192;  // diagnostics: wall-clock stamps per stamped workgroup
+inline bool chain4_supported(int H, int L, int k_pad, int64_t rows) {
+  return H == 256 && L == 8 && k_pad % C4_KC == 0 && rows % C4_BM == 0 && rows > CHAIN3_MAX_ROWS &&
+         rows <= CHAIN3_WIDE_MAX_ROWS && std::getenv("INF_CHAIN4") != nullptr &&
+         std::getenv("INF_CHAIN4")[0] == '1';
+}
+int launch_chain4(const Chain3Args& a, hipStream_t stream);
 
 }  // namespace inf

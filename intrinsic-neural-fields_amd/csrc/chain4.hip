@@ -1,0 +1,693 @@
+// Large-batch fused training chain (chain3.hip's step, re-tiled for batches above
+// CHAIN3_MAX_ROWS): gather -> forward -> head + loss -> dX chain for 128 rays per workgroup,
+// leaving the X^T / Y^T / dZ^T fragment images and the bias / head / loss partials the dW
+// GEMM (fgemm.hip) and the update launch read -- the same outputs as chain3's wide tiles.
+//
+// Why a second kernel.  chain3's wide tiles (64 rays, 8 compute waves + a store wave, two
+// waves per SIMD) cap every wave at 168 VGPRs: four ray tiles of accumulators, W_y x parked
+// in LDS, epilogues that no other work covers -- 75 us per 64-ray workgroup at 65,536 rays
+// against ~17 us of MFMA work.  Here a workgroup is FOUR waves, one per SIMD, each with the
+// whole 512-register file: wave w owns output features [64 w, 64 w + 64) (TN = 4 tiles of
+// 16) for all RT = 8 ray tiles, so every weight fragment fetched from L2 feeds 8 MFMAs
+// (chain3 wide: 4) and a k block is 32 independent MFMAs (512 cycles) -- enough to cover
+// the fragment ring and the B-operand LDS reads without a second wave on the SIMD.  Both
+// input layers' accumulator sets (W_0 x and W_y x, 2 x 128 fp32 per lane) stay in
+// registers from phase 0 to the skip layer, so the feature tile is gathered once per step
+// in 128-column chunks (32 KiB) and read by both input layers.
+//
+// One activation buffer (64 KiB for 128 rays x 256 features): an epilogue writes the next
+// layer's input into the tile the layer just read, behind a barrier that ends the reads
+// (B1), and a second barrier publishes it (B2).  The X^T / Y^T / dZ^T images are copied by
+// all four waves out of the LDS tiles (ds_read_b64_tr_b16 transposes, whole-line write-
+// through stores) right after B2, i.e. while the next phase's fragments are in flight.
+//
+// Numerics are chain3's chunked wide schedule's: the same MFMA k order for W_0 x and W_y x
+// (two fp32 sums, added in the skip epilogue with the biases last), bf16-rounded ReLU
+// outputs, the head, loss and dL/dz in fp32.  Only the fp32 summation orders of the head's
+// dot products and of the per-workgroup partials differ (128 rays, 4 waves).
+#include <cstdlib>
+#include <utility>
+
+#include "c3common.hpp"
+#include "chain3.hpp"
+
+namespace inf {
+namespace {
+
+using namespace c3;
+
+constexpr float C4_CAUCHY_C2 = (20.f / 255.f) * (20.f / 255.f);
+
+// f(integral_constant<int, I>) for I = 0 .. N-1: a k-block loop whose ring slot (I % D) is
+// a compile-time constant, so the fragment registers are statically indexed
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// 1 if x != 0 else 0, as one v_min_u32 (a compare would put its lane mask in an SGPR pair)
+__device__ __forceinline__ unsigned nz1_4(unsigned x) {
+  unsigned r;
+  asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+template <int NL>
+struct L4 {
+  static constexpr int H = 256, CW = 4, THREADS = CW * 64;
+  static constexpr int RT = C4_BM / 16;           // 16-ray MFMA tiles per workgroup
+  static constexpr int BM = C4_BM;
+  static constexpr int TN = H / (16 * CW);        // 16-feature tiles per wave (4)
+  static constexpr int UPL = H / 32;              // k blocks per hidden layer (8)
+  static constexpr int NT = H / 16;               // 16-row tiles per k block of a hidden image
+  static constexpr int KC = C4_KC;                // feature columns per gathered chunk
+  static constexpr int KBC = KC / 32;             // k blocks per chunk (4)
+  static constexpr int TILE_BYTES = 16 * H * 2;   // one 16-ray activation tile (act_off layout)
+  static constexpr int ACT_BYTES = RT * TILE_BYTES;
+  static constexpr int XROW = KC * 2;             // bytes per ray row of the feature chunk
+  static constexpr int OFF_ACT = 0;
+  static constexpr int OFF_X = OFF_ACT + ACT_BYTES;                   // [BM][KC] bf16 (tile_off swizzle)
+  static constexpr int OFF_VEC = OFF_X + BM * XROW;                   // biases [NL-1][H], Ly.bias [H]
+  static constexpr int OFF_W7 = OFF_VEC + NL * H * 4;                 // [3][H], b7[3]
+  static constexpr int OFF_ZP = OFF_W7 + 3 * H * 4 + 16;              // [CW][BM][3] head partial dots
+  static constexpr int OFF_DZ = OFF_ZP + CW * BM * 12;                // [CW][BM][3] dL/dz (a copy per wave)
+  static constexpr int OFF_TGT = OFF_DZ + CW * BM * 12;               // [BM][3] targets
+  static constexpr int OFF_PRED = OFF_TGT + BM * 12;                  // [BM][3]
+  static constexpr int OFF_RAY = OFF_PRED + BM * 12;                  // [BM][4] vertex ids, [BM][3] ok
+  static constexpr int OFF_RBARY = OFF_RAY + BM * 16 + BM * 12;       // [BM][3] barycentrics
+  static constexpr int OFF_LS = OFF_RBARY + BM * 12;                  // [2] f64 loss / SSE
+  static constexpr int LDS = OFF_LS + 16;
+  static_assert(OFF_VEC % 16 == 0 && OFF_W7 % 16 == 0 && OFF_LS % 8 == 0, "LDS alignment");
+  static_assert(LDS <= 160 * 1024, "chain4: LDS budget");
+};
+
+// NL = num_layers (one instantiation: the 8-layer field of configs B / C / D / E)
+template <int NL, int LOSS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void chain4_kernel(const Chain3Args a) {
+  using C = L4<NL>;
+  constexpr int H = C::H, RT = C::RT, BM = C::BM, TN = C::TN, UPL = C::UPL, KBC = C::KBC, CW = C::CW;
+  constexpr int NV = TN * 4;          // accumulator values per lane and ray tile
+#ifndef C4_D
+#define C4_D 4
+#endif
+  constexpr int D = C4_D;             // fragment ring depth (k blocks in flight)
+  constexpr int MST = NL - 2;         // ReLU masks kept: Y_0 .. Y_{NL-3}
+  static_assert(UPL % D == 0 && KBC % D == 0, "ring slots are static per k block");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = a.s, k_pad = a.k_pad;
+  char* act = smem + C::OFF_ACT;
+  char* xs = smem + C::OFF_X;
+  float* vecs = reinterpret_cast<float*>(smem + C::OFF_VEC);
+  float* w7s = reinterpret_cast<float*>(smem + C::OFF_W7);
+  float* zps = reinterpret_cast<float*>(smem + C::OFF_ZP);
+  float* dzs = reinterpret_cast<float*>(smem + C::OFF_DZ);
+  float* tgs = reinterpret_cast<float*>(smem + C::OFF_TGT);
+  float* preds = reinterpret_cast<float*>(smem + C::OFF_PRED);
+  int* rvid = reinterpret_cast<int*>(smem + C::OFF_RAY);
+  float* rbary = reinterpret_cast<float*>(smem + C::OFF_RBARY);
+  double* lss = reinterpret_cast<double*>(smem + C::OFF_LS);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wc = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int b0 = blockIdx.x * BM;
+  const int64_t part0 = blockIdx.x;  // one partial per workgroup
+  const int t0 = wc * TN;           // the wave's first 16-feature tile
+  // diagnostics (tools/chain4_timing.py): wave 0 of the first and the last workgroup stamps
+  // the wall clock (100 MHz) at every step of its schedule, C4_STAMPS slots each
+  unsigned long long* stl = nullptr;
+  if (a.stamps != nullptr && wc == 0 && lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    stl = a.stamps + (blockIdx.x == 0 ? 0 : C4_STAMPS);
+  int nst = 0;
+  auto stamp = [&]() {
+    if (stl != nullptr) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (nst < C4_STAMPS) stl[nst] = wall_clock64();
+      ++nst;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp();  // entry
+
+  // ---- ray records, targets, vectors ----------------------------------------------------
+  int64_t offset = a.idx_offset;
+  if (a.ctrl != nullptr && a.offset_from_ctrl) offset += (int64_t)a.ctrl->batch_index * a.batch;
+  for (int x = tid; x < BM * 3; x += C::THREADS) {
+    const int rl = x / 3, i = x % 3;
+    const int b = b0 + rl;
+    int v = 0, ok = 0;
+    float w = 0.f, tt = 0.f;
+    const int64_t rr = b < a.batch ? source_row(a.ray_idx, a.idx_dtype, offset, b, a.num_rays, a.num_src) : -1;
+    if (rr >= 0) {
+      const int64_t e = vid_at(a.vids, a.vid_dtype, 3 * rr + i);
+      ok = (uint64_t)e < (uint64_t)a.num_vertices;  // an out-of-range id reads as a zero row
+      v = ok ? (int)e : 0;
+      w = a.bary[3 * rr + i];
+      tt = a.rgb[3 * rr + i];
+    }
+    rvid[rl * 4 + i] = v;
+    rbary[rl * 3 + i] = w;
+    rvid[BM * 4 + x] = ok;
+    tgs[x] = tt;
+  }
+  for (int i = tid; i < (NL - 1) * H; i += C::THREADS) vecs[i] = a.bias[i / H][i % H];
+  for (int i = tid; i < H; i += C::THREADS) vecs[(NL - 1) * H + i] = a.bias_y[i];
+  for (int i = tid; i < 3 * H + 3; i += C::THREADS) w7s[i] = i < 3 * H ? a.W7[i] : a.b7[i - 3 * H];
+  if (a.count_step && blockIdx.x == 0 && tid == 0) a.ctrl->step += 1;
+
+  // ---- the weight stream: k block i of the step's sequence --------------------------------
+  //   phase 0, chunk c: W_0 k blocks 4c .. 4c+3, then W_y 4c .. 4c+3 (i < P0 = 2 k_pad / 32)
+  //   forward layers l = 1 .. NL-2: W_l k blocks 0..7 (the skip layer: Lx)
+  //   backward l = NL-2 .. 1: W_l^T k blocks 0..7
+  const int nkx = k_pad / 32, P0 = 2 * nkx;
+  const int nseq = P0 + 2 * (NL - 2) * UPL;
+  const unsigned lane_off = (unsigned)(t0 * 64 + lane) * 16u;
+  auto frag_i = [&](int i, bf16x8 (&dst)[TN]) {
+    i = i < nseq ? i : nseq - 1;  // past the end: harmless reloads keep the waits exact
+    const bf16* img;
+    int kb, ntile;
+    if (i < P0) {
+      const int c = i / (2 * KBC), j = i % (2 * KBC);
+      img = j < KBC ? a.w0_img : a.wy_img;
+      kb = c * KBC + (j % KBC);
+      ntile = C::NT;
+    } else if (i < P0 + (NL - 2) * UPL) {
+      const int q = i - P0;
+      img = a.wf[1 + q / UPL];
+      kb = q % UPL;
+      ntile = C::NT;
+    } else {
+      const int q = i - P0 - (NL - 2) * UPL;
+      img = a.wb[(NL - 2) - q / UPL];
+      kb = q % UPL;
+      ntile = C::NT;
+    }
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(img), (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      dst[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + j * 1024,
+                                                                                  kb * ntile * 1024, 0));
+  };
+  bf16x8 fr[D][TN];
+#pragma unroll
+  for (int kb = 0; kb < D; ++kb) {
+    frag_i(kb, fr[kb]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---- LDS tile helpers ------------------------------------------------------------------
+  int aoffs[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) aoffs[q] = act_off(q, r16, g4) - q * 1024;
+  auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
+  auto put_act = [&](const float (&v)[TN][4], char* tile) {
+#pragma unroll
+    for (int j = 0; j < TN; j += 2) {
+      u32x4 w;
+      w[0] = pack_bf16x2(v[j][0], v[j][1]);
+      w[1] = pack_bf16x2(v[j][2], v[j][3]);
+      w[2] = pack_bf16x2(v[j + 1][0], v[j + 1][1]);
+      w[3] = pack_bf16x2(v[j + 1][2], v[j + 1][3]);
+      *reinterpret_cast<u32x4*>(tile + act_off((t0 + j) >> 1, r16, g4)) = w;
+    }
+  };
+  auto get_act = [&](float (&v)[TN][4], const char* tile) {
+#pragma unroll
+    for (int j = 0; j < TN; j += 2) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(tile + act_off((t0 + j) >> 1, r16, g4));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[j + q / 2][2 * (q % 2)] = __builtin_bit_cast(float, w[q] << 16);
+        v[j + q / 2][2 * (q % 2) + 1] = __builtin_bit_cast(float, w[q] & 0xFFFF0000u);
+      }
+    }
+  };
+  // sums over the 16 rays (lanes of a row) of per-lane values -> the owner lane of feature
+  // feat(idx / 4) + idx % 4 returns it (lanes r16 < NV)
+  auto ray_sums = [&](const float (&v)[TN][4], int& fo) -> float {
+    float t[NV];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[j * 4 + r] = v[j][r];
+    const float sm = ray_sum<NV>(t, lane);
+    const int idx = r16 % NV;
+    fo = feat(idx >> 2) + (idx & 3);
+    return sm;
+  };
+
+  // ---- fragment images for the dW GEMM out of an LDS tile (chain3's store wave's copy) ----
+  // a 16-lane group reads 4 rays x 16 features with ds_read_b64_tr_b16 (lane 4 q + p: ray
+  // q's features 4 p .. 4 p + 3; lane i receives feature i of the 4 rays); one store
+  // instruction writes the 512-byte pieces of 16-feature tiles 2 u and 2 u + 1 of a 16-ray
+  // tile (whole lines, write-through: the next launch reads them)
+  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3, trh = tg & 1;
+  const int64_t img_lane = (int64_t)(ti + 16 * trh) * 16;
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto tr_read = [&](const char* p8) -> s16x4 { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p8)); };
+  // units (n, u): ray tile n, tile pair u of R / 32 pairs in [u_begin, u_end); wave wc takes
+  // every CW-th unit.  addr(t, n, ray, quad): LDS address of features 16 t + 4 quad .. of
+  // `ray` of ray tile n.
+  auto copy_image = [&](auto addr, int R, bf16* img, int u_begin, int u_end) {
+    const int nu = u_end - u_begin;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(img, (short)0, 0x7FFFFFFF, 0x00020000);
+    constexpr int NB = 4;
+#pragma unroll 1
+    for (int q0 = wc; q0 < RT * nu; q0 += CW * NB) {
+      s16x4 lo[NB], hi[NB];
+#pragma unroll
+      for (int v = 0; v < NB; ++v) {
+        const int q = min(q0 + v * CW, RT * nu - 1);
+        const int n = q / nu, t = 2 * (u_begin + q % nu) + (tg >> 1);
+        lo[v] = tr_read(addr(t, n, 8 * trh + tq, tp));
+        hi[v] = tr_read(addr(t, n, 8 * trh + 4 + tq, tp));
+      }
+#pragma unroll
+      for (int v = 0; v < NB; ++v) {
+        const int q = q0 + v * CW;
+        if (q < RT * nu) {
+          const int n = q / nu, t = 2 * (u_begin + q % nu) + (tg >> 1);
+          const int b0n = b0 + 16 * n;
+          const int64_t off = (int64_t)(b0n >> 5) * (R / 16) * 1024 + ((b0n >> 4) & 1) * 512 + img_lane + (int64_t)t * 1024;
+          const s16x4x8 o = {lo[v][0], lo[v][1], lo[v][2], lo[v][3], hi[v][0], hi[v][1], hi[v][2], hi[v][3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rd, (unsigned)off, 0, 16);
+        }
+      }
+    }
+  };
+  auto act_addr = [&](int t, int n, int r, int q) -> const char* {
+    return act + n * C::TILE_BYTES + act_off(t >> 1, r, q) + 8 * (t & 1);
+  };
+
+  // ---- the feature chunk: columns [c KC, c KC + KC) of the 128 rays into LDS -------------
+  // 16-byte pieces (8 columns) per thread, fp32 FMA in the reference order b0 e0 + b1 e1 +
+  // b2 e2, one bf16 rounding (the gather kernel's numerics); all loads of a round first
+  const __amdgpu_buffer_rsrc_t rtab =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.table), (short)0, (int)0xFFFFFFFFu, 0x00020000);
+  auto gather_chunk = [&](int c) {
+#ifndef C4_GR
+#define C4_GR 4
+#endif
+    constexpr int CPR = C::KC / 8, NCH = BM * CPR, GR = C4_GR;
+    const int col0 = c * C::KC;
+#pragma unroll 1
+    for (int q0 = tid; q0 < NCH; q0 += C::THREADS * GR) {
+      u16x8 ev[GR][3];
+      float wv[GR][3];
+      int okv[GR];
+#pragma unroll
+      for (int g = 0; g < GR; ++g) {
+        const int q = q0 + C::THREADS * g;  // NCH is a multiple of THREADS * GR
+        const int r = q / CPR, ch = q % CPR;
+        okv[g] = rvid[BM * 4 + r * 3] & rvid[BM * 4 + r * 3 + 1] & rvid[BM * 4 + r * 3 + 2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          wv[g][i] = rbary[r * 3 + i];
+          if (a.table_big) {
+            const bf16* src = a.table + (int64_t)rvid[r * 4 + i] * k_pad + col0 + ch * 8;
+            ev[g][i] = __builtin_bit_cast(u16x8, *reinterpret_cast<const u32x4*>(src));
+          } else {
+            const unsigned off = ((unsigned)rvid[r * 4 + i] * (unsigned)k_pad + col0 + ch * 8) * 2u;
+            ev[g][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rtab, off, 0, 0));
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < GR; ++g) {
+        const int q = q0 + C::THREADS * g;
+        const int r = q / CPR, ch = q % CPR;
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = fmaf(wv[g][2], bf_val3(ev[g][2][e]), fmaf(wv[g][1], bf_val3(ev[g][1][e]), wv[g][0] * bf_val3(ev[g][0][e])));
+          o[e] = bf_bits3(okv[g] ? x : 0.f);
+        }
+        *reinterpret_cast<u16x8*>(xs + r * C::XROW + ((ch ^ (r & 15)) << 4)) = o;
+      }
+    }
+  };
+  auto x_addr = [&](int t, int n, int r, int q) -> const char* {  // t: tile within the chunk
+    return xs + (16 * n + r) * C::XROW + (((2 * t + (q >> 1)) ^ (r & 15)) << 4) + 8 * (q & 1);
+  };
+
+  // ---- accumulators, ReLU masks ------------------------------------------------------------
+  f32x4 acc[RT][TN], accy[RT][TN];
+#pragma unroll
+  for (int n = 0; n < RT; ++n)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      accy[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  // masks of Y_0 .. Y_{NL-3}: bit (n NV + j 4 + r) of word n / 2 ... kept as a stack (the
+  // forward pushes in layer order, the backward pops in reverse: static register indices)
+  unsigned mst[MST][RT / 2];
+#pragma unroll
+  for (int i = 0; i < MST; ++i)
+#pragma unroll
+    for (int w = 0; w < RT / 2; ++w) mst[i][w] = 0u;
+
+  // one k block of the stream: global index i (its fragments in slot i % D), B operand
+  // from the feature chunk (kx: its k block inside the chunk) or the activation tile
+  // (ka: k block of the tile); the slot is refilled with k block i + D
+  auto kblock = [&](f32x4 (&tgt)[RT][TN], auto SLOTc, const int i, const bool from_x, const int kbl) {
+    constexpr int slot = decltype(SLOTc)::value;
+    auto bread = [&](int n) -> bf16x8 {
+      if (from_x) return *reinterpret_cast<const bf16x8*>(xs + (16 * n + r16) * C::XROW + (((kbl * 4 + g4) ^ r16) << 4));
+      return *reinterpret_cast<const bf16x8*>(act + n * C::TILE_BYTES + kbl * 1024 + aoffs[kbl & 3]);
+    };
+    bf16x8 bq[2];
+    bq[0] = bread(0);
+#pragma unroll
+    for (int n = 0; n < RT; ++n) {
+      if (n + 1 < RT) bq[(n + 1) & 1] = bread(n + 1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        tgt[n][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[slot][j], bq[n & 1], tgt[n][j], 0, 0, 0);
+    }
+    frag_i(i + D, fr[slot]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  lbar();  // records, targets, vectors in LDS
+  stamp();
+
+  // ================= phase 0: both input layers over the gathered feature chunks ==========
+  const int nchunk = k_pad / C::KC;
+#pragma unroll 1
+  for (int c = 0; c < nchunk; ++c) {
+    if (c > 0) lbar();  // every wave is done with the previous chunk (MFMA reads, X^T copy)
+    gather_chunk(c);
+    lbar();  // chunk c in LDS
+    stamp();
+    // X^T of the chunk for the dW of W_0 and W_y (feature tiles c KC / 16 ..)
+    {
+      auto xa = [&](int t, int n, int r, int q) -> const char* { return x_addr(t - c * (C::KC / 16), n, r, q); };
+      copy_image(xa, k_pad, a.XT, c * (C::KC / 32), (c + 1) * (C::KC / 32));
+    }
+    stamp();
+    const int i0 = c * 2 * KBC;
+    sfor<KBC>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, i0 + KB, true, KB); });
+    sfor<KBC>([&](auto KB) {
+      kblock(accy, std::integral_constant<int, (KBC + decltype(KB)::value) % D>{}, i0 + KBC + KB, true, KB);
+    });
+    stamp();
+  }
+
+  // ---- forward epilogue of layer l: bias (+ W_y x and Ly.bias at the skip layer) + ReLU ---
+  // -> the activation tile (B1 before: every wave's reads of the tile are done), the masks
+  auto fwd_epilogue = [&](int l) {
+    const bool skip = l == s;
+    unsigned bits[RT / 2];
+#pragma unroll
+    for (int w = 0; w < RT / 2; ++w) bits[w] = 0u;
+    lbar();  // B1
+    stamp();
+#pragma unroll
+    for (int n = 0; n < RT; ++n) {
+      float hq[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+        f32x4 z = acc[n][j];
+        if (skip) {
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (NL - 1) * H + feat(j));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[r] = ((z[r] + accy[n][j][r]) + bv[r]) + yv[r];
+        } else {
+          z += bv;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const unsigned w = pack_bf16x2(relu1(z[r]), relu1(z[r + 1]));
+          hq[j][r] = __builtin_bit_cast(float, w << 16);
+          hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
+          // h > 0 <=> the bf16 bits without the sign are nonzero
+          bits[n / 2] |= nz1_4(w & 0x7FFFu) << ((n % 2) * NV + j * 4 + r);
+          bits[n / 2] |= nz1_4(w & 0x7FFF0000u) << ((n % 2) * NV + j * 4 + r + 1);
+        }
+        acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      put_act(hq, act + n * C::TILE_BYTES);
+    }
+#pragma unroll
+    for (int i = MST - 1; i > 0; --i)
+#pragma unroll
+      for (int w = 0; w < RT / 2; ++w) mst[i][w] = mst[i - 1][w];
+#pragma unroll
+    for (int w = 0; w < RT / 2; ++w) mst[0][w] = bits[w];
+    lbar();  // B2: the next layer's input complete
+    stamp();
+    if (l <= NL - 3) copy_image(act_addr, H, a.YT[l], 0, H / 32);  // Y_l^T
+    stamp();
+  };
+
+  fwd_epilogue(0);
+  int seq = P0;  // stream position
+#pragma unroll 1
+  for (int l = 1; l <= NL - 3; ++l) {
+    sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, seq + KB, false, KB); });
+    seq += UPL;
+    stamp();
+    fwd_epilogue(l);
+  }
+
+  // ================= the last hidden layer, the head, the loss, the head backward =========
+  sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, seq + KB, false, KB); });
+  seq += UPL;
+  stamp();
+  {
+    const int l = NL - 2;
+    const bool skip = l == s;
+    lbar();  // B1: the tile's reads are done (it takes this layer's activations next)
+    // ReLU activations of the last hidden layer (bf16) into the tile, the head's partial
+    // dot products over this wave's features into zps
+#pragma unroll
+    for (int n = 0; n < RT; ++n) {
+      float hq[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+        f32x4 z = acc[n][j];
+        if (skip) {
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (NL - 1) * H + feat(j));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[r] = ((z[r] + accy[n][j][r]) + bv[r]) + yv[r];
+        } else {
+          z += bv;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const unsigned w = pack_bf16x2(relu1(z[r]), relu1(z[r + 1]));
+          hq[j][r] = __builtin_bit_cast(float, w << 16);
+          hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
+        }
+        acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        float z = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
+        }
+        z = col_sum4(z);
+        if (g4 == 0) zps[(wc * BM + 16 * n + r16) * 3 + o] = z;
+      }
+      put_act(hq, act + n * C::TILE_BYTES);
+    }
+    lbar();  // Bh: every wave's head partial sums complete
+    stamp();
+    // sigmoid, loss and dL/dz (model.py:89-94, config.py:113-122, trainer.py:76): every wave
+    // computes all BM x 3 of them into its own copy of dz (same-wave LDS order only)
+    {
+      float* dzw = dzs + wc * BM * 3;
+      float lsum = 0.f, ssum = 0.f;
+#pragma unroll 1
+      for (int e0 = 0; e0 < BM * 3; e0 += 64) {
+        const int e = e0 + lane;
+        const int b = b0 + e / 3, o = e % 3;
+        float z = w7s[3 * H + o];
+#pragma unroll
+        for (int w = 0; w < CW; ++w) z += zps[w * BM * 3 + e];
+        const float pv = 1.f / (1.f + expf(-z));
+        float dz = 0.f;
+        if (b < a.batch) {
+          const float d = pv - tgs[e];
+          float lv, g;
+          if constexpr (LOSS == INF_LOSS_L2) {
+            lv = d * d;
+            g = 2.f * d;
+          } else if constexpr (LOSS == INF_LOSS_L1) {
+            lv = fabsf(d);
+            g = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+          } else {
+            const float qq = d * d / C4_CAUCHY_C2;
+            lv = C4_CAUCHY_C2 * logf(1.f + qq);
+            g = 2.f * d / (1.f + qq);
+          }
+          dz = (g * a.inv_count) * (1.f - pv) * pv;
+          lsum += lv;
+          ssum += d * d;
+        }
+        dzw[e] = dz;
+        if (wc == 0) preds[e] = pv;
+      }
+      if (wc == 0) {
+        lsum = col_sum4(row_sum16(lsum));
+        ssum = col_sum4(row_sum16(ssum));
+        if (lane == 0) {
+          lss[0] = lsum;
+          lss[1] = ssum;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's dz writes
+    }
+    // head backward: dZ_{L-2} = (dz W7) * (h > 0) into the tile (each lane its own slots),
+    // its ray sums (the bias partial), the output layer's weight-gradient partials
+    float cst[TN][4], hst[3][TN][4], dbs[3];
+#pragma unroll
+    for (int n = 0; n < RT; ++n) {
+      float dzr[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) dzr[o] = dzs[wc * BM * 3 + (16 * n + r16) * 3 + o];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) dbs[o] = n == 0 ? dzr[o] : dbs[o] + dzr[o];
+      float hq[TN][4];
+      get_act(hq, act + n * C::TILE_BYTES);
+      float gv[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(w7s + 0 * H + feat(j));
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(w7s + 1 * H + feat(j));
+        const f32x4 w2 = *reinterpret_cast<const f32x4*>(w7s + 2 * H + feat(j));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = fmaf(dzr[2], w2[r], fmaf(dzr[1], w1[r], dzr[0] * w0[r]));
+          gv[j][r] = hq[j][r] > 0.f ? g : 0.f;
+        }
+      }
+      put_act(gv, act + n * C::TILE_BYTES);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          cst[j][r] = n == 0 ? gv[j][r] : cst[j][r] + gv[j][r];
+#pragma unroll
+          for (int o = 0; o < 3; ++o) hst[o][j][r] = n == 0 ? dzr[o] * hq[j][r] : fmaf(dzr[o], hq[j][r], hst[o][j][r]);
+        }
+    }
+    if (wc == 0) {
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        const float db = row_sum16(dbs[o]);
+        if (lane == 0) a.hb_part[part0 * 3 + o] = db;
+      }
+    }
+    {
+      int fo;
+      const float sm = ray_sums(cst, fo);
+      if (r16 < NV) a.colsum[NL - 2][part0 * H + fo] = sm;
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        const float sh = ray_sums(hst[o], fo);
+        if (r16 < NV) a.hw_part[(part0 * 3 + o) * H + fo] = sh;
+      }
+    }
+    lbar();  // B2: dZ_{L-2} complete
+    stamp();
+    if (tid < 2 && a.loss_part != nullptr) a.loss_part[2 * part0 + tid] = lss[tid];
+    if (a.pred != nullptr)
+      for (int e = tid; e < BM * 3; e += C::THREADS)
+        if (b0 + e / 3 < a.batch) a.pred[(int64_t)b0 * 3 + e] = preds[e];
+    copy_image(act_addr, H, a.dZT[NL - 2], 0, H / 32);
+    stamp();
+  }
+
+  // ================= backward: dX of layers NL-2 .. 1 ======================================
+#pragma unroll 1
+  for (int l = NL - 2; l >= 1; --l) {
+    sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, seq + KB, false, KB); });
+    seq += UPL;
+    stamp();
+    // dZ_{l-1} = acc * (Y_{l-1} > 0): the mask stack's top
+    unsigned bits[RT / 2];
+#pragma unroll
+    for (int w = 0; w < RT / 2; ++w) bits[w] = mst[0][w];
+#pragma unroll
+    for (int i = 0; i + 1 < MST; ++i)
+#pragma unroll
+      for (int w = 0; w < RT / 2; ++w) mst[i][w] = mst[i + 1][w];
+    float cst[TN][4];
+    lbar();  // B1
+    stamp();
+#pragma unroll
+    for (int n = 0; n < RT; ++n) {
+      float v[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[j][r] = ((bits[n / 2] >> ((n % 2) * NV + j * 4 + r)) & 1u) ? acc[n][j][r] : 0.f;
+          cst[j][r] = n == 0 ? v[j][r] : cst[j][r] + v[j][r];
+        }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      put_act(v, act + n * C::TILE_BYTES);
+    }
+    {
+      int fo;
+      const float sm = ray_sums(cst, fo);
+      if (r16 < NV) a.colsum[l - 1][part0 * H + fo] = sm;
+    }
+    lbar();  // B2
+    stamp();
+    copy_image(act_addr, H, a.dZT[l - 1], 0, H / 32);
+    stamp();
+  }
+  stamp();  // end
+}
+
+template <int NL, int LOSS>
+int launch_typed(const Chain3Args& a, hipStream_t stream) {
+  using C = L4<NL>;
+  static bool attr = false;
+  if (!attr) {
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)chain4_kernel<NL, LOSS>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
+    attr = true;
+  }
+  chain4_kernel<NL, LOSS><<<dim3((unsigned)(a.rows / C::BM)), dim3(C::THREADS), C::LDS, stream>>>(a);
+  INF_LAUNCH_CHECK();
+  return INF_OK;
+}
+
+}  // namespace
+
+int launch_chain4(const Chain3Args& a_in, hipStream_t stream) {
+  Chain3Args a = a_in;
+  a.table_big = a.num_vertices * (int64_t)a.k_pad * 2 >= ((int64_t)1 << 32);
+  INF_CHECK_ARG(chain4_supported(a.H, a.L, a.k_pad, a.rows), "chain4: unsupported shape");
+  INF_CHECK_ARG(a.encoding == INF_ENC_NONE && a.xpre == nullptr && !a.x3 && a.zin == nullptr,
+                "chain4: eigenfunction-table batches only");
+  INF_CHECK_ARG(a.table != nullptr && a.vids != nullptr && a.bary != nullptr && a.rgb != nullptr && a.XT != nullptr,
+                "chain4: inputs");
+  INF_CHECK_ARG(a.vid_dtype == INF_DTYPE_I32 || a.vid_dtype == INF_DTYPE_I64, "chain4: vertex id dtype");
+  INF_CHECK_ARG(a.w0_img != nullptr && a.wy_img != nullptr, "chain4: input-layer images");
+  for (int l = 1; l <= a.L - 2; ++l) INF_CHECK_ARG(a.wf[l] != nullptr && a.wb[l] != nullptr, "chain4: hidden images");
+  for (int l = 0; l <= a.L - 2; ++l)
+    INF_CHECK_ARG(a.colsum[l] != nullptr && a.dZT[l] != nullptr && (l > a.L - 3 || a.YT[l] != nullptr), "chain4: outputs");
+  if (a.loss == INF_LOSS_L2) return launch_typed<8, INF_LOSS_L2>(a, stream);
+  if (a.loss == INF_LOSS_L1) return launch_typed<8, INF_LOSS_L1>(a, stream);
+  return launch_typed<8, INF_LOSS_CAUCHY>(a, stream);
+}
+
+}  // namespace inf

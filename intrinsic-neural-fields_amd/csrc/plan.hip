@@ -80,6 +80,7 @@ struct inf_plan {
   // (lgemm.hip GT) -- no split-K slabs, no update launch (config D; INF_LGF=0/1 forces it)
   bool lgf = false;
   bool last_lgf = false;  // the last training step took it
+  bool last_chain4 = false;  // the last fused bf16 step ran chain4.hip (128-ray workgroups)
   int train_unit = 128;
   int bp_max = 0;
   int grid_hb = 1;
@@ -775,9 +776,11 @@ std::vector<AdamSeg> bucket_segs(const inf_plan* p) {
   return t;
 }
 
+int step_bm(const inf_plan* p, int Bp);
+
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
-  const int parts = chain == 3 ? Bp / chain3_bm(Bp)
+  const int parts = chain == 3 ? Bp / step_bm(p, Bp)
                     : chain == CHAIN_BIG ? Bp / LY_RAYS
                     : (chain == CHAIN_F32 || chain == CHAIN_X3) ? Bp / 16
                     : chain ? Bp / chain_partial_rows(chain_bm(Bp))
@@ -980,6 +983,12 @@ bool use_fgemm(const inf_plan* p, int Bp, int splits) {
   return true;
 }
 
+// Rays per workgroup of the fused bf16 step at this padded batch (chain3: 16 / 64; chain4:
+// 128) -- one bias / head / loss partial per workgroup
+int step_bm(const inf_plan* p, int Bp) {
+  return p->mode == INF_MODE_BF16 && chain4_supported(p->H, p->L, p->k_pad, Bp) ? C4_BM : chain3_bm(Bp);
+}
+
 bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   const ParamSeg* w1 = p->weight_seg(1, 0);
   const ParamSeg* w0 = p->weight_seg(0, 0);
@@ -1159,6 +1168,17 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.count_step = 1;
   a.stamps = p->stamps;
   a.xpre = b->encoding == INF_ENC_NONE ? xpre : nullptr;
+  if (!x3 && b->encoding == INF_ENC_NONE && a.xpre == nullptr && !zp && step_bm(p, Bp) == C4_BM) {
+    a.w0_img = img(p->weight_seg(0, 0), true);
+    a.wy_img = img(p->weight_seg(s, 1), true);
+    for (int l = 1; l <= L - 2; ++l) {
+      a.wf[l] = img(p->weight_seg(l, 0), true);
+      a.wb[l] = img(p->weight_seg(l, 0), false);
+    }
+    p->last_chain4 = true;
+    return launch_chain4(a, st);
+  }
+  p->last_chain4 = false;
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
@@ -1870,7 +1890,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     p->saved_batch = batch->batch;
     p->saved_bp = Bp;
     ck = 3;
-    nloss = Bp / chain3_bm(Bp);
+    nloss = Bp / step_bm(p, Bp);
     p->stepped = true;
     p->last_lgf = false;
     if (!bucketed && (p->lgf || std::getenv("INF_FUSED_UPDATE") != nullptr)) {
@@ -2326,7 +2346,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
         f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
         // every workgroup streams W_0, W_y and the hidden weights twice over (L2 -> CU);
         // three table rows per ray in; X^T, Y^T, dZ^T out
-        by = (double)(Bp / chain3_bm(Bp)) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * e +
+        by = (double)(Bp / step_bm(p, Bp)) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * e +
              B * (3.0 * p->k_pad * e + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * e;
       } else {
         rc = run_chain(p, b, Bp, true, nullptr, nullptr, nullptr, nullptr, st);
@@ -2447,6 +2467,7 @@ int inf_debug_buffer(inf_plan* p, int which, void* dst, int64_t* bytes, inf_stre
 
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;
+  if (p->last_chain == 3 && p->last_chain4) return 9;
   if (p->last_chain == 3 && chain3_wide(p->saved_bp)) return 5;
   return p->last_chain == 3 && p->k_pad > C3_KC ? 4 : p->last_chain;
 }

@@ -397,6 +397,59 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
         assert np.abs(gw[n] - gl[n]).max() / scale < 1e-5, n
 
 
+@pytest.mark.parametrize("B,loss,bad", [(16384, "L2", False), (10240, "L1", True), (65536, "L2", False),
+                                        (9000, "cauchy", False)])
+def test_chain4_matches_chain3_wide(B, loss, bad, monkeypatch):
+    """chain4.hip (128-ray workgroups of four waves, opt-in with INF_CHAIN4=1 above 8192 rays
+    for the 8 x 256 field) against chain3's 64-ray tiles (the default) on one batch: the same
+    feature tile, the same MFMA k order for W_0 x and W_y x (two fp32 sums added in the skip
+    epilogue), the same epilogue arithmetic -- so the forward activations and the X^T / Y^T /
+    dZ^T images they give the dW GEMM are bitwise equal, and only the head's dot products and
+    the per-workgroup partials are summed in another fp32 order: RGB within 1e-6, the loss
+    sums within 1e-6 relative; dL/dz's last bits then flip a bf16 rounding of dZ now and then,
+    so gradients within 1e-3 of each tensor's max (seen 2.5e-4 on layers.0).  `bad`:
+    out-of-range vertex ids and ray-index values read as zero rows / zero targets on both;
+    9000 rays: a ragged batch (padded to 9088, 71 workgroups, the last one partly empty)."""
+    rng = np.random.default_rng(44)
+    k, H, L, s = CFG["B"]
+    V = 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    perm = torch.randperm(B)
+    if bad:
+        vids[::97, 1] = V + 5
+        perm[::131] = B + 7
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda(), validate=not bad)
+    out = {}
+    for tag in ("chain4", "chain3_wide"):
+        monkeypatch.setenv("INF_CHAIN4", "1" if tag == "chain4" else "0")
+        plan, params, w = make_plan("B", mode="bf16", loss=loss, max_batch=B, adam=True)
+        pred = torch.empty((B, 3), device="cuda")
+        b = plan.make_batch(source=src, batch=B, ray_idx=perm.cuda())
+        plan.train_step(b, pred, apply_adam=False)
+        c = plan.read_ctrl()
+        assert plan.last_step_path() == tag, plan.last_step_path()
+        assert c["step"] == 1
+        xt = plan.debug_buffer(0).cpu().numpy()
+        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"], c["sse_sum"], xt)
+        del plan
+        torch.cuda.empty_cache()
+    p4, g4, l4, s4, x4 = out["chain4"]
+    p3, g3, l3, s3, x3 = out["chain3_wide"]
+    assert np.isfinite(p4).all()
+    assert np.array_equal(x4, x3)  # X^T images: the same gathered features
+    np.testing.assert_allclose(p4, p3, atol=1e-6)
+    assert abs(l4 - l3) <= 1e-6 * max(1.0, abs(l3)) and abs(s4 - s3) <= 1e-6 * max(1.0, abs(s3)), (l4, l3, s4, s3)
+    for n in O.layer_names(L, s):
+        scale = max(np.abs(g3[n]).max(), 1e-12)
+        err = float(np.abs(g4[n] - g3[n]).max() / scale)
+        assert err < 1e-3, (n, err)
+
+
 @pytest.mark.parametrize("name,B,bad", [("B", 4096, False), ("R", 4096, False), ("B", 2048, True)])
 def test_chain3_precomputed_input_layers(name, B, bad, monkeypatch):
     """chain3's ZP schedule (INF_ZP=1, csrc/igemm.hip: gather X / X^T, then Z = [W_0; W_y] X^T
@@ -693,7 +746,8 @@ def test_bf16_chain3_matches_bf16_oracle(name, B, big, monkeypatch):
     plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
     pred = torch.empty((B, 3), device="cuda")
     plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
-    assert plan.last_step_path() == ("layer_big" if big else "chain3_wide" if B > 8192 else "chain3"), plan.last_step_path()
+    want = ("layer_big",) if big else ("chain3_wide", "chain4") if B > 8192 else ("chain3",)
+    assert plan.last_step_path() in want, plan.last_step_path()
     c = plan.read_ctrl()
     if big:
         assert c["step"] == 1  # the head workgroup counts the step, as chain3's store wave does
