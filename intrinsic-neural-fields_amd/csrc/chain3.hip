@@ -167,7 +167,8 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
   float* w7s = reinterpret_cast<float*>(smem + C::OFF_W7);
   float* vecs = reinterpret_cast<float*>(smem + C::OFF_VEC);
   char* xs = smem + C::off_x(L);  // gathered features [BM][kx] bf16 (tile_off layout)
-  const int kx = XC ? C::KC : k_pad;  // columns resident in LDS
+  // columns resident in LDS (ZP: the region holds W_y x, zin_parts slices of 16 rays x H fp32)
+  const int kx = ZP ? a.zin_parts * 2 * H : (XC ? C::KC : k_pad);
   const int xrow = kx * 2;
   const int x_lo = BM * xrow;  // X3: the lo feature tile, from the hi one
 
@@ -430,6 +431,14 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
       for (int j = 0; j < TN; ++j)
         z0[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                               rz, ((unsigned)(blockIdx.x * (2 * H / 16) + t0 + j) * 64u + lane) * 16u, 0, 0));
+      // further k slices (zg.hip), added in order
+#pragma unroll 1
+      for (int sl = 1; sl < a.zin_parts; ++sl)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          z0[j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rz, ((unsigned)(blockIdx.x * (2 * H / 16) + t0 + j) * 64u + lane) * 16u,
+                                                 (int)(sl * a.zin_stride * 4), 0));
     }
     // the first block's fragments, in k order (the loop's waits assume that order); issued
     // after the dependent ray-record loads so those are not queued behind them
@@ -692,7 +701,11 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
               f32x4 wy = f32x4{0.f, 0.f, 0.f, 0.f};
               if constexpr (ACCY) wy = accy[n][j];
               else if constexpr (PARK) wy = *reinterpret_cast<const f32x4*>(wy_slot(n, j));
-              else if constexpr (ZP) wy = *reinterpret_cast<const f32x4*>(xs + ((t0 + j) * 64 + lane) * 16);
+              else if constexpr (ZP) {
+                wy = *reinterpret_cast<const f32x4*>(xs + ((t0 + j) * 64 + lane) * 16);
+                for (int sl = 1; sl < a.zin_parts; ++sl)  // the k slices in order
+                  wy += *reinterpret_cast<const f32x4*>(xs + ((sl * (H / 16) + t0 + j) * 64 + lane) * 16);
+              }
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 float v = z[r];
@@ -1131,9 +1144,12 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
     // B2(0), read in the skip layer's epilogue (phase s >= 1)
     if constexpr (ZP) {
       const char* zy = reinterpret_cast<const char*>(a.zin) + ((int64_t)blockIdx.x * (2 * H / 16) + H / 16) * 1024 + lane * 16;
+#pragma unroll 1
+      for (int sl = 0; sl < a.zin_parts; ++sl)  // slice sl at H / 16 KiB steps
 #pragma unroll
-      for (int t = 0; t < H / 16; ++t)
-        __builtin_amdgcn_global_load_lds(zy + t * 1024, (__attribute__((address_space(3))) void*)(xs + t * 1024), 16, 0, 0);
+        for (int t = 0; t < H / 16; ++t)
+          __builtin_amdgcn_global_load_lds(zy + (int64_t)sl * a.zin_stride * 4 + t * 1024,
+                                           (__attribute__((address_space(3))) void*)(xs + (sl * (H / 16) + t) * 1024), 16, 0, 0);
     }
     lbar();  // barrier 0: feature tile in LDS
     if (a.count_step && blockIdx.x == 0 && lane == 0) a.ctrl->step += 1;
@@ -1295,7 +1311,7 @@ __global__ __launch_bounds__(C3_THREADS) void chain3_kernel(const Chain3Args a) 
 template <int H, int LOSS, bool ENC, bool XC, int NR, bool ZP = false, bool X3 = false>
 int launch3_enc(const Chain3Args& a, hipStream_t stream) {
   using C = L3<H, NR, X3>;
-  const int lds = C::lds_bytes(a.L, a.kc, XC);
+  const int lds = C::lds_bytes(a.L, ZP ? a.zin_parts * 2 * H : a.kc, XC);
   INF_CHECK_ARG(lds <= C3_LDS_CAP, "chain3: LDS budget exceeded for this depth / feature width");
   static int attr_set = 0;
   if (attr_set < lds) {
@@ -1364,11 +1380,11 @@ int launch_chain3(const Chain3Args& a_in, int bm, hipStream_t stream) {
   INF_CHECK_ARG(bm == C3BM || (a.encoding == INF_ENC_NONE && a.xpre == nullptr), "chain3: wide tiles gather tables only");
   INF_CHECK_ARG(a.rows % bm == 0 && a.rows >= bm, "chain3: rows must be a multiple of the tile height");
   INF_CHECK_ARG(a.nphase == 2 * a.L - 3, "chain3: phases");
-  // precomputed input layers: the narrow whole-tile schedule, W_y x staged in the idle
-  // feature-tile region (16 rays x H fp32 <= 16 x k_pad bf16)
+  // precomputed input layers: the narrow schedule, W_y x (zin_parts k slices) staged in
+  // the feature-tile region
   INF_CHECK_ARG(a.zin == nullptr || (bm == C3BM && a.encoding == INF_ENC_NONE && a.xpre == nullptr &&
-                                     a.kc == a.k_pad && a.k_pad >= 2 * a.H),
-                "chain3: precomputed input layers need the whole-tile schedule");
+                                     a.zin_parts >= 1 && a.zin_parts <= 8 && a.k_pad >= 2 * a.H),
+                "chain3: precomputed input layers need the narrow schedule");
   INF_CHECK_ARG(a.nblk >= 1 && a.nblk <= C3_MAX_BLOCKS, "chain3: weight-stream blocks");
   INF_CHECK_ARG(!a.x3 || (bm == C3BM && a.table_f32 != nullptr && chain3_x3_lds_fits(a.H, a.L, a.k_pad)),
                 "chain3: split-bf16 chain: 16-ray tiles over an fp32 table");

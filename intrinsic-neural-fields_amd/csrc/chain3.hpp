@@ -71,6 +71,9 @@ struct Chain3Args {
   // accumulator layout ([rows / 16][2H / 16] KiB); X^T already written (null: the kernel
   // gathers and streams W_0 / W_y itself)
   const float* zin;
+  // ... as zin_parts slices at zin + s zin_stride (zg.hip's k slices), added in order s = 0, 1, ..
+  int32_t zin_parts;
+  int64_t zin_stride;
   // weight stream: phases 0..L-2 forward layer p, L-1.. dX of layer (L-2) - (p - (L-1))
   C3Block blk[C3_MAX_BLOCKS];
   int32_t nblk, nphase;
@@ -162,17 +165,16 @@ inline int chain3_kc(int k_pad, int64_t rows) {
 
 int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream);
 
-// chain4.hip: the large-batch step on 128-ray workgroups of four waves (one per SIMD, the
-// whole register file each), the 8-layer H = 256 field (configs B / C / D / E) above
-// CHAIN3_MAX_ROWS.  Opt-in (INF_CHAIN4=1): measured slower than chain3's 64-ray tiles at
-// 65536 rays (533 vs 344 us of chain; tools/chain4_timing.py)
+// chain4.hip: the large-batch step on 128-ray workgroups of eight waves (two per SIMD),
+// the 8-layer H = 256 field (configs B / C / D / E) above CHAIN3_MAX_ROWS.  Opt-in
+// (INF_CHAIN4=1) until it measures faster than chain3's 64-ray tiles
 constexpr int C4_BM = 128;
-constexpr int C4_KC = 128;  // feature columns gathered per chunk
-constexpr int C4_STAMPS = 192;  // diagnostics: wall-clock stamps per stamped workgroup
+constexpr int C4_KC = 64;  // feature columns gathered per chunk (two chunks in flight)
+constexpr int C4_STAMPS = 256;  // diagnostics: wall-clock stamps per stamped workgroup
 inline bool chain4_supported(int H, int L, int k_pad, int64_t rows) {
-  return H == 256 && L == 8 && k_pad % C4_KC == 0 && rows % C4_BM == 0 && rows > CHAIN3_MAX_ROWS &&
-         rows <= CHAIN3_WIDE_MAX_ROWS && std::getenv("INF_CHAIN4") != nullptr &&
-         std::getenv("INF_CHAIN4")[0] == '1';
+  const char* e = std::getenv("INF_CHAIN4");
+  return H == 256 && L == 8 && k_pad % (2 * C4_KC) == 0 && rows % C4_BM == 0 && rows > CHAIN3_MAX_ROWS &&
+         rows <= CHAIN3_WIDE_MAX_ROWS && e != nullptr && e[0] == '1';
 }
 int launch_chain4(const Chain3Args& a, hipStream_t stream);
 

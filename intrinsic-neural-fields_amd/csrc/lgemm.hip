@@ -453,11 +453,30 @@ int launch_typed(const LgemmBatch& b, hipStream_t stream) {
 int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   INF_CHECK_ARG(bm == 32 || bm == 64, "lgemm: rows per block");
   INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= LGEMM_MAX_PROBLEMS, "lgemm: problem count");
-  const bool gt = b.fused == 2;  // split-K 1, the update on the LDS gradient tile (64 x 64 tiles)
+  const bool gt = b.fused == 2;  // split-K 1, the update on the LDS gradient tile
+  // Gradient tiles: 64 x 64, or 128 x 128 with INF_LGF_TILE=128 (config D: 608 blocks of 64 x
+  // 64, 2.4 per CU, each streaming 1 MB of operand panels for 33.5 MFLOP; 152 of 128 x 128,
+  // 2 MB for 134 MFLOP -- half the operand stream per FLOP, but see below).
   // (INF_LGF_BN=128: 64 x 128 gradient tiles -- config D's dW + update 44.8 -> 49.8 us, step
   // 128.7 -> 133.4 us: half the blocks at 2.4 -> 1.2 per CU, each a longer chain)
   const char* e_gbn = std::getenv("INF_LGF_BN");
-  const int gt_bn = e_gbn != nullptr && std::atoi(e_gbn) == 128 ? 128 : 64;
+  int gt_bn = e_gbn != nullptr && std::atoi(e_gbn) == 128 ? 128 : 64;
+  if (gt) {
+    int64_t blocks64 = 0;
+    bool ok128 = true;
+    for (int i = 0; i < b.nprob; ++i) {
+      blocks64 += (int64_t)(b.p[i].M / 64) * (b.p[i].N / 64);
+      ok128 = ok128 && b.p[i].M % 128 == 0 && b.p[i].N % 128 == 0;
+    }
+    // (measured slower at config D: dW + update 45.2 -> 60.0 us -- one wave per SIMD streams
+    // 2 MB per block at the lone-wave rate; opt-in)
+    const char* e_t = std::getenv("INF_LGF_TILE");
+    const bool t128 = e_t != nullptr && std::atoi(e_t) == 128 && blocks64 > 0;
+    if (t128 && ok128) {
+      bm = 128;
+      gt_bn = 128;
+    }
+  }
   const int bn = gt ? gt_bn : LG_BN;
   int blocks = 0;
   for (int i = 0; i < b.nprob; ++i) {
@@ -480,9 +499,10 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   }
   b.total_blocks = blocks;
   if (gt) {
-    INF_CHECK_ARG(bm == 64 && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.adam.items != nullptr,
+    INF_CHECK_ARG((bm == 64 || bm == 128) && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.adam.items != nullptr,
                   "lgemm: gradient-tile update layout");
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: the vector items reduce their slabs");
+    if (bm == 128) return launch_typed<128, true, false, 128, true>(b, stream);
     return gt_bn == 128 ? launch_typed<64, true, false, 128, true>(b, stream) : launch_typed<64, true, false, 64, true>(b, stream);
   }
   if (b.fused) {

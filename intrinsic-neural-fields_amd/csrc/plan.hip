@@ -22,6 +22,7 @@
 #include "head.hpp"
 #include "fgemm.hpp"
 #include "igemm.hpp"
+#include "zg.hpp"
 #include "layer.hpp"
 #include "lgemm.hpp"
 #include "rchain.hpp"
@@ -81,6 +82,7 @@ struct inf_plan {
   bool lgf = false;
   bool last_lgf = false;  // the last training step took it
   bool last_chain4 = false;  // the last fused bf16 step ran chain4.hip (128-ray workgroups)
+  bool last_zg = false;      // ... its input layers on zg.hip ahead of chain3
   int train_unit = 128;
   int bp_max = 0;
   int grid_hb = 1;
@@ -91,7 +93,8 @@ struct inf_plan {
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_tables_b = 0, o_ws_end = 0;
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
-  int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (igemm.hip), fp32 [bp_max][2H]
+  int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (igemm.hip / zg.hip), fp32 [parts][bp_max][2H]
+  int zin_parts_max = 0;       // k slices o_zin holds
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
   // the matrix items alone (the update launch after a dW GEMM that ran the vector items)
   int64_t o_mat_items = 0;
@@ -310,8 +313,12 @@ int build_layout(inf_plan* p) {
   p->o_x0t = take((int64_t)p->k_pad * Bp * p->esz);
   if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS)
     for (int i = 0; i < 2; ++i) p->o_xp[i] = take(Bp * p->k_pad * 2);
-  if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS && igemm_supported(H, p->k_pad, Bp))
-    p->o_zin = take(Bp * 2 * H * 4);
+  if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS &&
+      (igemm_supported(H, p->k_pad, Bp) || zg_supported(H, p->k_pad, Bp))) {
+    // zg.hip's k slices: at most zg_splits of the smallest batch (64 rays)
+    p->zin_parts_max = zg_supported(H, p->k_pad, Bp) ? zg_splits(p->k_pad, 64) : 1;
+    p->o_zin = take((int64_t)p->zin_parts_max * Bp * 2 * H * 4);
+  }
   const int64_t max_parts =
       std::max<int64_t>({chain_max_partials(Bp), std::min<int64_t>(Bp, CHAIN3_WIDE_MAX_ROWS) / 16, (int64_t)p->grid_hb});
   for (int l = 0; l < L - 1; ++l) {
@@ -1012,6 +1019,12 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
 // layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
 // k_pad > C3_KC (config D): X is streamed in C3_KC-column chunks and phase 0 runs W_y then
 // W_0 over each chunk (W_y x kept in the second accumulator set until the skip layer).
+// INF_ZG=1: the input layers on zg.hip ahead of the chain (opt-in)
+static bool use_zg(const inf_plan*) {
+  const char* e = std::getenv("INF_ZG");
+  return e != nullptr && e[0] == '1';
+}
+
 int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st, const bf16* xpre = nullptr,
                bool x3 = false) {
   const int H = p->H, L = p->L, s = p->s;
@@ -1081,10 +1094,47 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   // hidden layers only.  Opt-in: at config B the chain drops 42.3 -> 29.4 us but the gather
   // (9.2 us) and the GEMM (10.6 us) cost more than the 1 MB per-CU L2 stream they replace
   // -- the GEMM's X tiles come from the MALL at its per-CU rate (profiles/r03/s3/zp_step.json)
-  const bool zp = p->o_zin >= 0 && b->encoding == INF_ENC_NONE && xpre == nullptr && !xc && chain3_bm(Bp) == 16 &&
+  // INF_ZG=1: the same schedule with gather and GEMM in one launch (zg.hip: 64 rays x all 2H
+  // features x a k slice per workgroup, the slices added by the chain), any k_pad and table size
+  const int zg_s = zg_splits(p->k_pad, Bp);
+  const bool zgp = p->o_zin >= 0 && b->encoding == INF_ENC_NONE && xpre == nullptr && chain3_bm(Bp) == 16 &&
+                   zg_supported(H, p->k_pad, Bp) && zg_s <= p->zin_parts_max && use_zg(p);
+  const bool zp = !zgp && p->o_zin >= 0 && b->encoding == INF_ENC_NONE && xpre == nullptr && !xc && chain3_bm(Bp) == 16 &&
                   igemm_supported(H, p->k_pad, Bp) && b->num_vertices * (int64_t)p->k_pad * 2 < ((int64_t)1 << 32) &&
                   std::getenv("INF_ZP") != nullptr;
-  if (zp) {
+  a.zin_parts = 1;
+  p->last_zg = zgp;
+  if (zgp) {
+    ZgArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.table = a.table;
+    g.num_vertices = b->num_vertices;
+    g.k_pad = p->k_pad;
+    g.H = H;
+    g.vids = b->vids;
+    g.vid_dtype = b->vid_dtype;
+    g.bary = b->bary;
+    g.ray_idx = b->ray_idx;
+    g.idx_dtype = b->idx_dtype;
+    g.idx_offset = b->idx_offset;
+    g.num_rays = b->num_rays;
+    g.num_src = b->num_source_rays;
+    g.ctrl = p->ctrl;
+    g.offset_from_ctrl = b->offset_from_ctrl;
+    g.batch = b->batch;
+    g.rows = Bp;
+    g.splits = zg_s;
+    g.gather_nt = (size_t)b->num_vertices * (size_t)p->k_pad * 2 > C3_NT_TABLE_BYTES;
+    g.W0 = img(p->weight_seg(0, 0), true);
+    g.Wy = img(p->weight_seg(s, 1), true);
+    g.Z = p->W<float>(p->o_zin);
+    g.z_stride = (int64_t)Bp * 2 * H;
+    g.XT = p->W<bf16>(p->o_x0t);
+    if ((rc = launch_zg(g, st))) return rc;
+    a.zin = g.Z;
+    a.zin_parts = zg_s;
+    a.zin_stride = g.z_stride;
+  } else if (zp) {
     XGatherArgs g;
     std::memset(&g, 0, sizeof(g));
     g.table = a.table;
@@ -1138,8 +1188,8 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     }
   }
   for (int l = 1; l <= L - 2; ++l) {
-    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || zp || l != s))) return rc;
-    if (l == s && !xc && !zp)
+    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || zp || zgp || l != s))) return rc;
+    if (l == s && !xc && !zp && !zgp)
       for (int i = 0; i < nx; ++i)
         if ((rc = add(img(p->weight_seg(s, 1), true), i * upl, 1, i * upl, l, i == nx - 1))) return rc;
   }
@@ -2468,6 +2518,7 @@ int inf_debug_buffer(inf_plan* p, int which, void* dst, int64_t* bytes, inf_stre
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;
   if (p->last_chain == 3 && p->last_chain4) return 9;
+  if (p->last_chain == 3 && p->last_zg) return 10;
   if (p->last_chain == 3 && chain3_wide(p->saved_bp)) return 5;
   return p->last_chain == 3 && p->k_pad > C3_KC ? 4 : p->last_chain;
 }

@@ -496,6 +496,62 @@ def test_chain3_precomputed_input_layers(name, B, bad, monkeypatch):
         assert err < 1e-2, (n, err)
 
 
+@pytest.mark.parametrize("k,B,bad,V", [(1024, 4096, False, 3000), (1024, 2048, True, 3000), (4096, 4096, False, 20000),
+                                        (4096, 1024, True, 5000)])
+def test_chain3_zg_input_layers(k, B, bad, V, monkeypatch):
+    """chain3 after zg.hip (INF_ZG=1: gather + Z_s = [W_0; W_y] X_s^T over k slices in one
+    launch, the chain adding the slices in order and streaming the hidden layers only)
+    against the default schedule (the in-kernel gather and input-layer stream; config D's
+    k = 4096: the chunked tile) on one batch of the 8 x 256 field.  The gather numerics are
+    the same (b0 e0 + b1 e1 + b2 e2 in fp32, one bf16 rounding): X^T images bitwise.  Z is
+    summed per k slice and the slices added, so a bf16 activation may round the other way:
+    RGB 5e-4, loss 1e-3 relative, gradients 3e-2 of max (the bf16-oracle bar: two fp32
+    summation orders of the same bf16 arithmetic; seen 1.7e-2 on layers.0.0.weight at 2048 rays
+    with bad ids).  `bad`: out-of-range vertex ids and ray-index values read as zero rows /
+    zero targets."""
+    rng = np.random.default_rng(9)
+    H, L, s = 256, 8, 4
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    perm = torch.randperm(B)
+    if bad:
+        vids[::97, 1] = V + 5
+        perm[::131] = B + 7
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda(), validate=not bad)
+    import model as M
+    torch.manual_seed(0)
+    m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s})
+    w = {n: p.detach().numpy().copy() for n, p in m.named_parameters()}
+    out = {}
+    for tag in ("zg", "default"):
+        monkeypatch.setenv("INF_ZG", "1" if tag == "zg" else "0")
+        params = arena_from(w, L, s)
+        plan = rt().Plan(k, H, L, s, "bf16", "L2", B, params, grads=torch.zeros_like(params),
+                         exp_avg=torch.zeros_like(params), exp_avg_sq=torch.zeros_like(params))
+        pred = torch.empty((B, 3), device="cuda")
+        plan.train_step(plan.make_batch(source=src, batch=B, ray_idx=perm.cuda()), pred, apply_adam=False)
+        c = plan.read_ctrl()
+        want = "chain3_zg" if tag == "zg" else ("chain3_chunked" if k > 1024 else "chain3")
+        assert plan.last_step_path() == want, plan.last_step_path()
+        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"], plan.debug_buffer(0).cpu().numpy())
+        del plan
+        torch.cuda.empty_cache()
+    pz, gz, lz, xz = out["zg"]
+    pn, gn, ln, xn = out["default"]
+    assert np.isfinite(pz).all()
+    assert np.array_equal(xz, xn)  # X^T: the same gathered features
+    np.testing.assert_allclose(pz, pn, atol=5e-4)
+    assert abs(lz - ln) <= 1e-3 * max(1.0, abs(ln)), (lz, ln)
+    for n in O.layer_names(L, s):
+        scale = max(np.abs(gn[n]).max(), 1e-12)
+        err = np.abs(gz[n] - gn[n]).max() / scale
+        assert err < 3e-2, (n, err)
+
+
 def test_bf16_chain_render_matches_layered(monkeypatch):
     """bf16 render of the G7 frame: the forward-only register chain (rchain.hip, default),
     the LDS-ring chain (INF_NO_RCHAIN) and the layered kernels (INF_NO_CHAIN).  The register

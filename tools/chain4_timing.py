@@ -47,7 +47,7 @@ ev1.record()
 torch.cuda.synchronize()
 print(f"chain stage: {ev0.elapsed_time(ev1) / 10 * 1e3:.1f} us (B={B})")
 
-NS = 192
+NS = 256
 stamps = torch.zeros(2 * NS, dtype=torch.int64, device="cuda")
 lib.inf_debug_timing(plan.handle, ctypes.c_void_p(stamps.data_ptr()), 1)
 for _ in range(3):
@@ -55,10 +55,10 @@ for _ in range(3):
     plan.run_stage(STAGE_CHAIN, 0, b)
     torch.cuda.synchronize()
 lib.inf_debug_timing(plan.handle, None, 0)
-nchunk = (-(-k // 128) * 128) // 128
+nchunk = (-(-k // 128) * 128) // 64
 labels = ["entry", "records"]
 for c in range(nchunk):
-    labels += [f"chunk{c} gathered", f"chunk{c} X^T copied", f"chunk{c} MFMAs"]
+    labels += [f"chunk{c} rows in, X written", f"chunk{c} MFMAs, X^T, DMA"]
 labels += ["epi0 B1", "epi0 B2", "epi0 Y^T copy"]
 for l in range(1, L - 2):
     labels += [f"fwd{l} MFMAs", f"epi{l} B1", f"epi{l} B2", f"epi{l} Y^T copy"]
