@@ -1019,10 +1019,26 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
 // layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
 // k_pad > C3_KC (config D): X is streamed in C3_KC-column chunks and phase 0 runs W_y then
 // W_0 over each chunk (W_y x kept in the second accumulator set until the skip layer).
-// INF_ZG=1: the input layers on zg.hip ahead of the chain (opt-in)
-static bool use_zg(const inf_plan*) {
+// INF_FUSED_UPDATE=1 (the update inside a split-K dW launch) where that launch supports
+// it: every weight's rows 16-byte aligned (not config R's k = 1023), at most 4 splits --
+// otherwise the separate update launch, as by default
+static bool fused_update_requested(const inf_plan* p) {
+  if (std::getenv("INF_FUSED_UPDATE") == nullptr) return false;
+  if (p->dw_splits > 4) return false;
+  for (const auto& g : p->segs)
+    if (g.gemm && (g.C % 4 != 0 || g.off % 4 != 0)) return false;
+  return true;
+}
+
+// The input layers on zg.hip ahead of the chain: the default for the chunked-tile tables
+// (k_pad > C3_KC, config D: gather + input GEMM 26.5 us + the hidden-layer chain 31.9 us
+// against the chunked chain's 83 us, whose 16-ray workgroups each stream 4 MB of W_0 / W_y;
+// profiles/r05/zg/).  At config B it loses (16.1 + 31.1 us against 40 us: its 1 MB stream is
+// cheaper than the Z slices' 32 MB round trip).  INF_ZG=0/1 forces it.
+static bool use_zg(const inf_plan* p) {
   const char* e = std::getenv("INF_ZG");
-  return e != nullptr && e[0] == '1';
+  if (e != nullptr) return e[0] == '1';
+  return p->k_pad > C3_KC;
 }
 
 int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st, const bf16* xpre = nullptr,
@@ -1943,7 +1959,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     nloss = Bp / step_bm(p, Bp);
     p->stepped = true;
     p->last_lgf = false;
-    if (!bucketed && (p->lgf || std::getenv("INF_FUSED_UPDATE") != nullptr)) {
+    if (!bucketed && (p->lgf || fused_update_requested(p))) {
       // the update inside the dW launch: lgf (default, split-K 1: each block its own tile
       // from LDS) or INF_FUSED_UPDATE (split-K slabs, the last arriving block of a tile)
       p->last_chain = 3;

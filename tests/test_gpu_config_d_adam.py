@@ -5,7 +5,8 @@ At k > 1024 the bf16 step fuses the update into the weight-gradient GEMM (lgemm.
 biases and head in the launch's leading blocks).  Its gradient is pinned against the bf16
 oracle elsewhere (test_gpu_kernels.py::test_bf16_chunked_chain3_matches_bf16_oracle, a
 gradient-only LGF step).  Here the update itself, at config D's own shape (k = 4096,
-8 x 256, skip 4, seed-0 reference init, 4096 rays), over three steps:
+8 x 256, skip 4, seed-0 reference init, 4096 rays; the chain after zg.hip's gather + input
+GEMM, config D's default), over three steps:
 
 * test_config_d_lgf_adam_is_torch_adam_on_its_gradient -- each step's gradient is read
   from a gradient-only replay of the SAME step (same launch, same LDS tile, same sums: the
@@ -96,7 +97,7 @@ def test_config_d_lgf_adam_is_torch_adam_on_its_gradient(monkeypatch):
         # the gradient this step's fused update will consume: a gradient-only replay of the
         # same launch (LGF writes the reduced gradient from the same LDS tile)
         plan.train_step(b, None, apply_adam=False)
-        assert plan.last_step_path() == "chain3_chunked" and plan.last_step_fused_update() == 1
+        assert plan.last_step_path() == "chain3_zg" and plan.last_step_fused_update() == 1
         g = to_dict(plan.grads, w)
         plan.ctrl.copy_(ctrl0)  # the replay counted a step and added to the epoch sums
         plan.train_step(b, None, apply_adam=True)
@@ -124,7 +125,7 @@ def test_config_d_lgf_matches_slab_path(apply_adam, monkeypatch):
         plan, params = make_plan(w, B)
         plan.set_lr(1e-4)
         plan.train_step(plan.make_batch(source=src, ray_idx=perm, offset=0, batch=B), None, apply_adam=apply_adam)
-        assert plan.last_step_path() == "chain3_chunked"
+        assert plan.last_step_path() == "chain3_zg"
         assert plan.last_step_fused_update() == (tag == "lgf")
         c = plan.read_ctrl()
         torch.cuda.synchronize()

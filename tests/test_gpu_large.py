@@ -53,7 +53,9 @@ def run_step(w, k, H, L, s, mode, src, B, env, monkeypatch):
     pred = torch.empty((B, 3), device="cuda")
     plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
     want = {"INF_NO_CHAIN": "layered", "INF_NO_CHAIN3": "chain"}
-    path = want[env[0]] if env else ("chain3_chunked" if k > 1024 else "chain3") if mode == "bf16" else "layered"
+    # (k > 1024 at H = 256: zg.hip's gather + input GEMM ahead of the chain, the default)
+    path = want[env[0]] if env else (("chain3_zg" if H == 256 else "chain3_chunked") if k > 1024 else "chain3") \
+        if mode == "bf16" else "layered"
     assert plan.last_step_path() == path, (plan.last_step_path(), path)
     g = plan.grads.cpu().numpy()
     out, off = {}, 0
