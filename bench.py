@@ -537,7 +537,9 @@ def config_d_bench(args, device, B=4096, steps=40):
     out = {"config": "human_dense D: k=4096 8x256 skip 4, L2, Adam lr 1e-4, V=500000, bf16 table 4.1 GB",
            "rays_per_step": B, "ms_per_step": ms, "value": B / (ms * 1e-3), "unit": "rays/s", "path": path,
            "roofline": step_roofline(4096, a.hidden, a.layers, B, P, ms),
-           "chain3_traffic_per_launch": _pmc_traffic("chain3_chunked_bf16_D4096"),
+           "traffic_per_launch": ({"zg": _pmc_traffic("zg_bf16_D4096"), "chain3": _pmc_traffic("chain3_zp_bf16_D4096"),
+                                   "dw_gemm_update": _pmc_traffic("lgf_bf16_D4096")} if path == "chain3_zg"
+                                  else {"chain3": _pmc_traffic("chain3_chunked_bf16_D4096")}),
            "stages": {kk: {"ms": v[0], "tflops": v[1] / (v[0] * 1e-3) / 1e12} for kk, v in st.items()},
            "gather_kernel": {"ms": gms, "table_row_bytes": row_bytes,
                              "table_gbs": row_bytes / (gms * 1e-3) / 1e9,
