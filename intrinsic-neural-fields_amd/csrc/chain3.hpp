@@ -166,15 +166,15 @@ inline int chain3_kc(int k_pad, int64_t rows) {
 int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream);
 
 // chain4.hip: the large-batch step on 128-ray workgroups of eight waves (two per SIMD),
-// the 8-layer H = 256 field (configs B / C / D / E) above CHAIN3_MAX_ROWS.  Opt-in
-// (INF_CHAIN4=1) until it measures faster than chain3's 64-ray tiles
+// the 8-layer H = 256 field (configs B / C / D / E) above CHAIN3_MAX_ROWS: 2-3 % under
+// chain3's 64-ray tiles at 65,536 rays; INF_CHAIN4=0 keeps chain3's
 constexpr int C4_BM = 128;
 constexpr int C4_KC = 64;  // feature columns gathered per chunk (two chunks in flight)
 constexpr int C4_STAMPS = 256;  // diagnostics: wall-clock stamps per stamped workgroup
 inline bool chain4_supported(int H, int L, int k_pad, int64_t rows) {
   const char* e = std::getenv("INF_CHAIN4");
   return H == 256 && L == 8 && k_pad % (2 * C4_KC) == 0 && rows % C4_BM == 0 && rows > CHAIN3_MAX_ROWS &&
-         rows <= CHAIN3_WIDE_MAX_ROWS && e != nullptr && e[0] == '1';
+         rows <= CHAIN3_WIDE_MAX_ROWS && (e == nullptr || e[0] != '0');
 }
 int launch_chain4(const Chain3Args& a, hipStream_t stream);
 

@@ -234,10 +234,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       kb = q % UPL;
     }
   };
-  auto frag_i = [&](int i, bf16x8 (&dst)[TN]) {
-    const bf16* img;
-    int kb;
-    frag_src(i, img, kb);
+  // k block kb of image img (the refills take img / kb from the caller, computed once per
+  // layer or chunk: an image pointer looked up per k block is a scalar load whose
+  // lgkmcnt(0) wait also drained the B-operand reads in flight)
+  auto frag_at = [&](const bf16* img, int kb, bf16x8 (&dst)[TN]) {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(img), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
@@ -245,18 +245,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       dst[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + j * 1024,
                                                                                   kb * C::NT * 1024, 0));
   };
+  auto frag_i = [&](int i, bf16x8 (&dst)[TN]) {
+    const bf16* img;
+    int kb;
+    frag_src(i, img, kb);
+    frag_at(img, kb, dst);
+  };
   // Phase 0 loads its fragments by inline asm, and waits for them with explicit counts: the
   // compiler treats the direct-to-LDS loads in flight as a second kind of vector-memory
   // event, assumes out-of-order completion and would drain the whole queue (vmcnt(0)) before
   // every k block -- the gather's two chunks in flight with it.
-  auto frag_asm = [&](int i, bf16x8 (&dst)[TN]) {
-    const bf16* img;
-    int kb;
-    frag_src(i, img, kb);
+  auto frag_asm_at = [&](const bf16* img, int kb, bf16x8 (&dst)[TN]) {
     const unsigned vo = lane_off + (unsigned)kb * C::NT * 1024u;
     static_assert(TN == 2, "two fragment loads per k block");
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst[0]) : "v"(vo), "s"(img) : "memory");
     asm volatile("global_load_dwordx4 %0, %1, %2 offset:1024" : "=v"(dst[1]) : "v"(vo), "s"(img) : "memory");
+  };
+  auto frag_asm = [&](int i, bf16x8 (&dst)[TN]) {
+    const bf16* img;
+    int kb;
+    frag_src(i, img, kb);
+    frag_asm_at(img, kb, dst);
   };
   bf16x8 fr[D][TN];
   sfor<D0>([&](auto KB) { frag_asm(decltype(KB)::value, fr[decltype(KB)::value]); });
@@ -266,6 +275,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int q = 0; q < 4; ++q) aoffs[q] = act_off(q, r16, g4) - q * 1024;
   auto feat = [&](int j) { return 16 * (t0 + j) + 4 * g4; };
+  // feat(j) from an opaque copy of the lane id: recomputed where it is used (two VALU ops)
+  // instead of kept live across the layers -- the compiler had spilled it, and reloading a
+  // spill is a vector-memory wait that drains the fragment ring at every epilogue
+  auto feat_now = [&](int j) {
+    int x = lane;
+    asm volatile("" : "+v"(x));
+    return 16 * (t0 + j) + 4 * (x >> 4);
+  };
   auto put_act = [&](const float (&v)[TN][4], char* tile) {
 #pragma unroll
     for (int j = 0; j < TN; j += 2) {
@@ -361,6 +378,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto act_addr = [&](int t, int n, int r, int q) -> const char* {
     return act + n * C::TILE_BYTES + act_off(t >> 1, r, q) + 8 * (t & 1);
   };
+  // one float to base[idx] through a buffer resource (a scalar base and a 32-bit lane
+  // offset: per-lane 64-bit addresses of the partials' stores had been spilled in the head)
+  auto st_f32 = [&](float* base, int idx, float v) {
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rb, (unsigned)idx * 4u, 0, 0);
+  };
   // the feature chunk X: row = ray (128 B), 16-byte chunk q of row R at q ^ ((R >> 1) & 7)
   // (16 rows at one chunk hit 16 distinct 16-byte bank slots)
   auto x_addr = [&](int t, int n, int r, int q) -> const char* {  // t: feature tile within the chunk
@@ -417,10 +440,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // (ASM: phase 0 -- the slot's loads are retired by an explicit count of this wave's later
   // vector-memory operations, `first` chunk 6 else 14, and the refill goes through frag_asm;
   // else the compiler's waits)
-  auto kblock = [&](f32x4 (&tgt)[RT][TN], auto SLOTc, auto DEPc, const int i, const bool from_x, const int kbl,
+  // (rimg / rkb: the refill's image and k block, i.e. k block i + DEP of the sequence)
+  auto kblock = [&](f32x4 (&tgt)[RT][TN], auto SLOTc, const bf16* rimg, const int rkb, const bool from_x, const int kbl,
                     auto ASMc, const bool first = false) {
     constexpr int slot = decltype(SLOTc)::value;
-    constexpr int dep = decltype(DEPc)::value;
     constexpr bool use_asm = decltype(ASMc)::value;
     if constexpr (use_asm) {
       static_assert(2 * (2 * KBC - 1) == 6 && 2 * (2 * KBC - 1) + C::XT_STORES + C::DMA == 14, "phase-0 counts");
@@ -434,7 +457,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         return *reinterpret_cast<const bf16x8*>(xs + (16 * n + r16) * C::XROW + (((kbl * 4 + g4) ^ ((r16 >> 1) & 7)) << 4));
       return *reinterpret_cast<const bf16x8*>(act + n * C::TILE_BYTES + kbl * 1024 + aoffs[kbl & 3]);
     };
-    // B operands RA ray tiles ahead: a read's LDS latency (~120 cycles) under 2 RA MFMAs
+    // B operands RA ray tiles ahead: a read's LDS latency (~120 cycles) under RA MFMAs
 #ifndef C4_RA
 #define C4_RA 4
 #endif
@@ -450,12 +473,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (n + RA < RT) bq[n % RA] = bread(n + RA);
     }
     if constexpr (use_asm)
-      frag_asm(i + dep, fr[slot]);
+      frag_asm_at(rimg, rkb, fr[slot]);
     else
-      frag_i(i + dep, fr[slot]);
+      frag_at(rimg, rkb, fr[slot]);
     __builtin_amdgcn_sched_barrier(0);
   };
-  using DH = std::integral_constant<int, D>;
   using NOW = std::false_type;
 
   // ================= phase 0: both input layers over the gathered feature chunks ==========
@@ -467,7 +489,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ops_after(c) = 14 (c = 0), 24 (c = 1), 16.
   auto ops_after = [&](int c) -> int { return c == 0 ? C::DMA + D0 * TN : c == 1 ? 2 * D0 * TN + C::XT_STORES + C::DMA : D0 * TN + C::XT_STORES + C::DMA; };
   static_assert(C::DMA == 3 * C::XT_STORES, "tail chunks repeat the X^T stores in place of a DMA");
-  using D0c = std::integral_constant<int, D0>;
   using ASM = std::true_type;
 #pragma unroll 1
   for (int c = 0; c < nchunk; ++c) {
@@ -475,13 +496,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     interpolate(c);
     lbar();                 // X holds chunk c; raw buffer c & 1 free
     stamp();
-    const int i0 = c * 2 * KBC;
     const bool first = c == 0;
+    // the refills: chunk c + 1's k blocks (W_0, then W_y), after the last chunk the first
+    // hidden layer's k blocks 0 .. D0 - 1
+    const bool lastc = c + 1 == nchunk;
+    const bf16* r0img = lastc ? a.wf[1] : a.w0_img;
+    const bf16* ryimg = lastc ? a.wf[1] : a.wy_img;
+    const int r0kb = lastc ? 0 : (c + 1) * KBC, rykb = lastc ? KBC : (c + 1) * KBC;
     sfor<KBC>([&](auto KB) {
-      kblock(acc, std::integral_constant<int, decltype(KB)::value>{}, D0c{}, i0 + KB, true, KB, ASM{}, first);
+      kblock(acc, std::integral_constant<int, decltype(KB)::value>{}, r0img, r0kb + KB, true, KB, ASM{}, first);
     });
     sfor<KBC>([&](auto KB) {
-      kblock(accy, std::integral_constant<int, KBC + decltype(KB)::value>{}, D0c{}, i0 + KBC + KB, true, KB, ASM{}, first);
+      kblock(accy, std::integral_constant<int, KBC + decltype(KB)::value>{}, ryimg, rykb + KB, true, KB, ASM{}, first);
     });
     const bool tail = c + 2 >= nchunk;
     {  // X^T of the chunk for the dW of W_0 and W_y (feature tiles c KC / 16 ..)
@@ -494,19 +520,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __builtin_amdgcn_sched_barrier(0);
     stamp();
   }
-  // the ring deepens to D for the hidden layers: k blocks P0 + D0 .. P0 + D - 1 (P0 .. P0 +
-  // D0 - 1 are in flight from the last chunk's refills)
+  // Drain the queue once, with a wait the compiler sees: its model still holds the direct-
+  // to-LDS loads of phase 0 as pending, and the hidden-layer loop's waits (merged with that
+  // state at the loop header) would otherwise stay vmcnt(0) in every layer.  (Slots 0 .. D0 -
+  // 1, the first hidden layer's k blocks, are in flight from the last chunk's refills.)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  // the ring deepens to D for the hidden layers: k blocks P0 + D0 .. P0 + D - 1
   sfor<D - D0>([&](auto KB) {
     frag_i(P0 + D0 + decltype(KB)::value, fr[D0 + decltype(KB)::value]);
     __builtin_amdgcn_sched_barrier(0);
   });
-  // ... and the asm-loaded slots 0 .. D0 - 1 have landed (after them: the last chunk's 8 X^T
-  // stores and the loads just issued), which the compiler cannot see
+  // ... the asm-loaded slots 0 .. D0 - 1 have landed (the drain above; the tie keeps their
+  // first uses below it)
   static_assert(D0 == 4, "four slots tied below");
   asm volatile("s_waitcnt vmcnt(%8)"
                : "+v"(fr[0][0]), "+v"(fr[0][1]), "+v"(fr[1][0]), "+v"(fr[1][1]), "+v"(fr[2][0]), "+v"(fr[2][1]),
                  "+v"(fr[3][0]), "+v"(fr[3][1])
-               : "n"(4 * C::XT_STORES + (D - D0) * TN)
+               : "n"((D - D0) * TN)
                : "memory");
 
   // ---- forward epilogue of layer l: bias (+ W_y x and Ly.bias at the skip layer) + ReLU ---
@@ -529,10 +559,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       unsigned wd[TN][2];  // the packed bf16 pairs, as put_act lays them out
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat_now(j));
         f32x4 z = acc[n][j];
         if (skip) {
-          const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (NL - 1) * H + feat(j));
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (NL - 1) * H + feat_now(j));
           const f32x4 ay = n < RT / 2 ? accy[n][j] : ypark[((n - RT / 2) * TN + j) * C::THREADS + tid];
 #pragma unroll
           for (int r = 0; r < 4; ++r) z[r] = ((z[r] + ay[r]) + bv[r]) + yv[r];
@@ -568,18 +598,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
 
   fwd_epilogue(0);
-  int seq = P0;  // stream position
 #pragma unroll 1
   for (int l = 1; l <= NL - 3; ++l) {
-    sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, DH{}, seq + KB, false, KB, NOW{}); });
-    seq += UPL;
+    const bf16* nimg = a.wf[l + 1];  // the refills: the next layer's k blocks (D = UPL)
+    sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, nimg, KB, false, KB, NOW{}); });
     stamp();
     fwd_epilogue(l);
   }
 
   // ================= the last hidden layer, the head, the loss, the head backward =========
-  sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, DH{}, seq + KB, false, KB, NOW{}); });
-  seq += UPL;
+  {
+    const bf16* nimg = a.wb[NL - 2];  // the refills: the first backward layer
+    sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, nimg, KB, false, KB, NOW{}); });
+  }
   stamp();
   {
     const int l = NL - 2;
@@ -592,10 +623,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float hq[TN][4];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat(j));
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(vecs + l * H + feat_now(j));
         f32x4 z = acc[n][j];
         if (skip) {  // (s == NL - 2: not taken, chain4_supported requires s < NL - 2)
-          const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (NL - 1) * H + feat(j));
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(vecs + (NL - 1) * H + feat_now(j));
           const f32x4 ay = n < RT / 2 ? accy[n][j] : ypark[((n - RT / 2) * TN + j) * C::THREADS + tid];
 #pragma unroll
           for (int r = 0; r < 4; ++r) z[r] = ((z[r] + ay[r]) + bv[r]) + yv[r];
@@ -608,14 +639,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           hq[j][r] = __builtin_bit_cast(float, w << 16);
           hq[j][r + 1] = __builtin_bit_cast(float, w & 0xFFFF0000u);
         }
-        acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int o = 0; o < 3; ++o) {
         float z = 0.f;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat(j));
+          const f32x4 w = *reinterpret_cast<const f32x4*>(w7s + o * H + feat_now(j));
 #pragma unroll
           for (int r = 0; r < 4; ++r) z = fmaf(hq[j][r], w[r], z);
         }
@@ -674,7 +704,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // head backward: dZ_{L-2} = (dz W7) * (h > 0) into the tile (each lane its own slots),
     // its ray sums (the bias partial), the output layer's weight-gradient partials
     float cst[TN][4], hst[3][TN][4], dbs[3];
-#pragma unroll
+    // (one ray tile at a time: unrolled, the compiler hoisted every tile's activation reads
+    // and spilled them)
+#pragma unroll 1
     for (int n = 0; n < RT; ++n) {
       float dzr[3];
 #pragma unroll
@@ -686,9 +718,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float gv[TN][4];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const f32x4 w0 = *reinterpret_cast<const f32x4*>(w7s + 0 * H + feat(j));
-        const f32x4 w1 = *reinterpret_cast<const f32x4*>(w7s + 1 * H + feat(j));
-        const f32x4 w2 = *reinterpret_cast<const f32x4*>(w7s + 2 * H + feat(j));
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(w7s + 0 * H + feat_now(j));
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(w7s + 1 * H + feat_now(j));
+        const f32x4 w2 = *reinterpret_cast<const f32x4*>(w7s + 2 * H + feat_now(j));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float g = fmaf(dzr[2], w2[r], fmaf(dzr[1], w1[r], dzr[0] * w0[r]));
@@ -709,17 +741,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int o = 0; o < 3; ++o) {
         const float db = row_sum16(dbs[o]);
-        if (lane == 0) a.hb_part[part0 * 3 + o] = db;
+        if (lane == 0) st_f32(a.hb_part, (int)part0 * 3 + o, db);
       }
     }
     {
       int fo;
       const float sm = ray_sums(cst, fo);
-      if (r16 < NV) a.colsum[NL - 2][part0 * H + fo] = sm;
+      if (r16 < NV) st_f32(a.colsum[NL - 2], (int)part0 * H + fo, sm);
 #pragma unroll
       for (int o = 0; o < 3; ++o) {
         const float sh = ray_sums(hst[o], fo);
-        if (r16 < NV) a.hw_part[(part0 * 3 + o) * H + fo] = sh;
+        if (r16 < NV) st_f32(a.hw_part, ((int)part0 * 3 + o) * H + fo, sh);
       }
     }
     lbar();  // B2: dZ_{L-2} complete
@@ -731,12 +763,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     copy_image(std::integral_constant<int, 4>{}, act_addr, H, a.dZT[NL - 2], 0, H / 32);
     stamp();
   }
+  // (the accumulators restart here, not in the head: their registers serve the head meanwhile)
+#pragma unroll
+  for (int n = 0; n < RT; ++n)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[n][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ================= backward: dX of layers NL-2 .. 1 ======================================
 #pragma unroll 1
   for (int l = NL - 2; l >= 1; --l) {
-    sfor<UPL>([&](auto KB) { kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, DH{}, seq + KB, false, KB, NOW{}); });
-    seq += UPL;
+    // the refills: the next backward layer (past the last: harmless reloads of its last k block)
+    const bf16* nimg = a.wb[l > 1 ? l - 1 : 1];
+    const int nkb0 = l > 1 ? 0 : UPL - 1, nstep = l > 1 ? 1 : 0;
+    sfor<UPL>([&](auto KB) {
+      kblock(acc, std::integral_constant<int, decltype(KB)::value % D>{}, nimg, nkb0 + nstep * KB, false, KB, NOW{});
+    });
     stamp();
     // dZ_{l-1} = acc * (Y_{l-1} > 0): the mask stack's top
     unsigned bits[MW];
@@ -766,7 +807,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     {
       int fo;
       const float sm = ray_sums(cst, fo);
-      if (r16 < NV) a.colsum[l - 1][part0 * H + fo] = sm;
+      if (r16 < NV) st_f32(a.colsum[l - 1], (int)part0 * H + fo, sm);
     }
     lbar();  // B2
     stamp();

@@ -400,8 +400,8 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
 @pytest.mark.parametrize("B,loss,bad", [(16384, "L2", False), (10240, "L1", True), (65536, "L2", False),
                                         (9000, "cauchy", False)])
 def test_chain4_matches_chain3_wide(B, loss, bad, monkeypatch):
-    """chain4.hip (128-ray workgroups of four waves, opt-in with INF_CHAIN4=1 above 8192 rays
-    for the 8 x 256 field) against chain3's 64-ray tiles (the default) on one batch: the same
+    """chain4.hip (128-ray workgroups of eight waves, the default above 8192 rays for the
+    8 x 256 field) against chain3's 64-ray tiles (INF_CHAIN4=0) on one batch: the same
     feature tile, the same MFMA k order for W_0 x and W_y x (two fp32 sums added in the skip
     epilogue), the same epilogue arithmetic -- so the forward activations and the X^T / Y^T /
     dZ^T images they give the dW GEMM are bitwise equal, and only the head's dot products and

@@ -4,7 +4,7 @@ plus the stage's HIP-event time.
 
     python tools/chain4_timing.py [batch] [k]
 
-chain4 is opt-in (INF_CHAIN4=1); this script sets it.
+chain4 is the default above 8192 rays (INF_CHAIN4=0: chain3 wide tiles).
 """
 import ctypes
 import os
@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 import numpy as np
 import torch
 
-os.environ.setdefault("INF_CHAIN4", "1")
+os.environ.setdefault("INF_CHAIN4", "1")  # (the caller may set INF_CHAIN4=0: chain3 wide)
 
 from inf_hip import STAGE_CHAIN, lib, runtime
 
