@@ -3,6 +3,8 @@
 // permlane cross-lane sums, the LDS hand-off barrier.
 #pragma once
 
+#include <utility>
+
 #include "common.hpp"
 
 namespace inf {
@@ -107,6 +109,17 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+
+// f(integral_constant<int, I>) for I = 0 .. N-1: a loop whose index is a compile-time
+// constant in the body (ring slots statically indexed, per-step schedules unrolled)
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // LDS hand-off barrier that does not drain the vector-memory queue (__syncthreads()

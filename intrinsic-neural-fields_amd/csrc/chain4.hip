@@ -47,17 +47,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr float C4_CAUCHY_C2 = (20.f / 255.f) * (20.f / 255.f);
 
-// f(integral_constant<int, I>) for I = 0 .. N-1: a k-block loop whose ring slot is a
-// compile-time constant, so the fragment registers are statically indexed
-template <typename F, int... I>
-__device__ __forceinline__ void sfor_impl(F& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void sfor(F&& f) {
-  sfor_impl(f, std::make_integer_sequence<int, N>{});
-}
-
 // 1 if x != 0 else 0, as one v_min_u32 (a compare would put its lane mask in an SGPR pair)
 __device__ __forceinline__ unsigned nz1_4(unsigned x) {
   unsigned r;

@@ -55,5 +55,9 @@ inline bool rchain_supported(int H, int L, int k_pad) {
 // the hidden layers 1 .. L - 2, nchunk = 0)
 int launch_rchain(const RchainArgs& a, hipStream_t stream);
 int launch_rproj(const RchainArgs& a, hipStream_t stream);
+// rprojw.hip: the projected-table chain on 128-ray tiles (the 8 x 256 field, skip 4; the
+// default there, INF_RPROJ_WIDE=0 keeps rproj.hip's 64-ray tiles)
+bool rprojw_supported(const RchainArgs& a);
+int launch_rprojw(const RchainArgs& a, hipStream_t stream);
 
 }  // namespace inf

@@ -512,6 +512,7 @@ int launch_rproj(const RchainArgs& a, hipStream_t stream) {
   INF_CHECK_ARG(a.pred != nullptr || (a.img != nullptr && a.hit != nullptr), "rproj: no output");
   for (int i = 0; i < a.nblk; ++i)
     INF_CHECK_ARG(a.blk[i].img != nullptr && a.blk[i].phase == i + 1 && a.blk[i].kb0 == 0, "rproj: weight stream");
+  if (rprojw_supported(a)) return launch_rprojw(a, stream);
   // compute waves: 8 (32 output features each; default) or INF_RPROJ_WAVES=4 (64 each: half
   // the LDS operand reads, one compute wave per SIMD)
   static const int waves = [] {

@@ -355,3 +355,60 @@ def test_projected_render_matches_bf16_oracle(k, H, L, s, V, N):
 
 
 PROJ_BF16_ORACLE_RGB = 1e-3  # seen 1.7e-4 (k=1024, 8 x 256) / 5e-5 (k=64); profiles/r02/bf16_oracle_parity_render.log
+
+
+@pytest.mark.parametrize("N,bad", [(1, False), (1000, True), (33_077, False), (200_000, True)])
+def test_rprojw_matches_rproj(N, bad, monkeypatch):
+    """rprojw.hip (128-ray tiles, the default for the 8 x 256 field with skip 4) against
+    rproj.hip's 64-ray tiles (INF_RPROJ_WIDE=0) on the same projected batches.  Up to the
+    last hidden layer both run the same arithmetic (the rows' fp32 fold and one bf16
+    rounding, the MFMA k order, the epilogues); the head then sums W7 h in another fp32
+    order (MFMAs over W7's bf16 hi + lo parts, 2^-17 of |W7| left out) -- RGB within 5e-5
+    (seen below 1e-6), the background bitwise.  N = 1 (one tile), 1000 with out-of-range
+    vertex ids and ray-index values (zero rows), 33,077 (259 tiles: a second tile on a few
+    workgroups, a ragged last one), 200,000 (about 6 tiles per workgroup: the loader's
+    zy / records / z0 pipeline across tiles).  The first workgroup's stamps tell which
+    kernel ran: 14 barriers per 128-ray tile."""
+    import ctypes
+    import model as M
+    from inf_hip import lib, runtime
+    rng = np.random.default_rng(50 + N)
+    k, H, L, s, V, HW = 1024, 256, 8, 4, 5000, 1 << 19
+    torch.manual_seed(0)
+    m = M.make_model({"k": k, "num_layers": L, "mlp_hidden_dim": H, "skip_layer_idx": s}).cuda()
+    m.kernel_mode = "bf16"
+    E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32) * 0.3).cuda()
+    vids = rng.integers(0, V, (N, 3))
+    perm = torch.from_numpy(rng.permutation(N))
+    if bad:
+        vids[7 % N, 1] = V + 5
+        perm[::131] = N + 7
+    bary = rng.dirichlet([1, 1, 1], N).astype(np.float32)
+    hit = torch.from_numpy(np.sort(rng.choice(HW, N, replace=False))).cuda()
+    src = runtime.RaySource(E, torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(), None,
+                            validate=not bad)
+    plan = m.hip_plan(4096)
+    P = plan.project_table(src.table_for(plan))
+    out = {}
+    for wide in ("1", "0"):
+        monkeypatch.setenv("INF_RPROJ_WIDE", wide)
+        pred = torch.empty((N, 3), device="cuda")
+        plan.forward(plan.make_batch(source=src, batch=N, ray_idx=perm.cuda(), projected=P), pred, save=False)
+        img = torch.ones((HW, 3), device="cuda")
+        st = torch.zeros(2 * 68, dtype=torch.int64, device="cuda")
+        lib.inf_debug_timing(plan.handle, ctypes.c_void_p(st.data_ptr()), 0)
+        plan.render(plan.make_batch(source=src, batch=N, projected=P), hit, None, img)
+        torch.cuda.synchronize()
+        lib.inf_debug_timing(plan.handle, None, 0)
+        nst = int((st[:68] != 0).sum())
+        if wide == "1":  # the first workgroup's tiles (ntile // grid of them), two stamped
+            ntile = -(-N // 128)
+            want = 3 + 13 * min(2, ntile // min(ntile, 256))  # (the 14th barrier is not stamped)
+            assert nst == want, (nst, want)
+        out[wide] = (pred.cpu().numpy(), img.cpu().numpy())
+    assert np.isfinite(out["1"][0]).all()
+    err_p = float(np.abs(out["1"][0] - out["0"][0]).max())
+    err_i = float(np.abs(out["1"][1] - out["0"][1]).max())
+    print("rprojw vs rproj", N, err_p, err_i)
+    assert err_p < 5e-5 and err_i < 5e-5, (err_p, err_i)
+    assert (out["1"][1] == 1.0).sum() == (out["0"][1] == 1.0).sum() == out["1"][1].size - 3 * N
