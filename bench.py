@@ -697,10 +697,13 @@ def render_bench(args, device):
             "frac": max(t_mfma, t_hbm) / ms, "achieved_tflops": flops / (ms * 1e-3) / 1e12,
             "achieved_gbs": byts / (ms * 1e-3) / 1e9}
     if project:  # measured HBM bytes (PMC) of the frame's two launches: projection GEMM + rproj
-        tr_g, tr_p = _pmc_traffic(f"project_gemm_{args.mode}_render"), _pmc_traffic(f"rproj_{args.mode}_render")
+        # (rprojw.hip's 128-ray tiles for the 8 x 256 field with skip 4, else rproj.hip)
+        wide = (Hd, L, args.skip) == (256, 8, 4) and os.environ.get("INF_RPROJ_WIDE", "1") != "0"
+        kern = "rprojw" if wide else "rproj"
+        tr_g, tr_p = _pmc_traffic(f"project_gemm_{args.mode}_render"), _pmc_traffic(f"{kern}_{args.mode}_render")
         if tr_g is not None and tr_p is not None:
             roof["traffic_projection"] = tr_g
-            roof["traffic_rproj"] = tr_p
+            roof["traffic_" + kern] = tr_p
             roof["traffic"] = tr_g + tr_p
     else:
         tr = _pmc_traffic(f"rchain_{args.mode}_render_{chunk}")
@@ -743,7 +746,8 @@ def render_bench(args, device):
         variants["random_ids_100pct"] = variant(H * W, False)
     return {"value": H * W / (ms * 1e-3), "unit": "pixels/s", "ms_per_frame": ms, "frame": f"{H}x{W}",
             "hits": nhit, "verts": V, "chunk": chunk, "streams": nstreams, "variants": variants,
-            "path": "projected table (inf_project_table per frame + rproj)" if project else "feature gather rchain",
+            "path": ("projected table (inf_project_table per frame + rprojw, 128-ray tiles)" if project and wide else
+                     "projected table (inf_project_table per frame + rproj)" if project else "feature gather rchain"),
             "projection_ms": ms_proj, "ms_per_frame_feature_gather": ms_gather,
             "feature_gather_pixels_per_s": H * W / (ms_gather * 1e-3), "roofline": roof}
 

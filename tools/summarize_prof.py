@@ -18,7 +18,7 @@ def short(name):
         return "chain3_kernel<chunked>"
     if name.startswith("Cijk_"):  # hipBLASLt's kernels (the projection GEMM)
         return "hipblaslt_gemm"
-    for key in ("zg_kernel", "chain4_kernel", "gather_rows_kernel", "proj_gemm_kernel", "fgemm_kernel", "igemm_kernel", "xgather_kernel", "chainf_kernel", "rproj_kernel", "rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
+    for key in ("zg_kernel", "chain4_kernel", "gather_rows_kernel", "proj_gemm_kernel", "fgemm_kernel", "igemm_kernel", "xgather_kernel", "chainf_kernel", "rprojw_kernel", "rproj_kernel", "rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
                 "head_bwd_kernel", "pack_kernel", "ctrl_advance_kernel"):
         if key in name:
             tail = ""
@@ -66,7 +66,7 @@ def counters(d, counter):
 # bench.py stage -> kernel, for the per-launch traffic table bench.py reads
 STAGE_KERNEL = {"chain3": "chain3_kernel", "dw_gemm": "lgemm_kernel", "update": "update_kernel",
                 "rchain": "rchain_kernel", "chain3_chunked": "chain3_kernel<chunked>",
-                "rproj": "rproj_kernel", "project_gemm": "proj_gemm_kernel"}
+                "rproj": "rproj_kernel", "rprojw": "rprojw_kernel", "project_gemm": "proj_gemm_kernel"}
 
 
 def main(root, tag=None):
