@@ -26,12 +26,12 @@
 // Interval j ends at barrier j; the odd ones (1 .. 11) are the MFMA phases.  Loader side,
 // in groups of 12 row loads per thread (two register sets, A and B), every fold into Z in
 // an MFMA phase so that the epilogue intervals stay short:
-//   1: fold zy(i) g0, g1; load records(i + 1), pixels(i); load zy(i) g2 -> A, g3 -> B
-//   2: store records(i + 1) (set (tile - first + 1) & 1), pixels(i)
+//   1: fold zy(i) g0, g1; load zy(i) g2 -> A, g3 -> B
 //   3: fold zy(i) g2, g3                      (zy complete before layer s's start: 2s - 1)
 //   5: load z0(i + 1) g0 -> A, g1 -> B
 //   9: fold z0(i + 1) g0, g1 (Z free after barrier 2s - 1); load g2 -> A, g3 -> B
-//  11: fold z0(i + 1) g2, g3; load zy(i + 1) g0 -> A, g1 -> B
+//  11: fold z0(i + 1) g2, g3; load records(i + 2), pixels(i + 1); load zy(i + 1) g0 -> A, g1 -> B
+//  12: store records(i + 2) (set (tile - first) & 1); 0 (of i + 1): store pixels(i + 1)
 // (zy of the first tile: loaded ahead of the loop.)  The schedule is unrolled, so the
 // compiler's vmcnt waits count each group's loads exactly.
 #include <cstdlib>
@@ -48,7 +48,7 @@ using namespace c3;
 #define RW_DEPTH 4
 #endif
 #ifndef RW_RA
-#define RW_RA 4
+#define RW_RA 2  // (4: 4 spills, 2.05 vs 1.96 ms per 2M hits; depth 5 / 6 no better)
 #endif
 // loader schedule: 0 = the group loads in MFMA intervals (above), 1 = in the epilogue
 // intervals (2: zy g2 / g3, 6 and 10: z0, 12: the next zy g0 / g1)
@@ -96,7 +96,8 @@ struct WP {
   static_assert(S == 4 && NH == 6, "loader schedule");
 };
 
-template <int L_, int S_>
+// SIMPLE: rays in batch order with 32-bit vertex ids (no permutation)
+template <int L_, int S_, bool SIMPLE>
 __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const RchainArgs a) {
   using C = WP<L_, S_>;
   constexpr int RT = C::RT, BM = C::BM, TN = C::TN, UPL = C::UPL, CW = C::CW, G = C::G, HC = C::HC,
@@ -198,12 +199,42 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
       rbary[set * C::NREC + x] = r.w;
     }
   };
-  // the image pixel of ray x of a tile (renderer.py:139-141's placement index)
-  auto pix_load = [&](int tile, int x) -> int64_t {
+  // The loader's records and pixel indices, issued one interval set ahead of their stores
+  // with no use in between (branch-free addresses), so that no wait of theirs lands in a
+  // short interval: a record's raw vertex id and weight, and whether the ray has a row
+  struct RecRaw {
+    int e;  // vertex id (-1: out of range in the general path; range-checked at the store)
+    float w;
+    int ok;  // the ray has a source row
+  };
+  auto rec_issue = [&](int tile, int x) -> RecRaw {
+    const int b = tile * BM + x / 3, i = x % 3;
+    if constexpr (SIMPLE) {
+      // rays in order, 32-bit ids (the render's batches): two independent loads, no waits
+      const int64_t rr = x < C::NREC && b < a.batch ? source_row(nullptr, 0, a.idx_offset, b, a.num_rays, a.num_src) : -1;
+      const int64_t q = rr >= 0 ? 3 * rr + i : 0;
+      return RecRaw{reinterpret_cast<const int32_t*>(a.vids)[q], a.bary[q], rr >= 0};
+    }
+    else {  // (a permutation or 64-bit ids: the loads' waits land in interval 11)
+      const int64_t rr =
+          x < C::NREC && b < a.batch ? source_row(a.ray_idx, a.idx_dtype, a.idx_offset, b, a.num_rays, a.num_src) : -1;
+      const int64_t q = rr >= 0 ? 3 * rr + i : 0;
+      const int64_t e = vid_at(a.vids, a.vid_dtype, q);
+      return RecRaw{(uint64_t)e < (uint64_t)a.num_vertices ? (int)e : -1, a.bary[q], rr >= 0};
+    }
+  };
+  auto rec_put = [&](const RecRaw& r, int set, int x) {  // out-of-range ids: zero rows (gather.hip)
+    rec_store(Rec{r.ok && (uint32_t)r.e < (uint64_t)a.num_vertices ? r.e : -1, r.w}, set, x);
+  };
+  // the image pixel of ray x of a tile (renderer.py:139-141's placement index): hit[b]
+  // issued, the pixel map applied at the store
+  auto pix_issue = [&](int tile, int x) -> int64_t {
     const int b = tile * BM + x;
-    if (a.img == nullptr || x >= BM || b >= a.batch) return -1;
-    const int64_t p = a.hit[b];
-    return a.pixel_map != nullptr ? a.pixel_map[p] : p;
+    return a.img != nullptr ? a.hit[x < BM && b < a.batch ? b : 0] : -1;
+  };
+  auto pix_put = [&](int64_t p, int tile, int x) {
+    const int b = tile * BM + x;
+    if (x < BM) rpix[x] = a.img != nullptr && b < a.batch ? (a.pixel_map != nullptr ? a.pixel_map[p] : p) : -1;
   };
 
   // ---- 16-byte chunk c of half h (0: W_0 E, 1: W_y E) of ray r's projected row: the three
@@ -286,37 +317,31 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
 #pragma unroll
       for (int m = 0; m < G; ++m) rows_store(set, lr + C::RPI * (g * G + m), lc, e[m]);
     };
-    load_group(1, 0, 0, eA);  // zy of the first tile, groups 0 and 1
+    // ahead of the loop: the second tile's records (set 1), the first tile's pixels, zy of
+    // the first tile (groups 0 and 1)
+    if (tb + 1 < te) {
+      rec_put(rec_issue(tb + 1, x), 1, x);
+      rec_put(rec_issue(tb + 1, x + LT), 1, x + LT);
+    }
+    int64_t px = pix_issue(tb, x);
+    load_group(1, 0, 0, eA);
     load_group(1, 0, 1, eB);
 #pragma unroll 1
     for (int tile = tb; tile < te; ++tile) {
       const int cur = (tile - tb) & 1, nxt = cur ^ 1;
       const bool has_next = tile + 1 < te;
-      Rec r0{-1, 0.f}, r1{-1, 0.f};
-      int64_t px = -1;
+      RecRaw r0{-1, 0.f, 0}, r1{-1, 0.f, 0};
       sfor<NBAR>([&](auto J) {
         constexpr int j = decltype(J)::value;
         constexpr bool E = RW_SCHED == 1;
+        if constexpr (j == 0) pix_put(px, tile, x);  // (the previous tile's head has read rpix)
         if constexpr (j == 1) {
           store_group(cur, 0, eA);
           store_group(cur, 1, eB);
-          // (their dependent loads wait for the whole queue: issued before the group loads)
-          if (has_next) {
-            r0 = rec_load(tile + 1, x);
-            r1 = rec_load(tile + 1, x + LT);
-          }
-          px = pix_load(tile, x);
         }
         if constexpr (j == (E ? 2 : 1)) {
           load_group(1, cur, 2, eA);
           load_group(1, cur, 3, eB);
-        }
-        if constexpr (j == 2) {
-          if (has_next) {
-            rec_store(r0, nxt, x);
-            rec_store(r1, nxt, x + LT);
-          }
-          if (x < BM) rpix[x] = px;
         }
         if constexpr (j == 3) {
           store_group(cur, 2, eA);
@@ -344,6 +369,19 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
           if (has_next) {
             store_group(nxt, 2, eA);
             store_group(nxt, 3, eB);
+          }
+          // records of tile + 2 (stored in interval 12, into this tile's set: its last
+          // reader, zy's fold, was interval 3) and pixels of tile + 1 (stored in its interval 0)
+          if (tile + 2 < te) {
+            r0 = rec_issue(tile + 2, x);
+            r1 = rec_issue(tile + 2, x + LT);
+          }
+          if (has_next) px = pix_issue(tile + 1, x);
+        }
+        if constexpr (j == 12) {
+          if (tile + 2 < te) {
+            rec_put(r0, cur, x);
+            rec_put(r1, cur, x + LT);
           }
         }
         if constexpr (j == (E ? 12 : 11)) {
@@ -495,15 +533,17 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
       }
     }
     lbar();  // 13: the activation tile free for the next tile (the loader: its intervals)
+    if (st) stamp(sbase + 13);
   }
 }
 
-template <int L, int S>
+template <int L, int S, bool SIMPLE>
 int launch_typed(const RchainArgs& a, hipStream_t stream) {
   using C = WP<L, S>;
   static bool attr_set = false;
   if (!attr_set) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)rprojw_kernel<L, S>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
+    INF_HIP_TRY(
+        hipFuncSetAttribute((const void*)rprojw_kernel<L, S, SIMPLE>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
     attr_set = true;
   }
   static int ncu = 0;
@@ -514,7 +554,7 @@ int launch_typed(const RchainArgs& a, hipStream_t stream) {
   }
   const int64_t ntile = ceil_div(a.batch, C::BM);
   const int grid = (int)std::min<int64_t>(ntile, ncu);
-  rprojw_kernel<L, S><<<dim3((unsigned)grid), dim3(C::THREADS), C::LDS, stream>>>(a);
+  rprojw_kernel<L, S, SIMPLE><<<dim3((unsigned)grid), dim3(C::THREADS), C::LDS, stream>>>(a);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -529,7 +569,8 @@ bool rprojw_supported(const RchainArgs& a) {
 // (launch_rproj has checked the arguments)
 int launch_rprojw(const RchainArgs& a, hipStream_t stream) {
   INF_CHECK_ARG(rprojw_supported(a), "rprojw: unsupported shape");
-  return launch_typed<8, 4>(a, stream);
+  if (a.ray_idx == nullptr && a.vid_dtype == INF_DTYPE_I32) return launch_typed<8, 4, true>(a, stream);
+  return launch_typed<8, 4, false>(a, stream);
 }
 
 }  // namespace inf

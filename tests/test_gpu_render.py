@@ -368,7 +368,7 @@ def test_rprojw_matches_rproj(N, bad, monkeypatch):
     vertex ids and ray-index values (zero rows), 33,077 (259 tiles: a second tile on a few
     workgroups, a ragged last one), 200,000 (about 6 tiles per workgroup: the loader's
     zy / records / z0 pipeline across tiles).  The first workgroup's stamps tell which
-    kernel ran: 14 barriers per 128-ray tile."""
+    kernel ran: 14 stamped barriers per 128-ray tile."""
     import ctypes
     import model as M
     from inf_hip import lib, runtime
@@ -403,7 +403,7 @@ def test_rprojw_matches_rproj(N, bad, monkeypatch):
         nst = int((st[:68] != 0).sum())
         if wide == "1":  # the first workgroup's tiles (ntile // grid of them), two stamped
             ntile = -(-N // 128)
-            want = 3 + 13 * min(2, ntile // min(ntile, 256))  # (the 14th barrier is not stamped)
+            want = 3 + 14 * min(2, ntile // min(ntile, 256))
             assert nst == want, (nst, want)
         out[wide] = (pred.cpu().numpy(), img.cpu().numpy())
     assert np.isfinite(out["1"][0]).all()
