@@ -61,6 +61,11 @@ using namespace c3;
 #endif
 // diagnostics (tools/rchain_timing.py; results wrong): the loader waves' row work, 1 = none
 // (barriers only), 2 = loads without folds, 3 = folds of constants without loads
+// diagnostics (results wrong): RW_ROWS_L2 = 1 reads every row from the first 1024 vertices
+// (an L2-resident 1 MB): the row loads' cost without their HBM latency
+#ifndef RW_ROWS_L2
+#define RW_ROWS_L2 0
+#endif
 #ifndef RW_LOADER_IDLE
 #define RW_LOADER_IDLE 0
 #endif
@@ -243,7 +248,7 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
   auto rows_load = [&](int h, int set, int r, int c, u16x8 (&ev)[3]) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int v = max(rvid[set * C::NREC + r * 3 + i], 0);
+      const int v = max(rvid[set * C::NREC + r * 3 + i], 0) & (RW_ROWS_L2 ? 1023 : -1);
       ev[i] = __builtin_bit_cast(u16x8,
                                  *reinterpret_cast<const u32x4*>(a.table + (int64_t)v * (2 * H) + (h * HC + c) * 8));
     }
