@@ -22,7 +22,7 @@ E = torch.randn((V, k), generator=g, device="cuda")
 E /= E.max(0, keepdim=True).values - E.min(0, keepdim=True).values
 T = runtime.pack_table(E, plan.in_pad, torch.bfloat16)
 del E
-variants = ["1", "5", "0", "blaslt"]
+variants = [v for v in os.environ.get("PTAB_VARIANTS", "1,5,0,blaslt").split(",")]
 outs = {}
 times = {v: [] for v in variants}
 
