@@ -63,6 +63,9 @@ using namespace c3;
 // (barriers only), 2 = loads without folds, 3 = folds of constants without loads
 // diagnostics (results wrong): RW_ROWS_L2 = 1 reads every row from the first 1024 vertices
 // (an L2-resident 1 MB): the row loads' cost without their HBM latency
+#ifndef RW_LSTAMP
+#define RW_LSTAMP 0
+#endif
 #ifndef RW_ROWS_L2
 #define RW_ROWS_L2 0
 #endif
@@ -294,6 +297,10 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
     const int x = tid - CW * 64;
     const int lc = x % HC, lr = x / HC;
     u16x8 eA[G][3], eB[G][3];
+    // diagnostics (RW_LSTAMP): the first loader thread of workgroup 0 stamps its arrival at
+    // each barrier of the second tile (stamps 34 + j)
+    unsigned long long* lst = nullptr;
+    if (RW_LSTAMP && a.stamps != nullptr && x == 0 && bid == 0) lst = a.stamps + 34;
     auto load_group = [&](int h, int set, int g, u16x8 (&e)[G][3]) {
       if constexpr (RW_LOADER_IDLE == 1 || RW_LOADER_IDLE == 3) {  // diagnostics: no loads
 #pragma unroll
@@ -393,6 +400,13 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
           if (has_next) {
             load_group(1, nxt, 0, eA);
             load_group(1, nxt, 1, eB);
+          }
+        }
+        if constexpr (RW_LSTAMP) {
+          if (lst != nullptr && tile == tb + 1) {
+            __builtin_amdgcn_sched_barrier(0);
+            lst[j] = wall_clock64();
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
         lbar();
