@@ -347,6 +347,55 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
         constexpr int j = decltype(J)::value;
         constexpr bool E = RW_SCHED == 1;
         if constexpr (j == 0) pix_put(px, tile, x);  // (the previous tile's head has read rpix)
+        if constexpr (RW_SCHED == 2) {
+          // balanced: the zy folds over intervals 1, 3, 5 (4, 4, 8 items), the records and
+          // pixels issued in interval 7 (no other loader work there)
+          if constexpr (j == 1) {
+            store_group(cur, 0, eA);
+            load_group(1, cur, 2, eA);
+          }
+          if constexpr (j == 3) {
+            store_group(cur, 1, eB);
+            load_group(1, cur, 3, eB);
+          }
+          if constexpr (j == 5) {
+            store_group(cur, 2, eA);
+            store_group(cur, 3, eB);
+            if (has_next) {
+              load_group(0, nxt, 0, eA);
+              load_group(0, nxt, 1, eB);
+            }
+          }
+          if constexpr (j == 7) {
+            if (tile + 2 < te) {
+              r0 = rec_issue(tile + 2, x);
+              r1 = rec_issue(tile + 2, x + LT);
+            }
+            if (has_next) px = pix_issue(tile + 1, x);
+          }
+          if constexpr (j == 9) {
+            if (has_next) {
+              store_group(nxt, 0, eA);
+              store_group(nxt, 1, eB);
+              load_group(0, nxt, 2, eA);
+              load_group(0, nxt, 3, eB);
+            }
+          }
+          if constexpr (j == 11) {
+            if (has_next) {
+              store_group(nxt, 2, eA);
+              store_group(nxt, 3, eB);
+              load_group(1, nxt, 0, eA);
+              load_group(1, nxt, 1, eB);
+            }
+          }
+          if constexpr (j == 12) {
+            if (tile + 2 < te) {
+              rec_put(r0, cur, x);
+              rec_put(r1, cur, x + LT);
+            }
+          }
+        } else {
         if constexpr (j == 1) {
           store_group(cur, 0, eA);
           store_group(cur, 1, eB);
@@ -401,6 +450,7 @@ __global__ __launch_bounds__((WP<L_, S_>::THREADS)) void rprojw_kernel(const Rch
             load_group(1, nxt, 0, eA);
             load_group(1, nxt, 1, eB);
           }
+        }
         }
         if constexpr (RW_LSTAMP) {
           if (lst != nullptr && tile == tb + 1) {
