@@ -26,11 +26,12 @@
 // Interval j ends at barrier j; the odd ones (1 .. 11) are the MFMA phases.  Loader side,
 // in groups of 12 row loads per thread (two register sets, A and B), every fold into Z in
 // an MFMA phase so that the epilogue intervals stay short:
-//   1: fold zy(i) g0, g1; load zy(i) g2 -> A, g3 -> B
-//   3: fold zy(i) g2, g3                      (zy complete before layer s's start: 2s - 1)
-//   5: load z0(i + 1) g0 -> A, g1 -> B
+//   1: fold zy(i) g0; load zy(i) g2 -> A
+//   3: fold zy(i) g1; load zy(i) g3 -> B
+//   5: fold zy(i) g2, g3 (zy complete before layer s's start: 2s - 1); load z0(i + 1) g0 -> A, g1 -> B
+//   7: load records(i + 2), pixels(i + 1)
 //   9: fold z0(i + 1) g0, g1 (Z free after barrier 2s - 1); load g2 -> A, g3 -> B
-//  11: fold z0(i + 1) g2, g3; load records(i + 2), pixels(i + 1); load zy(i + 1) g0 -> A, g1 -> B
+//  11: fold z0(i + 1) g2, g3; load zy(i + 1) g0 -> A, g1 -> B
 //  12: store records(i + 2) (set (tile - first) & 1); 0 (of i + 1): store pixels(i + 1)
 // (zy of the first tile: loaded ahead of the loop.)  The schedule is unrolled, so the
 // compiler's vmcnt waits count each group's loads exactly.
@@ -50,10 +51,13 @@ using namespace c3;
 #ifndef RW_RA
 #define RW_RA 2  // (4: 4 spills, 2.05 vs 1.96 ms per 2M hits; depth 5 / 6 no better)
 #endif
-// loader schedule: 0 = the group loads in MFMA intervals (above), 1 = in the epilogue
-// intervals (2: zy g2 / g3, 6 and 10: z0, 12: the next zy g0 / g1)
+// loader schedule: 2 = the default (below), 0 = the zy folds in intervals 1 and 3 (8 items
+// each) and the records in 11, 1 = as 0 with the group loads in the epilogue intervals.
+// The loader waves are the stragglers of every interval with 8 folds and 24 loads (their
+// barrier arrivals, RW_LSTAMP: 3.7-4.1 us against the compute waves' 2.7-3.3), so 2 spreads
+// the zy folds over 1 / 3 / 5 and moves the records to 7: 1913-1930 vs 1944-1946 us
 #ifndef RW_SCHED
-#define RW_SCHED 0
+#define RW_SCHED 2
 #endif
 // the loader's row loads paced: s_sleep RW_PACE (x 64 cycles) after each item's 3 loads
 #ifndef RW_PACE
