@@ -1002,6 +1002,43 @@ def cpu_baselines(args, device):
     return out
 
 
+def summary_of(line):
+    """Compact digest of the line's legs (times in us, rates in M/s or G/s), emitted as the
+    line's last key."""
+    def us(x):
+        return None if x is None else round(x * 1e3, 2)
+
+    def get(d, *path):
+        for p in path:
+            if not isinstance(d, dict) or p not in d:
+                return None
+            d = d[p]
+        return d
+
+    s = {"B_us": us(line["ms_per_step"]), "B_Mrays": round(line["value"] / 1e6, 2),
+         "stages_us": {k: us(v.get("ms")) for k, v in (line.get("stages") or {}).items()},
+         "chain3_frac": round(line["roofline"]["frac"], 4)}
+    for name, leg in (line.get("secondary") or {}).items():
+        s[name + "_us"] = us(leg.get("ms_per_step"))
+    s["D_us"] = us(get(line, "config_D", "ms_per_step"))
+    s["large_us"] = {k: us(v.get("ms_per_step")) for k, v in (line.get("large_batch") or {}).items()}
+    def r4(x):
+        return None if x is None else round(x, 4)
+
+    s["render_ms"] = r4(get(line, "render", "ms_per_frame"))
+    s["render_Gpix"] = None if s["render_ms"] is None else round(line["render"]["value"] / 1e9, 3)
+    s["projection_ms"] = r4(get(line, "render", "projection_ms"))
+    s["render_coherent_ms"] = r4(get(line, "render", "variants", "coherent_ids_50pct", "ms_per_frame"))
+    s["strong_local_us"] = {k: {sh: us(t) if isinstance(t, float) else t for sh, t in v["ms_per_step"].items()}
+                            for k, v in (line.get("strong_scaling_local_steps") or {}).items()}
+    dp = line.get("data_parallel")
+    if dp:
+        s["dp_us"] = {k: us(v["ms_per_step"]) for k, v in dp.items() if isinstance(v, dict) and "ms_per_step" in v}
+    s["rff_us"] = us(get(line, "extrinsic_rff", "ms_per_step"))
+    s["cpu_rays"] = r4(get(line, "cpu_baseline", "value"))
+    return s
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1252,6 +1289,9 @@ def main():
             "psnr_vs_ref": psnr,
             "cpu_baseline": cpu,
         }
+        # last key: every leg's headline number in a few hundred bytes, so the tail of the
+        # line (a driver keeps the last 8 KB of stdout) carries them all
+        line["summary"] = summary_of(line)
         print(json.dumps(line))
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
