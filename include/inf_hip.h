@@ -331,8 +331,11 @@ int inf_debug_timing(inf_plan* plan, unsigned long long* stamps_dev, int max_ste
  * (lgemm, register-streamed chain path) records the 100 MHz wall clock at entry, after its
  * operand prologue, after its main loop and at exit: stamps_dev[block * 8 + i], block in
  * launch order (before the XCD remap); with the update fused in, also [4] ticket taken,
- * [5] items decided, [6] / [7] around its update item (8 words per block).  Pass null to
- * turn it off. */
+ * [5] items decided, [6] / [7] around its update item (8 words per block).  The update
+ * launch's workgroups (one work item each) record at stamps_dev[(6144 + item) * 8 + i]:
+ * [0] entry, [1] item and segment loaded, [2] the item's data loaded, [3] its stores
+ * issued, [4] exit after its stores completed (matrix items; the buffer must hold 8192
+ * blocks).  Pass null to turn it off. */
 int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
 
 /* Diagnostics: the kernel path the last inf_train_step took -- 0 layered GEMMs, 2 the
@@ -340,8 +343,8 @@ int inf_debug_block_times(inf_plan* plan, unsigned long long* stamps_dev);
  * (csrc/chain3.hip), 4 the same with the feature tile streamed in chunks (k_pad > 1024),
  * 5 the same in 64-ray tiles (batches above 8192 rays), 6 the fused fp32 chain of the
  * fp32 mode (csrc/chainf.hip), 7 the split-bf16 register chain of the bf16x3 mode
- * (csrc/chain3.hip X3), 8 the large-batch layer GEMMs (csrc/layer.hip, opt-in
- * INF_BIG_LAYERED=1); -1 before any step. */
+ * (csrc/chain3.hip X3), 10 the register-streamed chain after zg.hip's gather + input-layer
+ * GEMM launch (the default for k_pad > 1024); -1 before any step. */
 int inf_plan_last_step_path(const inf_plan* plan);
 
 /* Weight generation: a counter of the launches issued through this plan that may have

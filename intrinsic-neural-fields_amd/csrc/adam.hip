@@ -24,7 +24,17 @@ template <typename T>
 __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   __shared__ float tile[ADAM_TILE_C][ADAM_TILE_R + 1];
   __shared__ adam_dev::Scalars sc;
-  adam_dev::update_item<T>(a, a.items[blockIdx.x], tile, sc);
+  unsigned long long* st = a.stamps != nullptr ? a.stamps + (int64_t)blockIdx.x * 8 : nullptr;
+  adam_dev::stamp(st, 0);
+  // (every thread forming the step's scalars itself instead of thread 0 + an LDS barrier,
+  // update_item LOCAL_SC, measured 8.5 vs 8.1 us per launch: the barrier is not on the
+  // critical path -- the stamps (tools/update_items.py) put it in the data: ~1.5 us of loads
+  // at ~12 TB/s from the MALL, then ~2 us of stores, profiles/r06/update/)
+  adam_dev::update_item<T>(a, a.items[blockIdx.x], tile, sc, st);
+  if (st != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    adam_dev::stamp(st, 4);
+  }
 }
 
 // one item per workgroup: a 64 x 32 matrix tile (row-major [64][32] in the staging, zero

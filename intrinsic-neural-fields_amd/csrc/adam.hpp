@@ -38,6 +38,9 @@ struct AdamSeg {
   int32_t pad2_;
 };
 
+// inf_debug_block_times: the update launch's stamps start at this block of the buffer
+constexpr int UPDATE_STAMP_BLOCK0 = 6144;
+
 // Matrix work item = one ADAM_TILE_R x ADAM_TILE_C tile; vector item = ADAM_VEC elements.
 constexpr int ADAM_TILE_R = 64;
 constexpr int ADAM_TILE_C = 32;
@@ -78,6 +81,10 @@ struct AdamArgs {
   int32_t write_shadow;
   int32_t step_host;    // > 0: use this t and lr_host, else ctrl->step and ctrl->lr
   double lr_host;       // used as given (0 included) when step_host > 0
+  // ... and then 1 - beta^step_host from the host's std::pow (torch forms beta ** step with
+  // the platform libm's pow, as inf_adam_dense does); device-counted steps (ctrl->step) use
+  // adam_dev::pow_int, a few double ulps from it before the fp32 rounding
+  double bc1_host, bc2_host;
   inf_ctrl* ctrl;
   // end-of-step item (AdamItem.seg < 0): fixed-order sum of the fused chain's per-tile
   // loss / SSE partials into ctrl, and the batch-index advance of a replayed epoch
@@ -93,6 +100,10 @@ struct AdamArgs {
   int64_t g_base;
   char* wsh;
   int64_t w_base;
+  // diagnostics (inf_debug_block_times): wave 0 of item workgroup i stamps the wall clock
+  // (100 MHz) at entry, item + segment loaded, data loaded, update stored, exit:
+  // stamps[i * 8 + 0..4] (null: off)
+  unsigned long long* stamps;
 };
 
 int launch_update(const AdamArgs& a, int mode, hipStream_t stream);

@@ -32,6 +32,28 @@ struct Scalars {
   float bc2_sqrt;  // sqrt(1 - b2^t)
 };
 
+// The step's bias-correction scalars, by every thread that needs them (uniform: the same
+// double arithmetic on every lane, so bitwise the value one thread would publish in LDS)
+__device__ __forceinline__ Scalars step_scalars(const AdamArgs& a) {
+  // host-driven step (step_host > 0): t, lr and the bias corrections as given, lr = 0
+  // included (a frozen group); otherwise t and lr from ctrl (graph-replayed steps)
+  double lr = a.lr_host, bc1 = a.bc1_host, bc2 = a.bc2_host;
+  if (a.step_host <= 0) {
+    const int t = a.ctrl->step;
+    lr = a.ctrl->lr;
+    bc1 = 1.0 - pow_int(a.beta1_d, t);
+    bc2 = 1.0 - pow_int(a.beta2_d, t);
+  }
+  Scalars s;
+  s.step_neg = (float)(-(lr / bc1));
+  s.bc2_sqrt = (float)sqrt(bc2);
+  return s;
+}
+
+__device__ __forceinline__ void stamp(unsigned long long* st, int i) {
+  if (st != nullptr && threadIdx.x == 0) st[i] = wall_clock64();
+}
+
 // torch's single-tensor Adam op by op (torch/optim/adam.py, CPU kernels), with the
 // roundings pinned so no code path's FMA contraction can move a bit (the compiler contracted
 // differently in different inlined copies, which made two update paths disagree in the last
@@ -254,7 +276,8 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
 // in-launch hand-off of lgemm.hip: they were stored sc1 by other workgroups of the launch)
 template <typename T, bool VEC4, int PB, bool SC1>
 __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
-                                            const Scalars& sc, float (*tile)[ADAM_TILE_R + 1]) {
+                                            const Scalars& sc, float (*tile)[ADAM_TILE_R + 1],
+                                            unsigned long long* st = nullptr) {
   const int tid = threadIdx.x;
   const int c4 = tid & 7, rb = tid >> 3;
   const int cl = 4 * c4;
@@ -350,7 +373,12 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
       }
     }
   }
+  if (st != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(st, 2);
+  }
   mt_apply<T, VEC4>(a, seg, item, sc, tile, ok, e, w, m, v, g);
+  stamp(st, 3);
 }
 
 // NI matrix items of one segment, software-pipelined: the next item's parameters, Adam
@@ -365,20 +393,7 @@ __device__ __forceinline__ void matrix_items_pipelined(const AdamArgs& a, const 
   const int tid = threadIdx.x;
   const int c4 = tid & 7, rb = tid >> 3;
   const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
-  if (a.do_adam && tid == 0) {
-    int t = a.step_host;
-    double lr = a.lr_host;
-    // host-driven step (step_host > 0): t and lr as given, lr = 0 included (a frozen
-    // group); otherwise both from ctrl (graph-replayed steps)
-    if (t <= 0) {
-      t = a.ctrl->step;
-      lr = a.ctrl->lr;
-    }
-    const double bc1 = 1.0 - pow_int(a.beta1_d, t);
-    const double bc2 = 1.0 - pow_int(a.beta2_d, t);
-    sc.step_neg = (float)(-(lr / bc1));
-    sc.bc2_sqrt = (float)sqrt(bc2);
-  }
+  if (a.do_adam && tid == 0) sc = step_scalars(a);
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg.slab), (short)0, 0x7FFFFFFF, 0x00020000);
   const int ns = seg.nslab;
@@ -452,18 +467,7 @@ __device__ __forceinline__ void matrix_items_lds(const AdamArgs& a, const AdamSe
   const int tid = threadIdx.x;
   const int c4 = tid & 7, rb = tid >> 3;
   const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
-  if (a.do_adam && tid == 0) {
-    int t = a.step_host;
-    double lr = a.lr_host;
-    if (t <= 0) {
-      t = a.ctrl->step;
-      lr = a.ctrl->lr;
-    }
-    const double bc1 = 1.0 - pow_int(a.beta1_d, t);
-    const double bc2 = 1.0 - pow_int(a.beta2_d, t);
-    sc.step_neg = (float)(-(lr / bc1));
-    sc.bc2_sqrt = (float)sqrt(bc2);
-  }
+  if (a.do_adam && tid == 0) sc = step_scalars(a);
   struct Regs {
     bool ok[NR];
     int64_t e[NR];
@@ -547,11 +551,14 @@ __device__ inline void finish_step(const AdamArgs& a) {
 // One work item (adam.hpp AdamItem) on 256 threads: a matrix tile, a vector chunk or the
 // end-of-step item.  `tile` and `sc` are the caller's LDS.
 // VT: vector-partial loads in flight per thread; PB, SC1: matrix_tile; VEC_ONLY: the caller
-// runs vector / end-of-step items only (the dW GEMM's leading blocks, lgemm.hip AUX): the
-// matrix path is not compiled into it
-template <typename T, int VT = 64, int PB = 8, bool SC1 = false, bool VEC_ONLY = false>
+// runs vector / end-of-step items only: the matrix path is not compiled into it
+// LOCAL_SC: one item per workgroup (the update launch): every thread forms the step's
+// scalars itself, so no LDS hand-off and no barrier stand between the item's table loads and
+// its data loads (callers that run several items per workgroup keep the barrier, which also
+// separates one item's LDS tile from the next).  `st`: diagnostics stamps (AdamArgs::stamps).
+template <typename T, int VT = 64, int PB = 8, bool SC1 = false, bool VEC_ONLY = false, bool LOCAL_SC = false>
 __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& item, float (*tile)[ADAM_TILE_R + 1],
-                                            Scalars& sc) {
+                                            Scalars& sc_lds, unsigned long long* st = nullptr) {
   if (item.seg < 0) {
     if ((a.nloss > 0 || a.advance) && a.ctrl != nullptr) finish_step(a);
     return;
@@ -559,28 +566,22 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
   const AdamSeg seg = a.segs[item.seg];
   const int tid = threadIdx.x;
 
-  if (a.do_adam && tid == 0) {
-    int t = a.step_host;
-    double lr = a.lr_host;
-    // host-driven step (step_host > 0): t and lr as given, lr = 0 included (a frozen
-    // group); otherwise both from ctrl (graph-replayed steps)
-    if (t <= 0) {
-      t = a.ctrl->step;
-      lr = a.ctrl->lr;
-    }
-    const double bc1 = 1.0 - pow_int(a.beta1_d, t);
-    const double bc2 = 1.0 - pow_int(a.beta2_d, t);
-    sc.step_neg = (float)(-(lr / bc1));
-    sc.bc2_sqrt = (float)sqrt(bc2);
+  Scalars sc_loc{0.f, 1.f};
+  if constexpr (LOCAL_SC) {
+    if (a.do_adam) sc_loc = step_scalars(a);
+  } else {
+    if (a.do_adam && tid == 0) sc_lds = step_scalars(a);
+    if (a.do_adam) lds_barrier();
   }
-  if (a.do_adam) lds_barrier();
+  const Scalars& sc = LOCAL_SC ? sc_loc : sc_lds;
 
   if (seg.matrix) {
     if constexpr (!VEC_ONLY) {
+      stamp(st, 1);
       if (item.pad & ITEM_VEC4)
-        matrix_tile<T, true, PB, SC1>(a, seg, item, sc, tile);
+        matrix_tile<T, true, PB, SC1>(a, seg, item, sc, tile, st);
       else
-        matrix_tile<T, false, PB, SC1>(a, seg, item, sc, tile);
+        matrix_tile<T, false, PB, SC1>(a, seg, item, sc, tile, st);
     }
   } else {
     // vector chunk: ADAM_VEC (64) consecutive elements; wave w sums the partials w, w + 4,

@@ -136,7 +136,7 @@ struct L3 {
 // once, at its first block (two barriers: everyone is done with the previous chunk /
 // the new one is in LDS), and the store wave copies its X^T between them.
 // NR: 16-ray tiles per workgroup (1, or C3_NR_WIDE for large batches; not with ENC).
-// ZP: the input layers were computed ahead of the chain (igemm.hip: Z = [W_0; W_y] X^T in
+// ZP: the input layers were computed ahead of the chain (zg.hip: Z = [W_0; W_y] X^T in
 // the accumulator layout, X^T written by its gather): no gather here, phase 0 is the
 // layer-0 epilogue on Z, the skip layer adds W_y x from LDS (staged by the store wave with
 // direct-to-LDS loads) in its epilogue, and the weight stream holds the hidden layers only.

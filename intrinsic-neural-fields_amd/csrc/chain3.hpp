@@ -67,7 +67,7 @@ struct Chain3Args {
   // dZ^T outputs are hi / lo image pairs for lgemm's SPLIT dW (lo image at + features x rows)
   int32_t x3;
   const float* table_f32;
-  // precomputed input layers (igemm.hip): Z = [W_0; W_y] X^T without biases, fp32, in the
+  // precomputed input layers (zg.hip): Z = [W_0; W_y] X^T without biases, fp32, in the
   // accumulator layout ([rows / 16][2H / 16] KiB); X^T already written (null: the kernel
   // gathers and streams W_0 / W_y itself)
   const float* zin;
@@ -95,12 +95,6 @@ struct Chain3Args {
   float inv_count;
   inf_ctrl* ctrl;
   int32_t count_step;
-  // chain4 (large batches, csrc/chain4.hip): the fragment images by role -- W_0, W_y, the
-  // hidden layers' forward images wf[1 .. L-2] (Lx at the skip layer) and backward wb[..]
-  const bf16* w0_img;
-  const bf16* wy_img;
-  const bf16* wf[CHAIN_MAX_HIDDEN];
-  const bf16* wb[CHAIN_MAX_HIDDEN];
   // diagnostics: wall-clock stamps (100 MHz) of wave 0 of the first and the last
   // workgroup: [2][nphase * 5 + 6] = entry, {phase start, MFMAs done, epilogue done} ...,
   // end, weight prologue issued, feature tile written, barrier 0 passed, {after B1} ...,
@@ -113,7 +107,7 @@ struct Chain3Args {
 // stream (4096 rays -> 256 workgroups).  Larger batches fill the chip with 16-ray tiles many
 // times over and pay the stream once per 16 rays: there a workgroup takes C3_NR_WIDE tiles
 // (64 rays; 65,536 rays -> 1024 workgroups), each weight fragment feeding C3_NR_WIDE MFMAs.
-// tables above this size are read with non-temporal row loads (chain3.hip, igemm.hip)
+// tables above this size are read with non-temporal row loads (chain3.hip, zg.hip)
 constexpr size_t C3_NT_TABLE_BYTES = (size_t)256 << 20;
 constexpr int64_t CHAIN3_MAX_ROWS = 8192;
 #ifndef C3_NR_WIDE_DEF  // experiments (variant libraries only)
@@ -165,17 +159,5 @@ inline int chain3_kc(int k_pad, int64_t rows) {
 
 int launch_chain3(const Chain3Args& a, int bm, hipStream_t stream);
 
-// chain4.hip: the large-batch step on 128-ray workgroups of eight waves (two per SIMD),
-// the 8-layer H = 256 field (configs B / C / D / E) above CHAIN3_MAX_ROWS: 2-3 % under
-// chain3's 64-ray tiles at 65,536 rays; INF_CHAIN4=0 keeps chain3's
-constexpr int C4_BM = 128;
-constexpr int C4_KC = 64;  // feature columns gathered per chunk (two chunks in flight)
-constexpr int C4_STAMPS = 256;  // diagnostics: wall-clock stamps per stamped workgroup
-inline bool chain4_supported(int H, int L, int k_pad, int64_t rows) {
-  const char* e = std::getenv("INF_CHAIN4");
-  return H == 256 && L == 8 && k_pad % (2 * C4_KC) == 0 && rows % C4_BM == 0 && rows > CHAIN3_MAX_ROWS &&
-         rows <= CHAIN3_WIDE_MAX_ROWS && (e == nullptr || e[0] != '0');
-}
-int launch_chain4(const Chain3Args& a, hipStream_t stream);
 
 }  // namespace inf

@@ -87,14 +87,11 @@ __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\
 // GT (FUSED with LgemmBatch::fused == 2): split-K 1, and each block runs the update items of
 // its own tile on the gradient tile in LDS (adam_dev::matrix_items_lds) -- no slab, no
 // separate update launch; BN 64 keeps 224 blocks at config B.
-// AUX (LgemmBatch::aux_only): the first n_aux blocks run the update's vector / end-of-step
-// items, the rest the plain slab GEMM (the matrix items follow in the update launch).
-template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1, bool AUX = false>
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
 __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch) {
   static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
   static_assert(!GT || FUSED, "the gradient-tile update is a fused mode");
   static_assert(KS == 1 || (!FUSED && !GT), "k-split groups: the plain slab / C epilogues only");
-  static_assert(!AUX || (!FUSED && !SPLIT), "vector items beside the plain bf16 slab GEMM");
   constexpr int NP = SPLIT ? 2 : 1;
   using C = LG<BM, NP, BN, GT, KS>;
   constexpr int TM = C::TM, TN = C::TN, D = C::D, RA = C::RA, ACH = C::ACH;
@@ -104,19 +101,15 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
   float(*const atile)[ADAM_TILE_R + 1] = reinterpret_cast<float(*)[ADAM_TILE_R + 1]>(smem + C::ATILE_OFF);
   adam_dev::Scalars& asc =
       *reinterpret_cast<adam_dev::Scalars*>(smem + C::ATILE_OFF + ADAM_TILE_C * (ADAM_TILE_R + 1) * 4);
-  if constexpr (FUSED || AUX) {
+  if constexpr (FUSED) {
     if ((int)blockIdx.x < batch.n_aux) {
-      // (the update kernel's vector sum order either way: partial w, w + 4, ... per wave)
-      if ((int)blockIdx.x < batch.n_aux_items) {
-        if constexpr (AUX)
-          adam_dev::update_item<bf16, 64, 4, false, true>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
-        else
-          adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
-      }
+      // (the update kernel's vector sum order: partial w, w + 4, ... per wave)
+      if ((int)blockIdx.x < batch.n_aux_items)
+        adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
       return;
     }
   }
-  const int gblk = (int)blockIdx.x - ((FUSED || AUX) ? batch.n_aux : 0);  // n_aux % 8 == 0: same XCD order
+  const int gblk = (int)blockIdx.x - (FUSED ? batch.n_aux : 0);  // n_aux % 8 == 0: same XCD order
   unsigned long long* const stl =
       (batch.stamps != nullptr && threadIdx.x == 0) ? batch.stamps + 8 * (size_t)gblk : nullptr;
   if (stl != nullptr) stl[0] = wall_clock64();
@@ -433,17 +426,17 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
   }
 }
 
-template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1, bool AUX = false>
+template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
 int launch_typed(const LgemmBatch& b, hipStream_t stream) {
   constexpr int lds = LG<BM, SPLIT ? 2 : 1, BN, GT, KS>::LDS;
   static bool attr = false;
   if (!attr) {
-    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS, AUX>,
+    INF_HIP_TRY(hipFuncSetAttribute((const void*)lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
-  lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS, AUX>
-      <<<dim3((unsigned)(b.total_blocks + ((FUSED || AUX) ? b.n_aux : 0))), dim3(256 * KS), lds, stream>>>(b);
+  lgemm_kernel<BM, FUSED, SPLIT, BN, GT, KS>
+      <<<dim3((unsigned)(b.total_blocks + (FUSED ? b.n_aux : 0))), dim3(256 * KS), lds, stream>>>(b);
   INF_LAUNCH_CHECK();
   return INF_OK;
 }
@@ -454,30 +447,11 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   INF_CHECK_ARG(bm == 32 || bm == 64, "lgemm: rows per block");
   INF_CHECK_ARG(b.nprob >= 1 && b.nprob <= LGEMM_MAX_PROBLEMS, "lgemm: problem count");
   const bool gt = b.fused == 2;  // split-K 1, the update on the LDS gradient tile
-  // Gradient tiles: 64 x 64, or 128 x 128 with INF_LGF_TILE=128 (config D: 608 blocks of 64 x
-  // 64, 2.4 per CU, each streaming 1 MB of operand panels for 33.5 MFLOP; 152 of 128 x 128,
-  // 2 MB for 134 MFLOP -- half the operand stream per FLOP, but see below).
-  // (INF_LGF_BN=128: 64 x 128 gradient tiles -- config D's dW + update 44.8 -> 49.8 us, step
-  // 128.7 -> 133.4 us: half the blocks at 2.4 -> 1.2 per CU, each a longer chain)
-  const char* e_gbn = std::getenv("INF_LGF_BN");
-  int gt_bn = e_gbn != nullptr && std::atoi(e_gbn) == 128 ? 128 : 64;
-  if (gt) {
-    int64_t blocks64 = 0;
-    bool ok128 = true;
-    for (int i = 0; i < b.nprob; ++i) {
-      blocks64 += (int64_t)(b.p[i].M / 64) * (b.p[i].N / 64);
-      ok128 = ok128 && b.p[i].M % 128 == 0 && b.p[i].N % 128 == 0;
-    }
-    // (measured slower at config D: dW + update 45.2 -> 60.0 us -- one wave per SIMD streams
-    // 2 MB per block at the lone-wave rate; opt-in)
-    const char* e_t = std::getenv("INF_LGF_TILE");
-    const bool t128 = e_t != nullptr && std::atoi(e_t) == 128 && blocks64 > 0;
-    if (t128 && ok128) {
-      bm = 128;
-      gt_bn = 128;
-    }
-  }
-  const int bn = gt ? gt_bn : LG_BN;
+  // Gradient tiles of the fused update: 64 x 64 (config D: 608 blocks, 2.4 per CU, each
+  // streaming 1 MB of operand panels for 33.5 MFLOP).  Measured and removed (round 6): 64 x 128
+  // (dW + update 44.8 -> 49.8 us: half the blocks, each a longer chain) and 128 x 128 tiles
+  // (45.2 -> 60.0 us: one wave per SIMD streams 2 MB per block at the lone-wave rate).
+  const int bn = gt ? 64 : LG_BN;
   int blocks = 0;
   for (int i = 0; i < b.nprob; ++i) {
     LgemmProblem& p = b.p[i];
@@ -499,11 +473,10 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   }
   b.total_blocks = blocks;
   if (gt) {
-    INF_CHECK_ARG((bm == 64 || bm == 128) && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.adam.items != nullptr,
+    INF_CHECK_ARG(bm == 64 && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.adam.items != nullptr,
                   "lgemm: gradient-tile update layout");
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: the vector items reduce their slabs");
-    if (bm == 128) return launch_typed<128, true, false, 128, true>(b, stream);
-    return gt_bn == 128 ? launch_typed<64, true, false, 128, true>(b, stream) : launch_typed<64, true, false, 64, true>(b, stream);
+    return launch_typed<64, true, false, 64, true>(b, stream);
   }
   if (b.fused) {
     INF_CHECK_ARG(b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.counters != nullptr, "lgemm: fused update layout");
@@ -513,7 +486,6 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: fused update reduces the slabs");
   }
   INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
-  INF_CHECK_ARG(!(b.aux_only && (b.fused || b.split)), "lgemm: vector-item blocks: plain bf16 slab GEMM only");
   // the slab / C paths: two k groups per block where every block's K range splits into an
   // even number of 64-deep stages, each a multiple of RA (the default): the split-operand
   // (bf16x3) dW 122.3 -> 120.9 us per step, the bf16 step 64.1 -> 63.5 us (dW 14.8 -> 14.4,
@@ -530,13 +502,6 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
   }
   if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
-  if (b.aux_only) {
-    INF_CHECK_ARG(bm == 64 && b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.aux_items != nullptr,
-                  "lgemm: vector-item blocks layout");
-    for (int i = 0; i < b.nprob; ++i) INF_CHECK_ARG(b.p[i].slab != nullptr, "lgemm: vector-item blocks: slab path only");
-    return ks2 ? launch_typed<64, false, false, LG_BN, false, 2, true>(b, stream)
-               : launch_typed<64, false, false, LG_BN, false, 1, true>(b, stream);
-  }
   if (ks2) return launch_typed<64, false, false, LG_BN, false, 2>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }

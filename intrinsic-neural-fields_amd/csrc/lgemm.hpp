@@ -62,11 +62,6 @@ struct LgemmBatch {
   // fused == 2 ("gradient tile"): split-K 1 with 64 x 64 tiles, each block runs its own
   // tile's items on the gradient in LDS (no slab, no counters).
   int32_t fused;
-  // aux_only (with fused == 0): the first n_aux blocks run the vector and end-of-step items
-  // (adam.aux) while the rest compute the split-K slabs; the matrix items stay in the
-  // update launch that follows -- the leading blocks land on the CUs the GEMM's grid leaves
-  // idle, and the update launch loses the vector items' partial reads
-  int32_t aux_only;
   int32_t n_aux, n_aux_items;
   const AdamItem* aux_items;
   int32_t* counters;

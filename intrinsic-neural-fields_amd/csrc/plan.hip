@@ -8,6 +8,7 @@
 //   -> L-2 dX GEMMs (ReLU mask + bias-grad partials) -> ONE grouped split-K dW GEMM over
 //   all weight matrices -> ONE update launch (slab reduction + Adam + packed weights).
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -21,9 +22,7 @@
 #include "gemm.hpp"
 #include "head.hpp"
 #include "fgemm.hpp"
-#include "igemm.hpp"
 #include "zg.hpp"
-#include "layer.hpp"
 #include "lgemm.hpp"
 #include "rchain.hpp"
 #include "blaslt.hpp"
@@ -56,7 +55,6 @@ constexpr int64_t ALIGN = 256;
 // inf_plan::last_chain of a step on the fused fp32 chain (chainf.hip)
 constexpr int CHAIN_F32 = 6;
 constexpr int CHAIN_X3 = 7;  // the split-bf16 register chain (chain3.hip X3) of the bf16x3 mode
-constexpr int CHAIN_BIG = 8;  // the large-batch layer GEMMs (layer.hip, INF_BIG_LAYERED=1)
 
 }  // namespace
 }  // namespace inf
@@ -81,7 +79,6 @@ struct inf_plan {
   // (lgemm.hip GT) -- no split-K slabs, no update launch (config D; INF_LGF=0/1 forces it)
   bool lgf = false;
   bool last_lgf = false;  // the last training step took it
-  bool last_chain4 = false;  // the last fused bf16 step ran chain4.hip (128-ray workgroups)
   bool last_zg = false;      // ... its input layers on zg.hip ahead of chain3
   int train_unit = 128;
   int bp_max = 0;
@@ -93,13 +90,10 @@ struct inf_plan {
   // workspace layout (byte offsets)
   int64_t o_x0 = 0, o_x0t = 0, o_dz = 0, o_pred = 0, o_tables = 0, o_tables_b = 0, o_ws_end = 0;
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
-  int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (igemm.hip / zg.hip), fp32 [parts][bp_max][2H]
+  int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (zg.hip), fp32 [parts][bp_max][2H]
   int zin_parts_max = 0;       // k slices o_zin holds
   int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
   // the matrix items alone (the update launch after a dW GEMM that ran the vector items)
-  int64_t o_mat_items = 0;
-  int n_mat_items = 0;
-  bool last_aux_dw = false;  // the last training step ran its vector items in the dW launch
   // sharded update (data parallel, inf_plan_shard): the item-major staging layout of
   // `shard_world` ranks, this rank's items (+ the end-of-step item) as their own table
   int shard_world = 0, shard_rank = 0;
@@ -174,6 +168,8 @@ struct inf_plan {
 namespace {
 
 int64_t align_up(int64_t x) { return round_up(x, ALIGN); }
+
+static bool use_zg(const inf_plan* p);
 
 int build_layout(inf_plan* p) {
   const auto& d = p->d;
@@ -313,10 +309,10 @@ int build_layout(inf_plan* p) {
   p->o_x0t = take((int64_t)p->k_pad * Bp * p->esz);
   if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS)
     for (int i = 0; i < 2; ++i) p->o_xp[i] = take(Bp * p->k_pad * 2);
-  if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS &&
-      (igemm_supported(H, p->k_pad, Bp) || zg_supported(H, p->k_pad, Bp))) {
-    // zg.hip's k slices: at most zg_splits of the smallest batch (64 rays)
-    p->zin_parts_max = zg_supported(H, p->k_pad, Bp) ? zg_splits(p->k_pad, 64) : 1;
+  // zg.hip's k slices (at most zg_splits of the smallest batch, 64 rays), only where the
+  // step can run zg (use_zg: k_pad > C3_KC or INF_ZG=1)
+  if (p->mode == INF_MODE_BF16 && Bp <= CHAIN3_MAX_ROWS && zg_supported(H, p->k_pad, Bp) && use_zg(p)) {
+    p->zin_parts_max = zg_splits(p->k_pad, 64);
     p->o_zin = take((int64_t)p->zin_parts_max * Bp * 2 * H * 4);
   }
   const int64_t max_parts =
@@ -347,7 +343,6 @@ int build_layout(inf_plan* p) {
   p->o_tables = take(p->table_bytes);
   p->o_tables_b = take(align_up((int64_t)p->segs.size() * sizeof(AdamSeg)));
   p->o_aux_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
-  p->o_mat_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
   p->o_shard_items = take(align_up((nitems + 1) * sizeof(AdamItem)));
   int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
   for (const auto& g : p->segs)
@@ -488,7 +483,7 @@ int run_forward_layer(inf_plan* p, int Bp, bool transposed, int l, hipStream_t s
 bool use_fgemm(const inf_plan* p, int Bp, int splits);
 bool use_split_lgemm(const inf_plan* p, int Bp);
 int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain = 0, const AdamArgs* fuse = nullptr,
-                     int bucket = 0, const AdamArgs* aux = nullptr);
+                     int bucket = 0);
 
 // Backward from dZ_{L-2} (already produced by head_bwd) to the reduced gradients.
 int run_backward_layers(inf_plan* p, int Bp, hipStream_t st) {
@@ -538,10 +533,8 @@ bool use_split_lgemm(const inf_plan* p, int Bp) {
   return true;
 }
 
-int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket,
-                     const AdamArgs* aux) {
+int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamArgs* fuse, int bucket) {
   const int H = p->H, s = p->s;
-  INF_CHECK_ARG(aux == nullptr || (fuse == nullptr && bucket == 0 && chain == 3), "dW vector items: the chain3 slab path");
   if ((chain == CHAIN_F32 || chain == CHAIN_X3) && use_split_lgemm(p, Bp)) {
     INF_CHECK_ARG(fuse == nullptr, "split-operand dW: no fused update");
     const int splits = bucket ? p->bucket_splits : p->dw_splits;
@@ -584,7 +577,6 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     // large batches (the 64-ray chain tiles): 256 x 256 output tiles over the same images
     // (fgemm.hip), when every matrix is a whole number of them
     if (fuse == nullptr && use_fgemm(p, Bp, splits)) {
-      INF_CHECK_ARG(aux == nullptr, "dW vector items: lgemm only");
       FgemmBatch fb;
       std::memset(&fb, 0, sizeof(fb));
       fb.K = Bp;
@@ -650,13 +642,6 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       lb.n_aux = (int)round_up(p->n_aux_items, 8);
       lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
       lb.counters = p->W<int32_t>(p->o_counters);
-    } else if (aux != nullptr) {
-      // the update's vector / end-of-step items in the GEMM's leading blocks (lgemm.hpp aux_only)
-      lb.aux_only = 1;
-      lb.adam = *aux;
-      lb.n_aux_items = p->n_aux_items;
-      lb.n_aux = (int)round_up(p->n_aux_items, 8);
-      lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
     }
     // (128 x 128 tiles measured slower at 2 and 4 splits: step 75.3 / 71.6 vs 68.1-69.9 us,
     // profiles/r04/lgemm_tile_split_sweep.log; so were 4 splits of 64 x 128: 70.5-70.9)
@@ -719,6 +704,8 @@ AdamArgs update_args(inf_plan* p, int Bp) {
   a.beta2 = (float)p->beta2;
   a.one_minus_b2 = (float)(1.0 - p->beta2);
   a.eps = (float)p->eps;
+  // diagnostics (inf_debug_block_times): the update's item stamps after the dW GEMM's blocks
+  a.stamps = p->lg_stamps != nullptr ? p->lg_stamps + (int64_t)UPDATE_STAMP_BLOCK0 * 8 : nullptr;
   (void)Bp;
   return a;
 }
@@ -768,7 +755,7 @@ int ensure_rowmajor(inf_plan* p, hipStream_t st) {
 // fused chain3 steps in bf16 leave the row-major shadows to ensure_rowmajor
 // (INF_EAGER_SHADOWS=1: every update rewrites all shadows)
 int step_shadow_mode(const inf_plan* p, int chain) {
-  return (((chain == 3 || chain == CHAIN_BIG) && p->mode == INF_MODE_BF16) || ((chain == CHAIN_F32 || chain == CHAIN_X3) && p->mode != INF_MODE_BF16)) &&
+  return ((chain == 3 && p->mode == INF_MODE_BF16) || ((chain == CHAIN_F32 || chain == CHAIN_X3) && p->mode != INF_MODE_BF16)) &&
                  std::getenv("INF_EAGER_SHADOWS") == nullptr
              ? 2
              : 1;
@@ -783,12 +770,9 @@ std::vector<AdamSeg> bucket_segs(const inf_plan* p) {
   return t;
 }
 
-int step_bm(const inf_plan* p, int Bp);
-
 // The bias partial counts depend on the padded batch: refresh the seg table for it.
 int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
-  const int parts = chain == 3 ? Bp / step_bm(p, Bp)
-                    : chain == CHAIN_BIG ? Bp / LY_RAYS
+  const int parts = chain == 3 ? Bp / chain3_bm(Bp)
                     : (chain == CHAIN_F32 || chain == CHAIN_X3) ? Bp / 16
                     : chain ? Bp / chain_partial_rows(chain_bm(Bp))
                             : Bp / 64;
@@ -990,12 +974,6 @@ bool use_fgemm(const inf_plan* p, int Bp, int splits) {
   return true;
 }
 
-// Rays per workgroup of the fused bf16 step at this padded batch (chain3: 16 / 64; chain4:
-// 128) -- one bias / head / loss partial per workgroup
-int step_bm(const inf_plan* p, int Bp) {
-  return p->mode == INF_MODE_BF16 && chain4_supported(p->H, p->L, p->k_pad, Bp) ? C4_BM : chain3_bm(Bp);
-}
-
 bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
   const ParamSeg* w1 = p->weight_seg(1, 0);
   const ParamSeg* w0 = p->weight_seg(0, 0);
@@ -1105,19 +1083,15 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   const bool xc = p->k_pad > kc;
   a.kc = kc;
   a.nchunk = (int)ceil_div(p->k_pad, a.kc);
-  // INF_ZP=1: the input layers ahead of the chain (igemm.hip): gather X / X^T, then
-  // Z = [W_0; W_y] X^T as a GEMM tiled over output features; the chain's stream keeps the
-  // hidden layers only.  Opt-in: at config B the chain drops 42.3 -> 29.4 us but the gather
-  // (9.2 us) and the GEMM (10.6 us) cost more than the 1 MB per-CU L2 stream they replace
-  // -- the GEMM's X tiles come from the MALL at its per-CU rate (profiles/r03/s3/zp_step.json)
-  // INF_ZG=1: the same schedule with gather and GEMM in one launch (zg.hip: 64 rays x all 2H
-  // features x a k slice per workgroup, the slices added by the chain), any k_pad and table size
+  // zg.hip (use_zg: the default for k_pad > C3_KC, INF_ZG=1 forces it): the input layers
+  // ahead of the chain, gather and GEMM in one launch (64 rays x all 2H features x a k slice
+  // per workgroup, the slices added by the chain); the chain's stream keeps the hidden layers
+  // only.  (Round 3 measured the same schedule as a separate gather + GEMM, igemm.hip, at
+  // config B: the chain dropped 42.3 -> 29.4 us but gather 9.2 + GEMM 10.6 us cost more than
+  // the 1 MB per-CU stream they replaced; removed in round 6)
   const int zg_s = zg_splits(p->k_pad, Bp);
   const bool zgp = p->o_zin >= 0 && b->encoding == INF_ENC_NONE && xpre == nullptr && chain3_bm(Bp) == 16 &&
                    zg_supported(H, p->k_pad, Bp) && zg_s <= p->zin_parts_max && use_zg(p);
-  const bool zp = !zgp && p->o_zin >= 0 && b->encoding == INF_ENC_NONE && xpre == nullptr && !xc && chain3_bm(Bp) == 16 &&
-                  igemm_supported(H, p->k_pad, Bp) && b->num_vertices * (int64_t)p->k_pad * 2 < ((int64_t)1 << 32) &&
-                  std::getenv("INF_ZP") != nullptr;
   a.zin_parts = 1;
   p->last_zg = zgp;
   if (zgp) {
@@ -1150,39 +1124,6 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     a.zin = g.Z;
     a.zin_parts = zg_s;
     a.zin_stride = g.z_stride;
-  } else if (zp) {
-    XGatherArgs g;
-    std::memset(&g, 0, sizeof(g));
-    g.table = a.table;
-    g.num_vertices = b->num_vertices;
-    g.k_pad = p->k_pad;
-    g.vids = b->vids;
-    g.vid_dtype = b->vid_dtype;
-    g.bary = b->bary;
-    g.ray_idx = b->ray_idx;
-    g.idx_dtype = b->idx_dtype;
-    g.idx_offset = b->idx_offset;
-    g.num_rays = b->num_rays;
-    g.num_src = b->num_source_rays;
-    g.ctrl = p->ctrl;
-    g.offset_from_ctrl = b->offset_from_ctrl;
-    g.batch = b->batch;
-    g.rows = Bp;
-    g.gather_nt = (size_t)b->num_vertices * (size_t)p->k_pad * 2 > C3_NT_TABLE_BYTES;
-    g.X = p->W<bf16>(p->o_x0);
-    g.XT = p->W<bf16>(p->o_x0t);
-    if ((rc = launch_xgather(g, st))) return rc;
-    IGemmArgs q;
-    std::memset(&q, 0, sizeof(q));
-    q.X = g.X;
-    q.rows = Bp;
-    q.k_pad = p->k_pad;
-    q.H = H;
-    q.W0 = img(p->weight_seg(0, 0), true);
-    q.Wy = img(p->weight_seg(s, 1), true);
-    q.Z = p->W<float>(p->o_zin);
-    if ((rc = launch_igemm(q, st))) return rc;
-    a.zin = q.Z;
   } else if (!xc) {
     for (int i = 0; i < nx; ++i)
       if ((rc = add(img(p->weight_seg(0, 0), true), i * upl, 1, i * upl, 0, i == nx - 1))) return rc;
@@ -1204,8 +1145,8 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
     }
   }
   for (int l = 1; l <= L - 2; ++l) {
-    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || zp || zgp || l != s))) return rc;
-    if (l == s && !xc && !zp && !zgp)
+    if ((rc = add(img(p->weight_seg(l, 0), true), 0, 0, 0, l, xc || zgp || l != s))) return rc;
+    if (l == s && !xc && !zgp)
       for (int i = 0; i < nx; ++i)
         if ((rc = add(img(p->weight_seg(s, 1), true), i * upl, 1, i * upl, l, i == nx - 1))) return rc;
   }
@@ -1234,17 +1175,6 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
   a.count_step = 1;
   a.stamps = p->stamps;
   a.xpre = b->encoding == INF_ENC_NONE ? xpre : nullptr;
-  if (!x3 && b->encoding == INF_ENC_NONE && a.xpre == nullptr && !zp && step_bm(p, Bp) == C4_BM) {
-    a.w0_img = img(p->weight_seg(0, 0), true);
-    a.wy_img = img(p->weight_seg(s, 1), true);
-    for (int l = 1; l <= L - 2; ++l) {
-      a.wf[l] = img(p->weight_seg(l, 0), true);
-      a.wb[l] = img(p->weight_seg(l, 0), false);
-    }
-    p->last_chain4 = true;
-    return launch_chain4(a, st);
-  }
-  p->last_chain4 = false;
   return launch_chain3(a, chain3_bm(Bp), st);
 }
 
@@ -1255,121 +1185,6 @@ int run_chain3(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t
 // Y^T / dZ^T images it writes.  16-ray tiles, k_pad <= 1024, batches lgemm's split-K tiles
 // (Bp / dw_splits a multiple of 256); smaller batches take the layered split-bf16 kernels.
 // INF_NO_CHAIN3X3=1: the layered kernels.
-// Large batches as layer GEMMs with fused epilogues (layer.hip; opt-in INF_BIG_LAYERED=1):
-// the bf16 eigenfunction-table step of H = 256 MLPs on the 64-ray-tile batches (the dW on
-// fgemm, the update as the fused chain's).
-bool use_big(const inf_plan* p, const inf_batch* b, int Bp) {
-  const char* e = std::getenv("INF_BIG_LAYERED");
-  if (e == nullptr || std::atoi(e) == 0) return false;
-  return p->mode == INF_MODE_BF16 && b->encoding == INF_ENC_NONE && b->table != nullptr &&
-         b->table_dtype == INF_DTYPE_BF16 && b->vids != nullptr && layer_supported(p->H, Bp) && chain3_wide(Bp) &&
-         p->k_pad % LY_KC == 0 && b->num_vertices * (int64_t)p->k_pad * 2 < ((int64_t)1 << 32) &&
-         use_fgemm(p, Bp, p->dw_splits) && p->L - 1 <= CHAIN_MAX_HIDDEN;
-}
-
-int run_big(inf_plan* p, const inf_batch* b, int Bp, float* pred, hipStream_t st) {
-  const int H = p->H, L = p->L, s = p->s;
-  int rc;
-  // the gather: X (B-operand image) and X^T (the dW's fragment image)
-  XGatherArgs g;
-  std::memset(&g, 0, sizeof(g));
-  g.table = reinterpret_cast<const bf16*>(b->table);
-  g.num_vertices = b->num_vertices;
-  g.k_pad = p->k_pad;
-  g.vids = b->vids;
-  g.vid_dtype = b->vid_dtype;
-  g.bary = b->bary;
-  g.ray_idx = b->ray_idx;
-  g.idx_dtype = b->idx_dtype;
-  g.idx_offset = b->idx_offset;
-  g.num_rays = b->num_rays;
-  g.num_src = b->num_source_rays;
-  g.ctrl = p->ctrl;
-  g.offset_from_ctrl = b->offset_from_ctrl;
-  g.batch = b->batch;
-  g.rows = Bp;
-  g.gather_nt = (size_t)b->num_vertices * (size_t)p->k_pad * 2 > C3_NT_TABLE_BYTES;
-  g.X = p->W<bf16>(p->o_x0);
-  g.XT = p->W<bf16>(p->o_x0t);
-  if ((rc = launch_xgather(g, st))) return rc;
-  auto img = [&](const ParamSeg* w, bool fwd) -> const bf16* {
-    const int64_t off = fwd ? w->f_off : w->ft_off;
-    return off >= 0 ? reinterpret_cast<const bf16*>(p->shadow + off) : nullptr;
-  };
-  auto base = [&]() {
-    LayerArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.rows = Bp;
-    a.H = H;
-    return a;
-  };
-  // forward: layer 0 over X, hidden layers over Y_{l-1} (the skip layer also over X), the
-  // last hidden layer with the head, loss and head backward fused
-  for (int l = 0; l <= L - 2; ++l) {
-    LayerArgs a = base();
-    a.mode = l == L - 2 ? LY_MODE_HEAD : LY_MODE_FWD;
-    a.nsrc = 1;
-    a.in[0] = l == 0 ? g.X : p->W<bf16>(p->o_y[l - 1]);
-    a.kin[0] = l == 0 ? p->k_pad : H;
-    a.w[0] = img(p->weight_seg(l, 0), true);
-    a.bias0 = p->params + p->bias_seg(l, 0)->off;
-    if (l == s && l > 0) {
-      a.nsrc = 2;
-      a.in[1] = g.X;
-      a.kin[1] = p->k_pad;
-      a.w[1] = img(p->weight_seg(s, 1), true);
-      a.bias1 = p->params + p->bias_seg(s, 1)->off;
-    }
-    INF_CHECK_ARG(a.w[0] != nullptr && (a.nsrc == 1 || a.w[1] != nullptr), "layered step: fragment image missing");
-    if (a.mode == LY_MODE_FWD) {
-      a.out = p->W<bf16>(p->o_y[l]);
-      a.outT = p->W<bf16>(p->o_yt[l]);
-    } else {
-      a.out = p->W<bf16>(p->o_dZ[L - 2]);
-      a.outT = p->W<bf16>(p->o_dZT[L - 2]);
-      a.colsum = p->W<float>(p->o_colsum[L - 2]);
-      a.W7 = p->params + p->weight_seg(L - 1, 0)->off;
-      a.b7 = p->params + p->bias_seg(L - 1, 0)->off;
-      a.hw_part = p->W<float>(p->o_hw);
-      a.hb_part = p->W<float>(p->o_hb);
-      a.loss_part = p->W<double>(p->o_loss);
-      a.pred = pred;
-      INF_CHECK_ARG(b->rgb != nullptr, "training batch without target colours");
-      a.rgb = b->rgb;
-      a.ray_idx = b->ray_idx;
-      a.idx_dtype = b->idx_dtype;
-      a.idx_offset = b->idx_offset;
-      a.num_rays = b->num_rays;
-      a.num_src = b->num_source_rays;
-      a.offset_from_ctrl = b->offset_from_ctrl;
-      a.batch = b->batch;
-      a.loss = b->loss >= 0 ? b->loss : p->d.loss;
-      INF_CHECK_ARG(a.loss >= INF_LOSS_L2 && a.loss <= INF_LOSS_CAUCHY, "loss type");
-      const int64_t cnt = b->loss_count > 0 ? b->loss_count : (int64_t)3 * b->batch;
-      a.inv_count = (float)(1.0 / (double)cnt);
-      a.ctrl = p->ctrl;
-      a.count_step = 1;
-    }
-    if ((rc = launch_layer(a, st))) return rc;
-  }
-  // dX: dZ_{l-1} = (W_l^T dZ_l) * (Y_{l-1} > 0), l = L-2 .. 1 (the skip layer through Lx)
-  for (int l = L - 2; l >= 1; --l) {
-    LayerArgs a = base();
-    a.mode = LY_MODE_BWD;
-    a.nsrc = 1;
-    a.in[0] = p->W<bf16>(p->o_dZ[l]);
-    a.kin[0] = H;
-    a.w[0] = img(p->weight_seg(l, 0), false);
-    INF_CHECK_ARG(a.w[0] != nullptr, "layered step: transposed fragment image missing");
-    a.mask_in = p->W<bf16>(p->o_y[l - 1]);
-    a.out = p->W<bf16>(p->o_dZ[l - 1]);
-    a.outT = p->W<bf16>(p->o_dZT[l - 1]);
-    a.colsum = p->W<float>(p->o_colsum[l - 1]);
-    if ((rc = launch_layer(a, st))) return rc;
-  }
-  return INF_OK;
-}
-
 bool use_chain3x3(const inf_plan* p, const inf_batch* b, int Bp) {
   if (p->mode != INF_MODE_BF16X3 || p->k_pad > C3_KC || chain3_wide(Bp) ||
       !chain3_supported(p->H, p->L, p->k_pad, Bp) || !chain3_x3_lds_fits(p->H, p->L, p->k_pad))
@@ -1684,8 +1499,8 @@ int inf_plan_param_layout(const inf_plan* p, int64_t* offsets, int64_t* numels, 
   return INF_OK;
 }
 
-// The item subsets the fused dW + update reads (lgemm.hip): the vector and end-of-step
-// items its leading blocks run, and the matrix items.  Copies of p->adam_items: re-uploaded
+// The item subset the fused dW + update reads (lgemm.hip): the vector and end-of-step
+// items its leading blocks run.  A copy of p->adam_items: re-uploaded
 // whenever those change (bind, and inf_plan_shard's staging offsets goff / woff, which the
 // fused update's SHARD_GRAD_OUT items write through).
 static int upload_item_subsets(inf_plan* p) {
@@ -1694,12 +1509,6 @@ static int upload_item_subsets(inf_plan* p) {
     if (it.seg < 0 || !p->adam_segs[it.seg].matrix) aux.push_back(it);
   p->n_aux_items = (int)aux.size();
   INF_HIP_TRY(hipMemcpy(p->ws + p->o_aux_items, aux.data(), aux.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
-  std::vector<AdamItem> mat;
-  for (const auto& it : p->adam_items)
-    if (it.seg >= 0 && p->adam_segs[it.seg].matrix) mat.push_back(it);
-  p->n_mat_items = (int)mat.size();
-  if (!mat.empty())
-    INF_HIP_TRY(hipMemcpy(p->ws + p->o_mat_items, mat.data(), mat.size() * sizeof(AdamItem), hipMemcpyHostToDevice));
   return INF_OK;
 }
 
@@ -1910,7 +1719,6 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     return launch_update(a, p->mode, st);
   }
   // the update launch's arguments for a step whose gradient partials are complete
-  p->last_aux_dw = false;
   auto step_update = [&](int Bp_, int nloss_) {
     AdamArgs a = update_args(p, Bp_);
     a.grad_src = GRAD_SLABS;
@@ -1930,17 +1738,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
     return a;
   };
-  if (!bucketed && !shard && xslot < 0 && use_big(p, batch, Bp3)) {
-    // large batch as layer GEMMs (layer.hip) -> the 64-ray tiles' dW GEMM (-> update below)
-    const int Bp = Bp3;
-    if ((rc = run_big(p, batch, Bp, pred, st))) return rc;
-    if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
-    p->saved = false;
-    p->saved_batch = batch->batch;
-    p->saved_bp = Bp;
-    ck = CHAIN_BIG;
-    nloss = Bp / LY_RAYS;
-  } else if (use_chain3(p, batch, Bp3)) {
+  if (use_chain3(p, batch, Bp3)) {
     // fused gather + chain -> dW GEMM (-> update below).  INF_FUSED_UPDATE=1: the update
     // runs inside the dW launch instead (each tile's last split-K block applies Adam to
     // it, the first blocks do the biases and the end-of-step sums; bitwise the same) --
@@ -1956,7 +1754,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     p->saved_batch = batch->batch;
     p->saved_bp = Bp;
     ck = 3;
-    nloss = Bp / step_bm(p, Bp);
+    nloss = Bp / chain3_bm(Bp);
     p->stepped = true;
     p->last_lgf = false;
     if (!bucketed && (p->lgf || fused_update_requested(p))) {
@@ -1978,28 +1776,6 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
       a.segs = p->W<AdamSeg>(p->o_tables_b);
       a.num_items = p->n_items_b1;
       return launch_update(a, p->mode, st);
-    }
-    // INF_AUX_DW=1: the vector / end-of-step items in the dW launch's leading blocks (on the
-    // CUs its 224 blocks leave idle at 4096 rays), the matrix items alone in the update
-    // launch -- bitwise the same step (test_aux_dw_bitwise), measured neutral: the update
-    // 10.1 -> 9.8 us, the dW launch 14.5 -> 14.9 us under rocprof, steps 64.4-64.6 vs
-    // 64.7-64.9 us (profiles/r04/aux_dw/), so opt-in
-    const char* aux_env = std::getenv("INF_AUX_DW");
-    const bool aux_dw = (aux_env != nullptr ? std::atoi(aux_env) != 0 : false) && apply_adam && !shard &&
-                        p->mode == INF_MODE_BF16 && p->n_mat_items > 0 && !use_fgemm(p, Bp, p->dw_splits);
-    p->last_aux_dw = aux_dw;
-    if (aux_dw) {
-      ck = 3;
-      p->last_chain = 3;
-      if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
-      const AdamArgs a = step_update(Bp, nloss);
-      if ((rc = run_weight_grads(p, Bp, st, 3, nullptr, 0, &a))) return rc;
-      AdamArgs m = a;
-      m.items = p->W<AdamItem>(p->o_mat_items);
-      m.num_items = p->n_mat_items;
-      if ((rc = launch_update(m, p->mode, st))) return rc;
-      note_shadow_write(p, m, st);
-      return INF_OK;
     }
     if ((rc = run_weight_grads(p, Bp, st, 3))) return rc;
   } else if (use_chain3x3(p, batch, Bp3)) {
@@ -2068,6 +1844,10 @@ int inf_adam_ex(inf_plan* p, int step, double lr, int flags, inf_stream_t stream
   a.write_shadow = 1;
   a.step_host = step;
   a.lr_host = lr;
+  if (step > 0) {  // torch's 1 - beta ** step (Python double pow), as inf_adam_dense
+    a.bc1_host = 1.0 - std::pow(p->beta1, (double)step);
+    a.bc2_host = 1.0 - std::pow(p->beta2, (double)step);
+  }
   a.advance = (flags & INF_STEP_ADVANCE) ? 1 : 0;
   // after a fused chain3 step (the data-parallel tail) only the fragment images
   a.write_shadow = step_shadow_mode(p, p->last_chain);
@@ -2375,7 +2155,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
           }
         break;
       }
-      rc = run_weight_grads(p, Bp, st, p->last_chain == CHAIN_BIG ? 3 : p->last_chain);
+      rc = run_weight_grads(p, Bp, st, p->last_chain);
       for (const auto& g : p->segs)
         if (g.gemm) {
           f += 2.0 * g.R * g.C * B;
@@ -2385,7 +2165,7 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
     }
     case INF_STAGE_CHAIN: {
       INF_CHECK_ARG(b != nullptr && b->rgb != nullptr &&
-                        (use_chain(p) || p->last_chain == CHAIN_F32 || p->last_chain == CHAIN_X3 || p->last_chain == CHAIN_BIG),
+                        (use_chain(p) || p->last_chain == CHAIN_F32 || p->last_chain == CHAIN_X3),
                     "chain stage needs a fused training batch");
       // replay on the saved inputs; the step counter it advances is restored by the caller
       const double Lh = p->L;
@@ -2403,16 +2183,12 @@ int inf_run_stage(inf_plan* p, const inf_batch* b, int stage, int layer, double*
         // hi / lo bf16 weight images streamed per workgroup; fp32 rows in; hi / lo images out
         by = (double)(Bp / 16) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * 4.0 +
              B * (3.0 * p->k_pad * 4.0 + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * 4.0;
-      } else if (p->last_chain == CHAIN_BIG) {
-        rc = run_big(p, b, Bp, nullptr, st);
-        f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
-        by = B * (3.0 * p->k_pad * e + 24.0) + B * (2.0 * p->k_pad + 4.0 * (2.0 * Lh - 3) * H) * e;
       } else if (p->last_chain == 3) {
         rc = run_chain3(p, b, Bp, nullptr, st);
         f = 2.0 * B * (2.0 * k * H + (Lh - 2) * H * H + 3 * H) + 2.0 * B * ((Lh - 2) * H * H + 3 * H);
         // every workgroup streams W_0, W_y and the hidden weights twice over (L2 -> CU);
         // three table rows per ray in; X^T, Y^T, dZ^T out
-        by = (double)(Bp / step_bm(p, Bp)) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * e +
+        by = (double)(Bp / chain3_bm(Bp)) * (2.0 * p->k_pad * H + 2.0 * (Lh - 2) * H * H) * e +
              B * (3.0 * p->k_pad * e + 24.0) + B * (p->k_pad + (2.0 * Lh - 3) * H) * e;
       } else {
         rc = run_chain(p, b, Bp, true, nullptr, nullptr, nullptr, nullptr, st);
@@ -2533,7 +2309,6 @@ int inf_debug_buffer(inf_plan* p, int which, void* dst, int64_t* bytes, inf_stre
 
 int inf_plan_last_step_path(const inf_plan* p) {
   if (p == nullptr || !p->stepped) return -1;
-  if (p->last_chain == 3 && p->last_chain4) return 9;
   if (p->last_chain == 3 && p->last_zg) return 10;
   if (p->last_chain == 3 && chain3_wide(p->saved_bp)) return 5;
   return p->last_chain == 3 && p->k_pad > C3_KC ? 4 : p->last_chain;

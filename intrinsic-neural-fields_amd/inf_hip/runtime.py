@@ -515,11 +515,11 @@ class Plan:
 
     def last_step_path(self) -> str:
         """Kernel path of the last train_step: 'layered', 'chain', 'chain3', 'chain3_chunked',
-        'chain3_wide' (64-ray tiles), 'chain4' (128-ray workgroups, large batches of the
-        8 x 256 field), 'chain3_zg' (chain3 after the gather + input-layer GEMM launch, INF_ZG=1), 'chain_f32' (the fp32 mode's fused chain), 'chain3_x3' (the
-        bf16x3 mode's split-bf16 chain), 'layer_big' (the large-batch layer GEMMs, INF_BIG_LAYERED=1)."""
+        'chain3_wide' (64-ray tiles), 'chain3_zg' (chain3 after the gather + input-layer GEMM
+        launch, zg.hip: the default for k_pad > 1024), 'chain_f32' (the fp32 mode's fused
+        chain), 'chain3_x3' (the bf16x3 mode's split-bf16 chain)."""
         return {-1: None, 0: "layered", 2: "chain", 3: "chain3", 4: "chain3_chunked", 5: "chain3_wide", 6: "chain_f32",
-                7: "chain3_x3", 8: "layer_big", 9: "chain4", 10: "chain3_zg"}[
+                7: "chain3_x3", 10: "chain3_zg"}[
             int(lib.inf_plan_last_step_path(self.handle))]
 
     def weight_generation(self) -> int:

@@ -137,12 +137,16 @@ class _FusedEpoch:
                 b = self._batch
                 self.pipe.run(full % self.GRAPH_STEPS,
                               lambda xs: plan.train_step(b, None, apply_adam=True, advance=True, xslot=xs))
+                done = full
             else:
-                for n in graph_replays(full):
+                # the captured sizes only (a pipelined capture holds GRAPH_STEPS alone); the
+                # batches they do not cover run as eager steps below
+                done = 0
+                for n in graph_replays(full, tuple(sorted(graphs, reverse=True))):
                     graphs[n].replay()
-            optim.after_fused_steps(model, rt, group, full)
-            done = full
-            total = full * B
+                    done += n
+            optim.after_fused_steps(model, rt, group, done)
+            total = done * B
         # next() on the loader itself: a second iter() (as `for batch in it` would call)
         # reshuffles, and the reference draws ONE permutation per epoch (trainer.py:248)
         for i in range(nb):

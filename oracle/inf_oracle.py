@@ -201,25 +201,27 @@ def gather_bf16(E: np.ndarray, vids: np.ndarray, bary: np.ndarray) -> np.ndarray
     return bf16_round(x)
 
 
-def mlp_forward_bf16(w: dict, x_bf: np.ndarray, num_layers: int, skip: int):
+def mlp_forward_bf16(w: dict, x_bf: np.ndarray, num_layers: int, skip: int, mm=np.matmul, colsum=None):
     """The bf16 perf mode's arithmetic (chain3.hip epilogues): bf16 weights of the hidden
     / input layers, fp32 accumulation, bias added last, ReLU output rounded to bf16 once;
-    the sigmoid head on the bf16 activations with fp32 weights.  x_bf: gather_bf16 rows."""
+    the sigmoid head on the bf16 activations with fp32 weights.  x_bf: gather_bf16 rows.
+    mm: the fp32 matrix product (another summation order of the same arithmetic for the
+    derived test bars, tests/golden/make_bf16_spread.py); colsum: unused here."""
     wb = {n: bf16_round(v) for n, v in w.items() if n.endswith("weight")}
     cache = {"x": x_bf, "in": [], "out": []}
     h = x_bf
     for i in range(num_layers - 1):
         cache["in"].append(h)
         if i == skip:
-            z = (h @ wb[f"layers.{i}.Lx.weight"].T + x_bf @ wb[f"layers.{i}.Ly.weight"].T) + \
+            z = (mm(h, wb[f"layers.{i}.Lx.weight"].T) + mm(x_bf, wb[f"layers.{i}.Ly.weight"].T)) + \
                 w[f"layers.{i}.Lx.bias"] + w[f"layers.{i}.Ly.bias"]
         else:
-            z = h @ wb[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
+            z = mm(h, wb[f"layers.{i}.0.weight"].T) + w[f"layers.{i}.0.bias"]
         h = bf16_round(np.maximum(z.astype(np.float32), 0))
         cache["out"].append(h)
     i = num_layers - 1
     cache["in"].append(h)
-    z = h @ w[f"layers.{i}.0.weight"].T + w[f"layers.{i}.0.bias"]
+    z = mm(h, w[f"layers.{i}.0.weight"].T) + w[f"layers.{i}.0.bias"]
     p = _sigmoid(z.astype(np.float32)).astype(np.float32)
     cache["out"].append(p)
     cache["wb"] = wb
@@ -257,36 +259,41 @@ def mlp_forward_bf16_projected(w: dict, E: np.ndarray, vids: np.ndarray, bary: n
     return _sigmoid(z.astype(np.float32)).astype(np.float32)
 
 
-def mlp_backward_bf16(w: dict, cache: dict, dpred: np.ndarray, num_layers: int, skip: int) -> dict:
+def mlp_backward_bf16(w: dict, cache: dict, dpred: np.ndarray, num_layers: int, skip: int, mm=np.matmul,
+                      colsum=None) -> dict:
     """Reverse mode in the bf16 perf mode's arithmetic: dZ of every hidden layer rounded to
     bf16 once (the MFMA operand of the dX chain and of the dW GEMM), bias gradients from the
-    fp32 dZ before rounding, the head and its backward in fp32 (chain3.hip, lgemm.hip)."""
+    fp32 dZ before rounding, the head and its backward in fp32 (chain3.hip, lgemm.hip).
+    mm / colsum: the fp32 matrix product and column sum (another summation order: see
+    mlp_forward_bf16)."""
+    if colsum is None:
+        colsum = lambda a: a.sum(0)  # noqa: E731
     g = {}
     wb = cache["wb"]
     out, L = cache["out"], num_layers
     p = out[-1]
     dz = (dpred * (1 - p) * p).astype(np.float32)
     h = cache["in"][L - 1]
-    g[f"layers.{L - 1}.0.weight"] = dz.T @ h
-    g[f"layers.{L - 1}.0.bias"] = dz.sum(0)
-    v = (dz @ w[f"layers.{L - 1}.0.weight"]) * (h > 0)
+    g[f"layers.{L - 1}.0.weight"] = mm(dz.T, h)
+    g[f"layers.{L - 1}.0.bias"] = colsum(dz)
+    v = mm(dz, w[f"layers.{L - 1}.0.weight"]) * (h > 0)
     for i in range(L - 2, -1, -1):
         hin = cache["in"][i]
         v = v.astype(np.float32)
         dzb = bf16_round(v)
         if i == skip:
-            g[f"layers.{i}.Lx.weight"] = dzb.T @ hin
-            g[f"layers.{i}.Lx.bias"] = v.sum(0)
-            g[f"layers.{i}.Ly.weight"] = dzb.T @ cache["x"]
-            g[f"layers.{i}.Ly.bias"] = v.sum(0)
+            g[f"layers.{i}.Lx.weight"] = mm(dzb.T, hin)
+            g[f"layers.{i}.Lx.bias"] = colsum(v)
+            g[f"layers.{i}.Ly.weight"] = mm(dzb.T, cache["x"])
+            g[f"layers.{i}.Ly.bias"] = colsum(v)
             wmat = wb[f"layers.{i}.Lx.weight"]
         else:
-            g[f"layers.{i}.0.weight"] = dzb.T @ hin
-            g[f"layers.{i}.0.bias"] = v.sum(0)
+            g[f"layers.{i}.0.weight"] = mm(dzb.T, hin)
+            g[f"layers.{i}.0.bias"] = colsum(v)
             wmat = wb[f"layers.{i}.0.weight"]
         if i == 0:
             break
-        v = (dzb @ wmat) * (cache["out"][i - 1] > 0)
+        v = mm(dzb, wmat) * (cache["out"][i - 1] > 0)
     return g
 
 

@@ -364,18 +364,21 @@ def test_bucketed_step_bitwise_unbucketed(monkeypatch, graph):
     assert a[3:] == bb[3:] and a[5] == 3
 
 
-# fp32: 1024 input columns and 8 layers give Adam many elements whose gradient is at rounding
-# level, where the two half-batch summation orders move them differently (seen: 5.9e-6
-# relative on layers.0.0.weight after 10 steps, max 8.8e-6 = 0.09 lr)
-@pytest.mark.parametrize("mode,w_rel,loss_rtol", [("bf16", 5e-2, 2e-3), ("fp32", 1e-4, 1e-5)])
-def test_config_c_data_parallel_two_ranks_gloo(tmp_path, mode, w_rel, loss_rtol):
+@pytest.mark.parametrize("mode", ["bf16", "fp32"])
+def test_config_c_data_parallel_two_ranks_gloo(tmp_path, mode):
     """Config C -- the human k=1024, 8 x 256 (skip 4), L2, lr 1e-4, batch 4096 MLP of
     configs/texture_reconstruction/intrinsic_human_k1024_8x256.yaml -- through
     `torchrun --nproc-per-node 2 train.py <cfg> --data_parallel` (two ranks on the one GPU
     over gloo, 2048 rays per rank per step) against the single-process run of the same
     YAML on a synthetic dataset in the reference's layout (a torus, 1024 eigenfunction
-    columns): same files, logged scalars up to the two half-batch gradients' summation
-    order, weights close (bounds as test_train_data_parallel_two_ranks_one_gpu_gloo)."""
+    columns): same files and logged tags.  The world-2 run differs from the single one only
+    in the summation order of the two half-batch gradients, so its distance is held to a bar
+    DERIVED from a pure summation-order change (as
+    test_train_data_parallel_two_ranks_within_summation_order_spread): a second
+    single-process run that sums in another order (bf16: INF_LGEMM_KS=1, one k group per dW
+    block instead of two; fp32: INF_NO_CHAINF=1, the layered fp32 kernels instead of the
+    fused fp32 chain) measures the spread, and world 2
+    must stay within 10 x it per weight tensor (relative L2) and over the logged scalars."""
     import synthetic_views as S
     S.build(str(tmp_path), H=128, W=128, kmax=1024, views=(4, 1, 1))
     with open(os.path.join(ROOT, "configs", "texture_reconstruction", "intrinsic_human_k1024_8x256.yaml")) as fh:
@@ -387,36 +390,50 @@ def test_config_c_data_parallel_two_ranks_gloo(tmp_path, mode, w_rel, loss_rtol)
     assert (cfg["model"]["k"], cfg["model"]["num_layers"], cfg["model"]["mlp_hidden_dim"],
             cfg["model"]["skip_layer_idx"], cfg["training"]["batch_size"]) == (1024, 8, 256, 4, 4096)
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", INF_DP_BACKEND="gloo")
+    for key in ("INF_NO_CHAINF", "INF_LGEMM_KS"):
+        env.pop(key, None)
+    # (fp32: the split count does not change this batch's fused fp32 dW order -- INF_DW_SPLITS=8
+    # measured a spread of exactly 0 -- so the reordered run takes the layered fp32 kernels)
+    knob = {"INF_NO_CHAINF": "1"} if mode == "fp32" else {"INF_LGEMM_KS": "1"}
     results = {}
-    for tag in ("single", "dp2"):
+    for tag in ("single", "reordered", "dp2"):
         cfg["training"]["out_dir"] = f"out/{tag}"
         path = tmp_path / f"{tag}.yaml"
         with open(path, "w") as fh:
             yaml.safe_dump(cfg, fh)
-        if tag == "single":
+        if tag != "dp2":
             cmd = [sys.executable, os.path.join(PKG, "train.py"), str(path)]
         else:
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                    "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(PKG, "train.py"),
                    str(path), "--data_parallel"]
-        r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        r = subprocess.run(cmd, cwd=tmp_path, env=dict(env, **knob) if tag == "reordered" else env,
+                           capture_output=True, text=True, timeout=300)
         print(tag, r.stdout[-2000:], r.stderr[-3000:])
         assert r.returncode == 0, tag
         out = tmp_path / "out" / tag
         sd = torch.load(out / "model_last_epoch.pt", map_location="cpu", weights_only=True)
         rows = [json.loads(x) for x in open(out / "logs" / "scalars.jsonl")]
         results[tag] = (sorted(os.listdir(out)), sd, rows)
-    (fs, ws, rs), (fd, wd, rd) = results["single"], results["dp2"]
-    assert fs == fd
+    (fs, ws, rs), (fo, wo, ro), (fd, wd, rd) = results["single"], results["reordered"], results["dp2"]
+    assert fs == fd == fo
     assert ws["layers.4.Ly.weight"].shape == (256, 1024)
-    lr = float(cfg["training"]["lr"])
-    bad = []
-    for key in ws:
-        a, b = ws[key].float().numpy().reshape(-1), wd[key].float().numpy().reshape(-1)
-        rel = float(np.linalg.norm(a - b) / max(np.linalg.norm(a), 1e-12))
-        print(key, "max", float(np.abs(a - b).max()), "rel", rel)
-        if not (np.abs(a - b).max() <= 2 * lr * 200 and rel <= w_rel):
-            bad.append((key, rel))
+    assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd] == \
+        [(r["tag"], r["step"]) for r in ro]
+
+    def rel(a, b):
+        a, b = a.float().numpy().reshape(-1), b.float().numpy().reshape(-1)
+        return float(np.linalg.norm(a - b) / max(np.linalg.norm(a), 1e-12))
+
+    spread = {key: rel(ws[key], wo[key]) for key in ws}
+    got = {key: rel(ws[key], wd[key]) for key in ws}
+    print(mode, "weights rel: world 2", {k: f"{v:.2e}" for k, v in got.items()})
+    print(mode, "weights rel: summation-order spread", {k: f"{v:.2e}" for k, v in spread.items()})
+    assert max(spread.values()) > 0  # the reordered run did sum differently
+    bad = [(key, got[key], spread[key]) for key in ws if got[key] > 10 * spread[key] + 1e-7]
     assert not bad, bad
-    assert [(r["tag"], r["step"]) for r in rs] == [(r["tag"], r["step"]) for r in rd]
-    np.testing.assert_allclose([r["value"] for r in rs], [r["value"] for r in rd], rtol=loss_rtol)
+    vs, vo, vd = (np.array([r["value"] for r in x]) for x in (rs, ro, rd))
+    s_spread = float((np.abs(vs - vo) / np.maximum(np.abs(vs), 1e-12)).max())
+    s_got = float((np.abs(vs - vd) / np.maximum(np.abs(vs), 1e-12)).max())
+    print(mode, "scalars rel: world 2", s_got, "spread", s_spread)
+    assert s_got <= 10 * s_spread + 1e-7, (s_got, s_spread)

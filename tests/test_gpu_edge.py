@@ -255,7 +255,7 @@ def test_out_of_range_permutation_values_read_as_zero_rows(monkeypatch):
         loss = plan.read_ctrl()["loss_sum"]
         assert abs(loss - loss_ref) < (1e-5 if mode == "fp32" else 2e-2) * max(1.0, loss_ref), (mode, B, loss, loss_ref)
         if mode == "bf16" and B > 8192:
-            assert plan.last_step_path() in (("chain",) if env else ("chain3_wide", "chain4")), plan.last_step_path()
+            assert plan.last_step_path() in (("chain",) if env else ("chain3_wide",)), plan.last_step_path()
     monkeypatch.delenv("INF_NO_CHAIN3", raising=False)
     # the projected-table render (bf16)
     import model as M

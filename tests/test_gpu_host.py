@@ -285,7 +285,10 @@ def test_trainer_g12_curve_config_b(tmp_path):
     # would also move the mean of the last four epochs (0.2 dB bar; the variants: <= 0.16).
     for mode, floor in (("fp32", 0.005), ("bf16", 0.02)):
         c = curves[mode]
-        bar = np.maximum(g12_reference_envelope(bf16=mode == "bf16"), floor)
+        # the derived envelope, floored, and capped at the round-4 bar of 0.5 dB per epoch
+        # (the 1.5 x running max pooled over the fp32 and bf16 variants reaches
+        # ~0.82 dB late; the cap keeps each default summation order passing on its own)
+        bar = np.minimum(np.maximum(g12_reference_envelope(bf16=mode == "bf16"), floor), 0.5)
         err = np.abs(c - ref)
         print(mode, "bar", np.round(bar, 3).tolist())
         assert (err <= bar).all(), (mode, np.round(err, 3).tolist())

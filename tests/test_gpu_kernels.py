@@ -397,105 +397,6 @@ def test_chain3_wide_tiles_match_narrow(name, B, monkeypatch):
         assert np.abs(gw[n] - gl[n]).max() / scale < 1e-5, n
 
 
-@pytest.mark.parametrize("B,loss,bad", [(16384, "L2", False), (10240, "L1", True), (65536, "L2", False),
-                                        (9000, "cauchy", False)])
-def test_chain4_matches_chain3_wide(B, loss, bad, monkeypatch):
-    """chain4.hip (128-ray workgroups of eight waves, the default above 8192 rays for the
-    8 x 256 field) against chain3's 64-ray tiles (INF_CHAIN4=0) on one batch: the same
-    feature tile, the same MFMA k order for W_0 x and W_y x (two fp32 sums added in the skip
-    epilogue), the same epilogue arithmetic -- so the forward activations and the X^T / Y^T /
-    dZ^T images they give the dW GEMM are bitwise equal, and only the head's dot products and
-    the per-workgroup partials are summed in another fp32 order: RGB within 1e-6, the loss
-    sums within 1e-6 relative; dL/dz's last bits then flip a bf16 rounding of dZ now and then,
-    so gradients within 1e-3 of each tensor's max (seen 2.5e-4 on layers.0).  `bad`:
-    out-of-range vertex ids and ray-index values read as zero rows / zero targets on both;
-    9000 rays: a ragged batch (padded to 9088, 71 workgroups, the last one partly empty)."""
-    rng = np.random.default_rng(44)
-    k, H, L, s = CFG["B"]
-    V = 3000
-    E = rng.standard_normal((V, k)).astype(np.float32)
-    E /= (E.max(0) - E.min(0))
-    vids = rng.integers(0, V, (B, 3))
-    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
-    rgb = rng.random((B, 3)).astype(np.float32)
-    perm = torch.randperm(B)
-    if bad:
-        vids[::97, 1] = V + 5
-        perm[::131] = B + 7
-    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
-                         torch.from_numpy(rgb).cuda(), validate=not bad)
-    out = {}
-    for tag in ("chain4", "chain3_wide"):
-        monkeypatch.setenv("INF_CHAIN4", "1" if tag == "chain4" else "0")
-        plan, params, w = make_plan("B", mode="bf16", loss=loss, max_batch=B, adam=True)
-        pred = torch.empty((B, 3), device="cuda")
-        b = plan.make_batch(source=src, batch=B, ray_idx=perm.cuda())
-        plan.train_step(b, pred, apply_adam=False)
-        c = plan.read_ctrl()
-        assert plan.last_step_path() == tag, plan.last_step_path()
-        assert c["step"] == 1
-        xt = plan.debug_buffer(0).cpu().numpy()
-        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"], c["sse_sum"], xt)
-        del plan
-        torch.cuda.empty_cache()
-    p4, g4, l4, s4, x4 = out["chain4"]
-    p3, g3, l3, s3, x3 = out["chain3_wide"]
-    assert np.isfinite(p4).all()
-    assert np.array_equal(x4, x3)  # X^T images: the same gathered features
-    np.testing.assert_allclose(p4, p3, atol=1e-6)
-    assert abs(l4 - l3) <= 1e-6 * max(1.0, abs(l3)) and abs(s4 - s3) <= 1e-6 * max(1.0, abs(s3)), (l4, l3, s4, s3)
-    for n in O.layer_names(L, s):
-        scale = max(np.abs(g3[n]).max(), 1e-12)
-        err = float(np.abs(g4[n] - g3[n]).max() / scale)
-        assert err < 1e-3, (n, err)
-
-
-@pytest.mark.parametrize("name,B,bad", [("B", 4096, False), ("R", 4096, False), ("B", 2048, True)])
-def test_chain3_precomputed_input_layers(name, B, bad, monkeypatch):
-    """chain3's ZP schedule (INF_ZP=1, csrc/igemm.hip: gather X / X^T, then Z = [W_0; W_y] X^T
-    as a GEMM ahead of the chain; the chain streams the hidden layers only) against the
-    default in-kernel gather + input-layer stream on one batch.  Layer 0 runs the same MFMA k
-    order into one accumulator: bitwise.  The skip layer adds W_y x as a separate fp32 sum
-    (the chunked schedule's order), so a bf16 activation may round the other way: RGB 5e-4,
-    gradients 1e-2 of max, the chain-vs-layered bars.  `bad`: out-of-range vertex ids and
-    ray-index values read as zero rows / zero targets on both paths."""
-    rng = np.random.default_rng(8)
-    k, H, L, s = CFG[name]
-    V = 3000
-    E = rng.standard_normal((V, k)).astype(np.float32)
-    E /= (E.max(0) - E.min(0))
-    vids = rng.integers(0, V, (B, 3))
-    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
-    rgb = rng.random((B, 3)).astype(np.float32)
-    perm = torch.randperm(B)
-    if bad:
-        vids[::97, 1] = V + 5
-        perm[::131] = B + 7
-    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
-                         torch.from_numpy(rgb).cuda(), validate=not bad)
-    out = {}
-    for tag in ("zp", "nozp"):
-        if tag == "zp":
-            monkeypatch.setenv("INF_ZP", "1")
-        else:
-            monkeypatch.delenv("INF_ZP")
-        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
-        pred = torch.empty((B, 3), device="cuda")
-        plan.train_step(plan.make_batch(source=src, batch=B, ray_idx=perm.cuda()), pred, apply_adam=False)
-        c = plan.read_ctrl()
-        assert plan.last_step_path() == "chain3", plan.last_step_path()
-        out[tag] = (pred.cpu().numpy(), arena_to_dict(plan.grads, w, L, s), c["loss_sum"])
-    pz, gz, lz = out["zp"]
-    pn, gn, ln = out["nozp"]
-    assert np.isfinite(pz).all()
-    np.testing.assert_allclose(pz, pn, atol=5e-4)
-    assert abs(lz - ln) <= 1e-3 * max(1.0, abs(ln)), (lz, ln)
-    for n in O.layer_names(L, s):
-        scale = max(np.abs(gn[n]).max(), 1e-12)
-        err = np.abs(gz[n] - gn[n]).max() / scale
-        assert err < 1e-2, (n, err)
-
-
 @pytest.mark.parametrize("k,B,bad,V", [(1024, 4096, False, 3000), (1024, 2048, True, 3000), (4096, 4096, False, 20000),
                                         (4096, 1024, True, 5000)])
 def test_chain3_zg_input_layers(k, B, bad, V, monkeypatch):
@@ -505,11 +406,14 @@ def test_chain3_zg_input_layers(k, B, bad, V, monkeypatch):
     k = 4096: the chunked tile) on one batch of the 8 x 256 field.  The gather numerics are
     the same (b0 e0 + b1 e1 + b2 e2 in fp32, one bf16 rounding): X^T images bitwise.  Z is
     summed per k slice and the slices added, so a bf16 activation may round the other way:
-    RGB 5e-4, loss 1e-3 relative, gradients within the bf16-oracle bar of each path (two fp32
-    summation orders of the same bf16 arithmetic): 3e-2 of max, 6e-2 at k = 4096 (config D's
-    oracle bar, test_bf16_chunked_chain3_matches_bf16_oracle; seen 4.7e-2 on Ly.weight, whose
-    4096-ray reduction meets 4096 bf16 feature columns).  `bad`: out-of-range vertex ids and
-    ray-index values read as zero rows / zero targets."""
+    RGB 5e-4, loss 1e-3 relative, gradients within the sum of the two paths' bf16-oracle bars
+    (two fp32 summation orders of the same bf16 arithmetic, each held to the oracle): 2 x 3e-2
+    of max at k = 1024 (BF16_ORACLE_GRAD, from measured values), and at k = 4096 per tensor
+    2 x bf16_spread_bar -- each path within twice the largest distance at which other
+    summation orders of the oracle land from it on these inputs (tests/golden/
+    make_bf16_spread.py; Ly.weight, whose 4096-ray reduction meets 4096 bf16 feature columns,
+    spreads 1.8e-2 there).  `bad`: out-of-range vertex ids and ray-index values read as zero
+    rows / zero targets."""
     rng = np.random.default_rng(9)
     H, L, s = 256, 8, 4
     E = rng.standard_normal((V, k)).astype(np.float32)
@@ -547,10 +451,14 @@ def test_chain3_zg_input_layers(k, B, bad, V, monkeypatch):
     assert np.array_equal(xz, xn)  # X^T: the same gathered features
     np.testing.assert_allclose(pz, pn, atol=5e-4)
     assert abs(lz - ln) <= 1e-3 * max(1.0, abs(ln)), (lz, ln)
+    errs = {}
     for n in O.layer_names(L, s):
         scale = max(np.abs(gn[n]).max(), 1e-12)
-        err = np.abs(gz[n] - gn[n]).max() / scale
-        assert err < (2 if k > 1024 else 1) * BF16_ORACLE_GRAD, (n, err)
+        errs[n] = float(np.abs(gz[n] - gn[n]).max() / scale)
+    print(k, B, {n: round(e, 5) for n, e in errs.items()})
+    for n, err in errs.items():
+        bar = 2 * (bf16_spread_bar(f"zg_{B}", n) if k > 1024 else BF16_ORACLE_GRAD)
+        assert err < bar, (n, err, bar)
 
 
 def test_bf16_chain_render_matches_layered(monkeypatch):
@@ -616,41 +524,6 @@ def test_fused_update_bitwise(apply_adam, monkeypatch):
     for a_, b_ in zip(out["separate"][:4], out["fused"][:4]):
         assert np.array_equal(a_, b_)
     assert out["separate"][4] == out["fused"][4]
-
-
-@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
-def test_aux_dw_bitwise(name, B, monkeypatch):
-    """The update's vector / end-of-step items run by the dW GEMM's leading blocks
-    (INF_AUX_DW=1: lgemm.hip AUX, the matrix items alone in the update launch) leave exactly
-    the bytes of the default split: parameters, Adam state and the step's loss sums over
-    three steps (config R: k = 1023, element-wise arena rows)."""
-    monkeypatch.setenv("INF_LGF", "0")
-    rng = np.random.default_rng(31)
-    k, H, L, s = CFG[name]
-    V = 3000
-    E = rng.standard_normal((V, k)).astype(np.float32)
-    E /= (E.max(0) - E.min(0))
-    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (B, 3))).cuda(),
-                         torch.from_numpy(rng.dirichlet([1, 1, 1], B).astype(np.float32)).cuda(),
-                         torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
-    out = {}
-    for tag in ("0", "1"):
-        monkeypatch.setenv("INF_AUX_DW", tag)
-        plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
-        plan.set_lr(1e-3)
-        b = plan.make_batch(source=src, batch=B)
-        sums = []
-        for _ in range(3):
-            plan.train_step(b, None, apply_adam=True)
-            c = plan.read_ctrl()
-            sums.append((c["loss_sum"], c["sse_sum"], c["batch_index"]))
-        assert plan.last_step_path() == "chain3"
-        torch.cuda.synchronize()
-        out[tag] = (params.cpu().numpy().copy(), plan.exp_avg.cpu().numpy().copy(),
-                    plan.exp_avg_sq.cpu().numpy().copy(), sums)
-    for a_, b_ in zip(out["0"][:3], out["1"][:3]):
-        assert np.array_equal(a_, b_)
-    assert out["0"][3] == out["1"][3]
 
 
 @pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
@@ -775,20 +648,15 @@ def test_dp_step_shape_bitwise_equals_fused_step():
         assert f[5] == d[5]
 
 
-@pytest.mark.parametrize("name,B,big", [("B", 4096, False), ("B", 1024, False), ("A", 4096, False), ("R", 2048, False),
-                                        ("B", 65536, False), ("B", 65536, True), ("B", 16384, True)])
-def test_bf16_chain3_matches_bf16_oracle(name, B, big, monkeypatch):
+@pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("A", 4096), ("R", 2048), ("B", 65536), ("B", 16384)])
+def test_bf16_chain3_matches_bf16_oracle(name, B, monkeypatch):
     """The fused bf16 step (csrc/chain3.hip + lgemm.hip) against an independent restatement
     of the bf16 mode's arithmetic (oracle.inf_oracle.mlp_forward_bf16 / mlp_backward_bf16:
     bf16 weights and activations, fp32 accumulation, the rounding points of the chain's
     epilogues) -- not against the builder's own layered bf16 kernels.  What is left is the
     fp32 summation order, which can flip a bf16 rounding now and then.  65,536 rays is the
     bench's large-batch line: chain3's 64-ray tiles (the feature tile streamed in 256-column
-    chunks, W_y x a separate fp32 sum) and the 256 x 256-tile dW GEMM (fgemm.hip).  big: the
-    same batch on the layer GEMMs (layer.hip, INF_BIG_LAYERED=1): 128-ray workgroups, the skip
-    layer's two sources in one accumulator, the head fused into the last layer's epilogue."""
-    if big:
-        monkeypatch.setenv("INF_BIG_LAYERED", "1")
+    chunks, W_y x a separate fp32 sum) and the 256 x 256-tile dW GEMM (fgemm.hip)."""
     rng = np.random.default_rng(77)
     k, H, L, s = CFG[name]
     w0 = weights(golden(f"g2_forward_{name}.npz"))
@@ -803,11 +671,9 @@ def test_bf16_chain3_matches_bf16_oracle(name, B, big, monkeypatch):
     plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
     pred = torch.empty((B, 3), device="cuda")
     plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
-    want = ("layer_big",) if big else ("chain3_wide", "chain4") if B > 8192 else ("chain3",)
-    assert plan.last_step_path() in want, plan.last_step_path()
+    want = "chain3_wide" if B > 8192 else "chain3"
+    assert plan.last_step_path() == want, plan.last_step_path()
     c = plan.read_ctrl()
-    if big:
-        assert c["step"] == 1  # the head workgroup counts the step, as chain3's store wave does
     p = pred.cpu().numpy()
     g = arena_to_dict(plan.grads, w, L, s)
     p_ref, cache = O.mlp_forward_bf16(w0, O.gather_bf16(E, vids, bary), L, s)
@@ -827,6 +693,18 @@ def test_bf16_chain3_matches_bf16_oracle(name, B, big, monkeypatch):
 # against the fp32 oracle the same path needs 2e-2 / 0.25 (test_bf16_chain_matches_layered_and_oracle)
 BF16_ORACLE_RGB = 1e-3
 BF16_ORACLE_GRAD = 3e-2
+
+
+def bf16_spread_bar(case, n, factor=2.0, floor=1e-3):
+    """Bar for tensor n of a device path against the bf16 oracle at config D's shape:
+    `factor` x the largest distance from the oracle at which five other fp32 summation orders
+    of its arithmetic land on the same inputs (split 2 / 4, 32-deep blocks, reversed,
+    float64; tests/golden/make_bf16_spread.py -> bf16_spread_D.npz, case "D" or "zg_<rays>"),
+    relative to the tensor's max.  The device order is one more such order; the factor 2
+    covers the tail of a max over six samples instead of five.  The floor is the fp32 head's
+    rounding level (its spread is 1e-4)."""
+    d = golden("bf16_spread_D.npz")
+    return max(factor * float(d[f"{case}/vs_ref:{n}"]), floor)
 
 
 @pytest.mark.parametrize("zg", [False, True])
@@ -863,7 +741,8 @@ def test_bf16_chunked_chain3_matches_bf16_oracle(zg, monkeypatch):
     gerr = {n: float(np.abs(g[n] - g_ref[n]).max() / max(np.abs(g_ref[n]).max(), 1e-12)) for n in O.layer_names(L, s)}
     print("D", perr, {n: round(e, 5) for n, e in gerr.items()})
     assert perr < BF16_ORACLE_RGB, perr
-    # seen: RGB 1.8e-4; gradients <= 1.7e-2 of max except Ly.weight at 3.3e-2 (its 4096-ray
-    # reduction against 4096 bf16 feature columns: more rounding flips per max)
+    # per tensor: derived from the oracle's own summation-order spread on these inputs
+    # (bf16_spread_bar; e.g. Ly.weight, whose 4096-ray reduction meets 4096 bf16 feature
+    # columns, 4.9e-2, layers.4.Lx.weight 1.2e-2; seen 3.3e-2 and <= 1.7e-2 in round 5)
     for n, e in gerr.items():
-        assert e < 2 * BF16_ORACLE_GRAD, (n, e)
+        assert e < bf16_spread_bar("D", n), (n, e, bf16_spread_bar("D", n))

@@ -18,7 +18,7 @@ def short(name):
         return "chain3_kernel<chunked>"
     if name.startswith("Cijk_"):  # hipBLASLt's kernels (the projection GEMM)
         return "hipblaslt_gemm"
-    for key in ("zg_kernel", "chain4_kernel", "gather_rows_kernel", "proj_gemm_kernel", "fgemm_kernel", "igemm_kernel", "xgather_kernel", "chainf_kernel", "rprojw_kernel", "rproj_kernel", "rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
+    for key in ("zg_kernel", "gather_rows_kernel", "proj_gemm_kernel", "fgemm_kernel", "chainf_kernel", "rprojw_kernel", "rproj_kernel", "rchain_kernel", "chain3_kernel", "lgemm_kernel", "prefetch_advance_kernel", "chain_kernel", "gemm_nt_kernel", "gather_kernel", "update_kernel", "head_fwd_kernel",
                 "head_bwd_kernel", "pack_kernel", "ctrl_advance_kernel"):
         if key in name:
             tail = ""
