@@ -660,10 +660,21 @@ def render_bench(args, device):
         for st in streams[1:]:
             cur.wait_stream(st)
 
-    def timed(fn, reps=5):
-        fn()
-        torch.cuda.synchronize()
+    def timed(fn, reps=10):
+        # untimed frames for SETTLE_MS of GPU time first: each variant's inputs are built on the
+        # host while the GPU idles (~140 ms), and the frames right after an idle period time a
+        # clock transient (round 6 kernel trace of this leg: the pixel-coherent variant's rprojw
+        # launches ran 2247 -> 1875 us over its five timed frames, profiles/r06/render/)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        spent = 0.0
+        while True:
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            spent += e0.elapsed_time(e1)
+            if spent >= SETTLE_MS:
+                break
         e0.record()
         for _ in range(reps):
             fn()

@@ -34,14 +34,6 @@ namespace inf {
 namespace {
 
 using c3::pack_bf16x2;
-// Experiment (variant library only, -DPTAB_TILED_EXP): the table read in a k-tiled layout
-// [tiles_m][K / BK][BM][BK] -- every stage's 256 x 64 slice one contiguous 32 KB run instead
-// of 256 pieces of 128 B strided by the row pitch (tools/ptab_tiled_exp.py)
-#ifdef PTAB_TILED_EXP
-constexpr bool kTiledA = true;
-#else
-constexpr bool kTiledA = false;
-#endif
 using c3::u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -111,24 +103,17 @@ __global__ __launch_bounds__(512, 1) void proj_gemm_kernel(const bf16* __restric
   // outputs are never stored).
   const int KT = K / BK;
   const char* srcp[P::GLDS];
-  int64_t sstep[P::GLDS];  // bytes per stage
 #pragma unroll
   for (int i = 0; i < P::GLDS; ++i) {
     const int p = tid + P::THREADS * i;
     const int row = p / CPR;
-    sstep[i] = ROWB;
     if (row < BN) {
       srcp[i] = reinterpret_cast<const char*>(B + (int64_t)(n0 + row) * K) + (((p % CPR) ^ P::swz(row)) << 4);
     } else {
       const int lr = row - BN;
-      if constexpr (kTiledA) {
-        srcp[i] = reinterpret_cast<const char*>(A + ((int64_t)tm * KT * BM + lr) * BK) + (((p % CPR) ^ P::swz(lr)) << 4);
-        sstep[i] = (int64_t)BM * ROWB;
-      } else {
-        int64_t m = m0 + lr;
-        if (m >= M) m = M - 1;
-        srcp[i] = reinterpret_cast<const char*>(A + m * lda) + (((p % CPR) ^ P::swz(lr)) << 4);
-      }
+      int64_t m = m0 + lr;
+      if (m >= M) m = M - 1;
+      srcp[i] = reinterpret_cast<const char*>(A + m * lda) + (((p % CPR) ^ P::swz(lr)) << 4);
     }
   }
   auto issue = [&](int t) {
@@ -139,7 +124,7 @@ __global__ __launch_bounds__(512, 1) void proj_gemm_kernel(const bf16* __restric
       // (the source as its own variable: with the pointer arithmetic inside the builtin's
       // argument list hipcc's host pass drops this kernel template's stub -- an undefined
       // symbol at load time)
-      const char* src = srcp[i] + (int64_t)t * sstep[i];
+      const char* src = srcp[i] + (int64_t)t * ROWB;
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(st + (wave + 8 * i) * 1024), 16, 0, 0);
     }
   };
