@@ -241,13 +241,15 @@ class Trainer:
                     with torch.cuda.graph(g2, stream=s):
                         self.plan.adam(0, 0.0, advance=True)
             elif not self.prefetch:
-                # the production trainer's graph set (trainer.GRAPH_SIZES: 32, 8, 4, 2, 1 steps
-                # per replay launch; a launch boundary costs ~5-8 us of idle GPU): n steps replay
-                # as trainer.graph_replays(n) -- the driver's K = 20 from an epoch start is
-                # 8 + 8 + 4, exactly what trainer.py replays for an epoch of 20 batches
-                from trainer import GRAPH_SIZES
+                # the production trainer's graphs (trainer.epoch_graph_sizes: ONE graph of an
+                # epoch's nb batches; a replay boundary costs ~8 us of idle GPU), plus the
+                # trainer.GRAPH_SIZES pieces for partial runs (settle, warmup): n steps replay as
+                # trainer.graph_replays(n) -- a timed window of K steps from an epoch start of an
+                # nb = K epoch is one replay, exactly what trainer.py replays for an epoch of K
+                # batches
+                from trainer import GRAPH_SIZES, epoch_graph_sizes
                 self.gset = {}
-                for n in GRAPH_SIZES:
+                for n in sorted({x for x in GRAPH_SIZES if x <= self.nb} | set(epoch_graph_sizes(self.nb)), reverse=True):
                     if n <= self.nb:
                         g = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(g, stream=s):
@@ -499,7 +501,7 @@ def config_d_bench(args, device, B=4096, steps=40):
     from inf_hip import STAGE_CHAIN, STAGE_DW_GEMM, STAGE_GATHER, STAGE_UPDATE
     a = copy.copy(args)
     a.k, a.verts, a.no_graph = 4096, 500_000, False
-    tr = Trainer(a, device, B, 0, 1)
+    tr = Trainer(a, device, B, 0, 1, nb=epoch_batches(steps))
     tr.capture()
     ms, _ = time_steps(tr, steps, 8, 1)
     path = tr.plan.last_step_path()
@@ -562,7 +564,7 @@ def _secondary_train(args, device, B, steps, **over):
     for kk, v in over.items():
         setattr(a, kk, v)
     a.no_graph = False
-    tr = Trainer(a, device, B, 0, 1)
+    tr = Trainer(a, device, B, 0, 1, nb=epoch_batches(steps))
     tr.capture()
     ms, _ = time_steps(tr, steps, 4, 1)
     P = tr.plan.info.num_params
@@ -1013,6 +1015,12 @@ def cpu_baselines(args, device):
     return out
 
 
+def epoch_batches(steps):
+    """Batches per epoch of a single-GPU timed leg: the timed window of K steps is one epoch
+    of K batches (at least 8), replayed as trainer.py replays an epoch -- one graph."""
+    return max(8, int(steps))
+
+
 def summary_of(line):
     """Compact digest of the line's legs (times in us, rates in M/s or G/s), emitted as the
     line's last key."""
@@ -1121,7 +1129,7 @@ def main():
             del trs
             torch.cuda.empty_cache()
     else:
-        tr = Trainer(args, device, args.batch, rank, world)
+        tr = Trainer(args, device, args.batch, rank, world, nb=epoch_batches(args.steps))
         tr.capture()
         ms, wall_ms = time_steps(tr, args.steps, args.warmup, world, tag="headline")
     tr_ar_in_graph = tr.ar_in_graph

@@ -20,18 +20,19 @@
 namespace inf {
 namespace {
 
-template <typename T>
+// ST: the diagnostics build of the launch (AdamArgs::stamps set), per-item wall-clock stamps
+template <typename T, bool ST>
 __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   __shared__ float tile[ADAM_TILE_C][ADAM_TILE_R + 1];
   __shared__ adam_dev::Scalars sc;
-  unsigned long long* st = a.stamps != nullptr ? a.stamps + (int64_t)blockIdx.x * 8 : nullptr;
-  adam_dev::stamp(st, 0);
+  unsigned long long* st = ST ? a.stamps + (int64_t)blockIdx.x * 8 : nullptr;
+  if constexpr (ST) adam_dev::stamp(st, 0);
   // (every thread forming the step's scalars itself instead of thread 0 + an LDS barrier,
   // update_item LOCAL_SC, measured 8.5 vs 8.1 us per launch: the barrier is not on the
   // critical path -- the stamps (tools/update_items.py) put it in the data: ~1.5 us of loads
   // at ~12 TB/s from the MALL, then ~2 us of stores, profiles/r06/update/)
-  adam_dev::update_item<T>(a, a.items[blockIdx.x], tile, sc, st);
-  if (st != nullptr) {
+  adam_dev::update_item<T, 64, 8, false, false, false, ST>(a, a.items[blockIdx.x], tile, sc, st);
+  if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     adam_dev::stamp(st, 4);
   }
@@ -83,10 +84,18 @@ int launch_update(const AdamArgs& a, int mode, hipStream_t stream) {
   INF_CHECK_ARG(!a.do_adam || (a.exp_avg != nullptr && a.exp_avg_sq != nullptr), "update: Adam state not bound");
   INF_CHECK_ARG(!(a.write_grads || a.grad_src == GRAD_FLAT) || a.grads != nullptr, "update: grads not bound");
   INF_CHECK_ARG(!a.do_adam || a.step_host > 0 || a.ctrl != nullptr, "update: no step source");
-  if (mode == INF_MODE_BF16)
-    update_kernel<bf16><<<a.num_items, 256, 0, stream>>>(a);
-  else
-    update_kernel<float><<<a.num_items, 256, 0, stream>>>(a);
+  const bool st = a.stamps != nullptr;
+  if (mode == INF_MODE_BF16) {
+    if (st)
+      update_kernel<bf16, true><<<a.num_items, 256, 0, stream>>>(a);
+    else
+      update_kernel<bf16, false><<<a.num_items, 256, 0, stream>>>(a);
+  } else {
+    if (st)
+      update_kernel<float, true><<<a.num_items, 256, 0, stream>>>(a);
+    else
+      update_kernel<float, false><<<a.num_items, 256, 0, stream>>>(a);
+  }
   INF_LAUNCH_CHECK();
   return INF_OK;
 }

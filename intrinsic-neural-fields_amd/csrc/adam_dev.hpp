@@ -274,7 +274,9 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
 // side is accessed element-wise (slabs are always padded and aligned).
 // PB: split-K partials loaded per batch; SC1: read the partials write-through (`sc1`, the
 // in-launch hand-off of lgemm.hip: they were stored sc1 by other workgroups of the launch)
-template <typename T, bool VEC4, int PB, bool SC1>
+// ST: diagnostics stamps at st (compiled in only for the stamped launch: the asm wait would
+// otherwise constrain the schedule of the product kernel)
+template <typename T, bool VEC4, int PB, bool SC1, bool ST = false>
 __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
                                             const Scalars& sc, float (*tile)[ADAM_TILE_R + 1],
                                             unsigned long long* st = nullptr) {
@@ -373,12 +375,12 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
       }
     }
   }
-  if (st != nullptr) {
+  if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(st, 2);
   }
   mt_apply<T, VEC4>(a, seg, item, sc, tile, ok, e, w, m, v, g);
-  stamp(st, 3);
+  if constexpr (ST) stamp(st, 3);
 }
 
 // NI matrix items of one segment, software-pipelined: the next item's parameters, Adam
@@ -556,7 +558,8 @@ __device__ inline void finish_step(const AdamArgs& a) {
 // scalars itself, so no LDS hand-off and no barrier stand between the item's table loads and
 // its data loads (callers that run several items per workgroup keep the barrier, which also
 // separates one item's LDS tile from the next).  `st`: diagnostics stamps (AdamArgs::stamps).
-template <typename T, int VT = 64, int PB = 8, bool SC1 = false, bool VEC_ONLY = false, bool LOCAL_SC = false>
+template <typename T, int VT = 64, int PB = 8, bool SC1 = false, bool VEC_ONLY = false, bool LOCAL_SC = false,
+          bool ST = false>
 __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& item, float (*tile)[ADAM_TILE_R + 1],
                                             Scalars& sc_lds, unsigned long long* st = nullptr) {
   if (item.seg < 0) {
@@ -577,11 +580,11 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
 
   if (seg.matrix) {
     if constexpr (!VEC_ONLY) {
-      stamp(st, 1);
+      if constexpr (ST) stamp(st, 1);
       if (item.pad & ITEM_VEC4)
-        matrix_tile<T, true, PB, SC1>(a, seg, item, sc, tile, st);
+        matrix_tile<T, true, PB, SC1, ST>(a, seg, item, sc, tile, st);
       else
-        matrix_tile<T, false, PB, SC1>(a, seg, item, sc, tile, st);
+        matrix_tile<T, false, PB, SC1, ST>(a, seg, item, sc, tile, st);
     }
   } else {
     // vector chunk: ADAM_VEC (64) consecutive elements; wave w sums the partials w, w + 4,

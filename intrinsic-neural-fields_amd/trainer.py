@@ -69,21 +69,34 @@ def _summary_writer(log_dir):
 # 61.7 us per step inside a graph, 69.8 us as single-step replays), so long epochs replay
 # the largest graph and an epoch's remainder takes at most four launches, not up to 7.
 GRAPH_SIZES = (32, 8, 4, 2, 1)
+# Round 6: an epoch's full batches replay as ONE captured graph (up to MAX_GRAPH_STEPS steps;
+# longer epochs as several of those plus a GRAPH_SIZES remainder), so an epoch pays one
+# replay boundary instead of one per 32 steps (+ up to four for its remainder).
+MAX_GRAPH_STEPS = 512
 
 
 def graph_replays(n, sizes=GRAPH_SIZES):
-    """The graph sizes, in replay order, that cover n consecutive steps."""
+    """The graph sizes, in replay order, that cover n consecutive steps (sizes: descending)."""
     out = []
-    for g in sizes:
+    for g in sorted(sizes, reverse=True):
         while n >= g:
             out.append(g)
             n -= g
     return out
 
 
+def epoch_graph_sizes(full):
+    """The graph sizes an epoch of `full` full batches captures: one graph of the whole epoch
+    (at most MAX_GRAPH_STEPS steps) and the GRAPH_SIZES pieces of what is left over."""
+    if full <= 0:
+        return []
+    head = min(full, MAX_GRAPH_STEPS)
+    return sorted({head} | set(graph_replays(full % head)), reverse=True)
+
+
 class _FusedEpoch:
-    """Replays captured fused steps (graphs of GRAPH_SIZES steps) over the full batches of
-    an epoch; the batch index advances on the device.  The gather runs
+    """Replays captured fused steps over the full batches of an epoch -- one graph of the
+    whole epoch (epoch_graph_sizes); the batch index advances on the device.  The gather runs
     inside the fused chain by default; INF_PREFETCH=1 moves the next batch's gather to a
     side stream (runtime.StepPipeline: each step then reads pre-gathered feature rows),
     which measured slower on one GPU (see StepPipeline)."""
@@ -142,7 +155,7 @@ class _FusedEpoch:
                 # the captured sizes only (a pipelined capture holds GRAPH_STEPS alone); the
                 # batches they do not cover run as eager steps below
                 done = 0
-                for n in graph_replays(full, tuple(sorted(graphs, reverse=True))):
+                for n in graph_replays(full, tuple(graphs)):
                     graphs[n].replay()
                     done += n
             optim.after_fused_steps(model, rt, group, done)
@@ -175,8 +188,8 @@ class _FusedEpoch:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         full = loader.N // B
-        # only the sizes this epoch replays (an epoch of 20 batches needs no 32-step graph)
-        sizes = sorted(set(graph_replays(full))) if self.pipe is None else [self.GRAPH_STEPS]
+        # one graph of the epoch's full batches (+ the pieces of a remainder past MAX_GRAPH_STEPS)
+        sizes = epoch_graph_sizes(full) if self.pipe is None else [self.GRAPH_STEPS]
         graphs = {}
         with torch.cuda.stream(s):
             for n in sizes:
