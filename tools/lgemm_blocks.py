@@ -2,7 +2,10 @@
 register-streamed training step: entry / prologue done / main loop done / exit clocks of
 every block (inf_debug_block_times).
 
-    python tools/lgemm_blocks.py [batch]
+    python tools/lgemm_blocks.py [batch] [k]
+
+(k > 1024: config D's shape, whose dW runs the update fused in -- LGB_STEP=1 times the
+step's launch with it)
 """
 import ctypes
 import os
@@ -17,13 +20,13 @@ import torch
 from inf_hip import lib, runtime, STAGE_DW_GEMM
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-k, H, L, s = 1024, 256, 8, 4
+k, H, L, s = (int(sys.argv[2]) if len(sys.argv) > 2 else 1024), 256, 8, 4
 rng = np.random.default_rng(0)
 P = H * k + H + (L - 3) * (H * H + H) + (H * H + H + H * k + H) + 3 * H + 3
 params = torch.from_numpy((rng.standard_normal(P) * 0.03).astype(np.float32)).cuda()
 plan = runtime.Plan(k, H, L, s, "bf16", "L2", B, params, grads=torch.zeros_like(params),
                     exp_avg=torch.zeros_like(params), exp_avg_sq=torch.zeros_like(params))
-V = 50000
+V = 50000 if k <= 1024 else 20000
 E = torch.from_numpy(rng.standard_normal((V, k)).astype(np.float32)).cuda()
 src = runtime.RaySource(E, torch.from_numpy(rng.integers(0, V, (B, 3))).cuda(),
                         torch.from_numpy(rng.dirichlet([1, 1, 1], B).astype(np.float32)).cuda(),
