@@ -70,7 +70,7 @@ def _summary_writer(log_dir):
 # the largest graph and an epoch's remainder takes at most four launches, not up to 7.
 GRAPH_SIZES = (32, 8, 4, 2, 1)
 # Round 6: an epoch's full batches replay as ONE captured graph (up to MAX_GRAPH_STEPS steps;
-# longer epochs as several of those plus a GRAPH_SIZES remainder), so an epoch pays one
+# longer epochs as several of those plus one graph of the remainder), so an epoch pays one
 # replay boundary instead of one per 32 steps (+ up to four for its remainder).
 MAX_GRAPH_STEPS = 512
 
@@ -87,11 +87,12 @@ def graph_replays(n, sizes=GRAPH_SIZES):
 
 def epoch_graph_sizes(full):
     """The graph sizes an epoch of `full` full batches captures: one graph of the whole epoch
-    (at most MAX_GRAPH_STEPS steps) and the GRAPH_SIZES pieces of what is left over."""
+    (at most MAX_GRAPH_STEPS steps; a longer epoch replays that graph, then one graph of what
+    is left over)."""
     if full <= 0:
         return []
     head = min(full, MAX_GRAPH_STEPS)
-    return sorted({head} | set(graph_replays(full % head)), reverse=True)
+    return sorted({head} | ({full % head} if full % head else set()), reverse=True)
 
 
 class _FusedEpoch:

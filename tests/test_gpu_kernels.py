@@ -746,3 +746,29 @@ def test_bf16_chunked_chain3_matches_bf16_oracle(zg, monkeypatch):
     # columns, 4.9e-2, layers.4.Lx.weight 1.2e-2; seen 3.3e-2 and <= 1.7e-2 in round 5)
     for n, e in gerr.items():
         assert e < bf16_spread_bar("D", n), (n, e, bf16_spread_bar("D", n))
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("step", [1, 9, 123457])
+def test_plan_adam_matches_dense_adam_at_large_steps(mode, step):
+    """The plan's host-stepped update (inf_adam, GRAD_FLAT) and the dense Adam of the
+    parameters outside a plan arena (inf_adam_dense) form torch's bias corrections the same
+    way -- 1 - beta ** step in double with the host's pow, as torch's Python scalars are --
+    so at any step count they leave bitwise the same parameters and moments (the
+    plan's update had squared repeatedly, which can round step_neg / bc2_sqrt differently at
+    large t)."""
+    import dense
+    plan, params, w = make_plan("A", mode=mode, max_batch=256, adam=True)
+    gen = torch.Generator(device="cuda").manual_seed(step)
+    g = torch.randn(params.shape, device="cuda", generator=gen) * 1e-3
+    m = torch.randn(params.shape, device="cuda", generator=gen) * 1e-4
+    v = torch.rand(params.shape, device="cuda", generator=gen) * 1e-6
+    plan.grads.copy_(g)
+    plan.exp_avg.copy_(m)
+    plan.exp_avg_sq.copy_(v)
+    p2, m2, v2 = params.clone(), m.clone(), v.clone()
+    plan.adam(step=step, lr=1e-3)
+    dense.adam_step(p2, g.clone(), m2, v2, step, 1e-3, 0.9, 0.999, 1e-8)
+    torch.cuda.synchronize()
+    assert torch.equal(plan.exp_avg, m2) and torch.equal(plan.exp_avg_sq, v2)
+    assert torch.equal(params, p2), float((params - p2).abs().max())
