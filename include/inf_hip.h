@@ -371,9 +371,8 @@ int inf_debug_buffer(inf_plan* plan, int which, void* dst, int64_t* bytes, inf_s
 int inf_plan_last_step_fused_update(const inf_plan* plan);
 
 /* Whether the last INF_STEP_PART1 step really split the gradient: 1 = bucketed (PART2 still
- * to run), 0 = it reduced the whole gradient (not the fused chain3 path, INF_FUSED_UPDATE, or
- * a batch not a multiple of 256 x the bucket splits: PART2 is then a no-op), -1 = no PART1
- * step yet. */
+ * to run), 0 = it reduced the whole gradient (not the fused chain3 path, or a batch not a
+ * multiple of 256 x the bucket splits: PART2 is then a no-op), -1 = no PART1 step yet. */
 int inf_plan_last_part1_bucketed(const inf_plan* plan);
 
 /* ---- Sharded optimizer step (data parallel; replaces nn.DataParallel's reduce to GPU 0 +

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void update_kernel(AdamArgs a) {
   // update_item LOCAL_SC, measured 8.5 vs 8.1 us per launch: the barrier is not on the
   // critical path -- the stamps (tools/update_items.py) put it in the data: ~1.5 us of loads
   // at ~12 TB/s from the MALL, then ~2 us of stores, profiles/r06/update/)
-  adam_dev::update_item<T, 64, 8, false, false, false, ST>(a, a.items[blockIdx.x], tile, sc, st);
+  adam_dev::update_item<T, 64, 8, false, false, ST>(a, a.items[blockIdx.x], tile, sc, st);
   if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     adam_dev::stamp(st, 4);

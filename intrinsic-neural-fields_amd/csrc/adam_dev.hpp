@@ -1,6 +1,6 @@
 // Device side of the parameter update (adam.hip), shared with the weight-gradient GEMM
-// (lgemm.hip), which runs the same work items for a tile once its last split-K partial
-// has landed: one definition, bitwise-identical results either way.
+// (lgemm.hip GT), which runs the same work items on each gradient tile it has just summed:
+// one definition of the arithmetic either way.
 #pragma once
 
 #include <cmath>
@@ -272,11 +272,10 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
 // time) so each thread keeps 16-24 16-byte loads in flight.  VEC4: the tensor's rows are
 // 16-byte aligned in the flat arena (C % 4 == 0, offset % 4 == 0); otherwise the arena
 // side is accessed element-wise (slabs are always padded and aligned).
-// PB: split-K partials loaded per batch; SC1: read the partials write-through (`sc1`, the
-// in-launch hand-off of lgemm.hip: they were stored sc1 by other workgroups of the launch)
+// PB: split-K partials loaded per batch
 // ST: diagnostics stamps at st (compiled in only for the stamped launch: the asm wait would
 // otherwise constrain the schedule of the product kernel)
-template <typename T, bool VEC4, int PB, bool SC1, bool ST = false>
+template <typename T, bool VEC4, int PB, bool ST = false>
 __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& seg, const AdamItem& item,
                                             const Scalars& sc, float (*tile)[ADAM_TILE_R + 1],
                                             unsigned long long* st = nullptr) {
@@ -337,8 +336,6 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
       for (int j = 0; j < 4; ++j) g[i][j] = 0.f;
     const float* base = seg.slab + gc;
     const int ns = seg.nslab;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg.slab), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll 1
     for (int k0 = 0; k0 < ns; k0 += PB) {
       float4 t[PB][NR];
@@ -348,16 +345,7 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
           const int64_t eo = (int64_t)(item.r0 + rb + 32 * i) * seg.slab_ld;
-          if constexpr (SC1) {
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const f4v x = (ok[i] && k0 + q < ns)
-                              ? __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                            rs, (unsigned)((sk + eo - seg.slab) * 4), 0, 16))
-                              : f4v{0.f, 0.f, 0.f, 0.f};
-            t[q][i] = make_float4(x[0], x[1], x[2], x[3]);
-          } else {
-            t[q][i] = (ok[i] && k0 + q < ns) ? *reinterpret_cast<const float4*>(sk + eo) : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
+          t[q][i] = (ok[i] && k0 + q < ns) ? *reinterpret_cast<const float4*>(sk + eo) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
       // fixed order: partial 0, 1, ..., ns-1
@@ -381,76 +369,6 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
   }
   mt_apply<T, VEC4>(a, seg, item, sc, tile, ok, e, w, m, v, g);
   if constexpr (ST) stamp(st, 3);
-}
-
-// NI matrix items of one segment, software-pipelined: the next item's parameters, Adam
-// state and split-K partials (sc1: published in-launch by other workgroups, lgemm.hip)
-// are in flight while the current one is applied.  Same arithmetic in the same order as
-// matrix_tile: bitwise the same results.  Requires VEC4 rows, GRAD_SLABS and nslab <= PB.
-template <typename T, int NI, int PB>
-__device__ __forceinline__ void matrix_items_pipelined(const AdamArgs& a, const AdamSeg& seg, const AdamItem (&items)[NI],
-                                                       Scalars& sc, float (*tile)[ADAM_TILE_R + 1]) {
-  constexpr int NR = ADAM_TILE_R / 32;
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const int tid = threadIdx.x;
-  const int c4 = tid & 7, rb = tid >> 3;
-  const bool adam = a.do_adam && a.grad_src != GRAD_NONE;
-  if (a.do_adam && tid == 0) sc = step_scalars(a);
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg.slab), (short)0, 0x7FFFFFFF, 0x00020000);
-  const int ns = seg.nslab;
-  struct Regs {
-    bool ok[NR];
-    int64_t e[NR];
-    float w[NR][4], m[NR][4], v[NR][4];
-    f4v t[PB][NR];
-  } R[2];
-  auto load = [&](const AdamItem& item, Regs& r) {
-    const int gc = item.c0 + 4 * c4;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int gr = item.r0 + rb + 32 * i;
-      r.ok[i] = gr < seg.R && gc < seg.C;
-      r.e[i] = seg.off + (int64_t)(r.ok[i] ? gr : 0) * seg.C + (r.ok[i] ? gc : 0);
-      auto ld = [&](const float* base, float (&dst)[4]) {
-        const float4 x = r.ok[i] ? *reinterpret_cast<const float4*>(base + r.e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[0] = x.x, dst[1] = x.y, dst[2] = x.z, dst[3] = x.w;
-      };
-      ld(a.params, r.w[i]);
-      if (adam) {
-        ld(a.exp_avg, r.m[i]);
-        ld(a.exp_avg_sq, r.v[i]);
-      }
-#pragma unroll
-      for (int q = 0; q < PB; ++q) {
-        const int64_t eo = (int64_t)q * seg.slab_stride + (int64_t)gr * seg.slab_ld + gc;
-        r.t[q][i] = (r.ok[i] && q < ns)
-                        ? __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(eo * 4), 0, 16))
-                        : f4v{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-  load(items[0], R[0]);
-  if (a.do_adam) lds_barrier();  // sc
-#pragma unroll
-  for (int it = 0; it < NI; ++it) {
-    Regs& r = R[it & 1];
-    if (it + 1 < NI) load(items[it + 1], R[(it + 1) & 1]);
-    float g[NR][4];
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g[i][j] = 0.f;
-#pragma unroll
-    for (int q = 0; q < PB; ++q)  // fixed order: partial 0, 1, ..., ns-1
-      if (q < ns)
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) g[i][j] += r.t[q][i][j];
-    lds_barrier();  // the previous item's LDS tile reads are done
-    mt_apply<T, true>(a, seg, items[it], sc, tile, r.ok, r.e, r.w, r.m, r.v, g);
-  }
 }
 
 // NI matrix items whose reduced gradient is an LDS tile (lgemm.hip GT: the dW^T tile of a
@@ -552,14 +470,13 @@ __device__ inline void finish_step(const AdamArgs& a) {
 
 // One work item (adam.hpp AdamItem) on 256 threads: a matrix tile, a vector chunk or the
 // end-of-step item.  `tile` and `sc` are the caller's LDS.
-// VT: vector-partial loads in flight per thread; PB, SC1: matrix_tile; VEC_ONLY: the caller
+// VT: vector-partial loads in flight per thread; PB: matrix_tile; VEC_ONLY: the caller
 // runs vector / end-of-step items only: the matrix path is not compiled into it
 // LOCAL_SC: one item per workgroup (the update launch): every thread forms the step's
 // scalars itself, so no LDS hand-off and no barrier stand between the item's table loads and
 // its data loads (callers that run several items per workgroup keep the barrier, which also
 // separates one item's LDS tile from the next).  `st`: diagnostics stamps (AdamArgs::stamps).
-template <typename T, int VT = 64, int PB = 8, bool SC1 = false, bool VEC_ONLY = false, bool LOCAL_SC = false,
-          bool ST = false>
+template <typename T, int VT = 64, int PB = 8, bool VEC_ONLY = false, bool LOCAL_SC = false, bool ST = false>
 __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& item, float (*tile)[ADAM_TILE_R + 1],
                                             Scalars& sc_lds, unsigned long long* st = nullptr) {
   if (item.seg < 0) {
@@ -582,9 +499,9 @@ __device__ __forceinline__ void update_item(const AdamArgs& a, const AdamItem& i
     if constexpr (!VEC_ONLY) {
       if constexpr (ST) stamp(st, 1);
       if (item.pad & ITEM_VEC4)
-        matrix_tile<T, true, PB, SC1, ST>(a, seg, item, sc, tile, st);
+        matrix_tile<T, true, PB, ST>(a, seg, item, sc, tile, st);
       else
-        matrix_tile<T, false, PB, SC1, ST>(a, seg, item, sc, tile, st);
+        matrix_tile<T, false, PB, ST>(a, seg, item, sc, tile, st);
     }
   } else {
     // vector chunk: ADAM_VEC (64) consecutive elements; wave w sums the partials w, w + 4,

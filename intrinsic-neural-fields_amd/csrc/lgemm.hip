@@ -90,7 +90,7 @@ __device__ __forceinline__ void lg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\
 template <int BM, bool FUSED, bool SPLIT = false, int BN = LG_BN, bool GT = false, int KS = 1>
 __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch) {
   static_assert(!(FUSED && SPLIT), "split operands: plain slab epilogue only");
-  static_assert(!GT || FUSED, "the gradient-tile update is a fused mode");
+  static_assert(GT == FUSED, "the fused update runs on gradient tiles only (LgemmBatch::fused == 2)");
   static_assert(KS == 1 || (!FUSED && !GT), "k-split groups: the plain slab / C epilogues only");
   constexpr int NP = SPLIT ? 2 : 1;
   using C = LG<BM, NP, BN, GT, KS>;
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
     if ((int)blockIdx.x < batch.n_aux) {
       // (the update kernel's vector sum order: partial w, w + 4, ... per wave)
       if ((int)blockIdx.x < batch.n_aux_items)
-        adam_dev::update_item<bf16, 16, 4, false>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
+        adam_dev::update_item<bf16, 16, 4>(batch.adam, batch.aux_items[blockIdx.x], atile, asc);
       return;
     }
   }
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
 
   if (P.slab != nullptr) {
     // dW^T tile -> slab [n][m]: four consecutive m per 16-byte store, write-through (sc1):
-    // read by the update launch (or another workgroup of this one: fused update)
+    // read by the update launch
     float* dst = P.slab + (int64_t)split * P.slab_stride;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
     constexpr int MQ = BM / 4;
@@ -329,66 +329,10 @@ __global__ __launch_bounds__(256 * KS) void lgemm_kernel(const LgemmBatch batch)
       const f32x4 v = {Cs[(mq * 4 + 0) * CLD + cs], Cs[(mq * 4 + 1) * CLD + cs], Cs[(mq * 4 + 2) * CLD + cs],
                        Cs[(mq * 4 + 3) * CLD + cs]};
       const int64_t eo = (int64_t)(n0 + col) * P.slab_ld + m0 + mq * 4;
-      if (FUSED || LG_SLAB_SC1)
+      if (LG_SLAB_SC1)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (unsigned)(eo * 4), 0, 16);
       else
         *reinterpret_cast<f32x4*>(dst + eo) = v;
-    }
-    if (FUSED) {
-      // publish this partial (sc1 stores drained by every wave, then a relaxed agent-scope
-      // ticket: cdna_hip_programming.md split-K recipe).  Every split block then takes one
-      // of the tile's NI update items: it waits (bounded) for the tile's last partial and
-      // claims item `split`; the last arriver claims and runs whatever is left (all of
-      // them if the waiters gave up), so no block ever waits for an item -- nothing can
-      // deadlock however the blocks are placed.  Items read the partials with sc1 loads
-      // and run the update kernel's own arithmetic (bitwise the same results).
-      // Counters never reset: per tile [0] arrivals (S per launch, so ticket / S is this
-      // launch's epoch e), [1 + i] the last epoch + 1 that claimed item i (atomic max).
-      constexpr int NI = (BN / ADAM_TILE_R) * (BM / ADAM_TILE_C);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      int* flag = reinterpret_cast<int*>(smem + C::LDS - 16);
-      int* ctr = batch.counters + (size_t)(P.ctr0 + tm * P.tiles_n + tn) * 8;
-      auto ld_rlx = [](int* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-      if (tid == 0) flag[0] = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (stl != nullptr) stl[4] = wall_clock64();
-      __syncthreads();
-      const int ticket = flag[0];
-      const int epoch = ticket / P.splits, target = (epoch + 1) * P.splits;
-      const bool last = ticket == target - 1;
-      auto claim = [&](int it) {
-        return __hip_atomic_fetch_max(ctr + 1 + it, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch + 1;
-      };
-      const AdamSeg seg = batch.adam.segs[P.adam_seg];  // into registers once
-      auto run_item = [&](int it) {
-        const AdamItem item[1] = {AdamItem{P.adam_seg, n0 + (it / (BM / ADAM_TILE_C)) * ADAM_TILE_R,
-                                           m0 + (it % (BM / ADAM_TILE_C)) * ADAM_TILE_C, P.adam_vec4}};
-        __syncthreads();
-        if (stl != nullptr) stl[6] = wall_clock64();
-        adam_dev::matrix_items_pipelined<bf16, 1, 4>(batch.adam, seg, item, asc, atile);
-        if (stl != nullptr) stl[7] = wall_clock64();
-      };
-      __syncthreads();
-      if (tid == 0) {
-        int won = 0;  // bit i: item i is this block's
-        if (last) {
-          // claim every item still open (those of waiters that gave up, or came late)
-          for (int it = 0; it < NI; ++it)
-            if (claim(it)) won |= 1 << it;
-        } else if (split < NI) {
-          const unsigned long long t0 = wall_clock64();
-          while (ld_rlx(ctr) < target && wall_clock64() - t0 < 20000ull)  // bounded: <= 200 us
-            __builtin_amdgcn_s_sleep(2);
-          if (ld_rlx(ctr) >= target && claim(split)) won = 1 << split;
-        }
-        flag[1] = won;
-      }
-      __syncthreads();
-      if (stl != nullptr) stl[5] = wall_clock64();
-      const int won = flag[1];
-#pragma unroll 1
-      for (int it = 0; it < NI; ++it)
-        if (won & (1 << it)) run_item(it);
     }
     if (stl != nullptr) stl[3] = wall_clock64();
     return;
@@ -478,14 +422,10 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
     INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: the vector items reduce their slabs");
     return launch_typed<64, true, false, 64, true>(b, stream);
   }
-  if (b.fused) {
-    INF_CHECK_ARG(b.n_aux % 8 == 0 && b.n_aux_items <= b.n_aux && b.counters != nullptr, "lgemm: fused update layout");
-    for (int i = 0; i < b.nprob; ++i)
-      INF_CHECK_ARG(b.p[i].slab != nullptr && b.p[i].adam_seg >= 0 && b.p[i].adam_vec4 && b.p[i].splits <= 4,
-                    "lgemm: fused update needs split-K slabs (at most 4), 16-byte rows");
-    INF_CHECK_ARG(b.adam.grad_src == GRAD_SLABS, "lgemm: fused update reduces the slabs");
-  }
-  INF_CHECK_ARG(!(b.fused && b.split), "lgemm: split operands with the fused update");
+  // (the update inside the split-K slab launch -- each tile's last arriving block applying
+  // Adam to the summed partials -- was bitwise the separate launch but slower: +3 us at
+  // config B, 140 vs 124 us at config D; removed in round 6)
+  INF_CHECK_ARG(b.fused == 0, "lgemm: the fused update runs on gradient tiles only (fused == 2)");
   // the slab / C paths: two k groups per block where every block's K range splits into an
   // even number of 64-deep stages, each a multiple of RA (the default): the split-operand
   // (bf16x3) dW 122.3 -> 120.9 us per step, the bf16 step 64.1 -> 63.5 us (dW 14.8 -> 14.4,
@@ -495,13 +435,12 @@ int launch_lgemm(LgemmBatch& b, int bm, hipStream_t stream) {
   // INF_LGEMM_KS=1 / 2 forces one or two.
   const char* eks = std::getenv("INF_LGEMM_KS");
   const int want_ks = eks != nullptr ? std::atoi(eks) : 2;
-  bool ks2 = bm == 64 && !b.fused && want_ks == 2;
+  bool ks2 = bm == 64 && want_ks == 2;
   for (int i = 0; i < b.nprob && ks2; ++i) ks2 = (b.p[i].K / b.p[i].splits) % (64 * 2 * LG_RA2) == 0;
   if (b.split) {
     if (ks2) return launch_typed<64, false, true, LG_BN, false, 2>(b, stream);
     return bm == 64 ? launch_typed<64, false, true>(b, stream) : launch_typed<32, false, true>(b, stream);
   }
-  if (b.fused) return bm == 64 ? launch_typed<64, true>(b, stream) : launch_typed<32, true>(b, stream);
   if (ks2) return launch_typed<64, false, false, LG_BN, false, 2>(b, stream);
   return bm == 64 ? launch_typed<64, false>(b, stream) : launch_typed<32, false>(b, stream);
 }

@@ -45,9 +45,8 @@ struct LgemmProblem {
   float* slab;
   int64_t slab_ld, slab_stride;
   int32_t tiles_m, tiles_n, block_begin;
-  // fused update (LgemmBatch::fused): the weight's AdamSeg index, its ITEM_VEC4 flag, and
-  // the first of its per-tile arrival counters
-  int32_t adam_seg, adam_vec4, ctr0;
+  // fused update (LgemmBatch::fused): the weight's AdamSeg index and its ITEM_VEC4 flag
+  int32_t adam_seg, adam_vec4;
 };
 
 struct LgemmBatch {
@@ -55,16 +54,13 @@ struct LgemmBatch {
   int32_t nprob;
   int32_t total_blocks;
   unsigned long long* stamps;  // diagnostics (inf_debug_block_times) or null
-  // Fused parameter update (adam.hip work items, same code): the last split-K block to
-  // finish a tile runs the matrix items of that tile on the summed partials; the first
-  // n_aux blocks of the grid (a multiple of 8; n_aux_items of them busy) run the vector
-  // and end-of-step items.  counters: one int per tile, zero between launches.
-  // fused == 2 ("gradient tile"): split-K 1 with 64 x 64 tiles, each block runs its own
-  // tile's items on the gradient in LDS (no slab, no counters).
+  // Fused parameter update (adam.hip work items, same code), fused == 2 ("gradient tile";
+  // 0 = none): split-K 1 with 64 x 64 tiles, each block runs its own tile's items on the
+  // gradient in LDS (no slab, no update launch); the first n_aux blocks of the grid (a
+  // multiple of 8; n_aux_items of them busy) run the vector and end-of-step items.
   int32_t fused;
   int32_t n_aux, n_aux_items;
   const AdamItem* aux_items;
-  int32_t* counters;
   AdamArgs adam;
   // split-bf16 operands (hi + lo images, three MFMAs per k block: the bf16x3 mode's dW)
   int32_t split;

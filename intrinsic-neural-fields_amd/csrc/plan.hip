@@ -92,7 +92,7 @@ struct inf_plan {
   int64_t o_xp[2] = {-1, -1};  // pre-gather slots (bf16 [bp_max][k_pad], inf_prefetch_batch)
   int64_t o_zin = -1;          // input-layer pre-activations ahead of chain3 (zg.hip), fp32 [parts][bp_max][2H]
   int zin_parts_max = 0;       // k slices o_zin holds
-  int64_t o_aux_items = 0, o_counters = 0;  // fused update in the dW GEMM (lgemm.hpp)
+  int64_t o_aux_items = 0;  // fused update in the dW GEMM (lgemm.hpp): its vector items
   // the matrix items alone (the update launch after a dW GEMM that ran the vector items)
   // sharded update (data parallel, inf_plan_shard): the item-major staging layout of
   // `shard_world` ranks, this rank's items (+ the end-of-step item) as their own table
@@ -344,10 +344,6 @@ int build_layout(inf_plan* p) {
   p->o_tables_b = take(align_up((int64_t)p->segs.size() * sizeof(AdamSeg)));
   p->o_aux_items = take(align_up((nitems + 8) * sizeof(AdamItem)));
   p->o_shard_items = take(align_up((nitems + 1) * sizeof(AdamItem)));
-  int64_t max_tiles = 0;  // lgemm tiles at its smallest block (32 rows x 128 columns)
-  for (const auto& g : p->segs)
-    if (g.gemm) max_tiles += ceil_div(g.c_pad, 32) * ceil_div(g.R, 128);
-  p->o_counters = take(align_up(max_tiles * 8 * 4));  // 8 ints per tile (lgemm.hip fused update)
   p->o_ws_end = w;
   return INF_OK;
 }
@@ -607,7 +603,6 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     const bool gt = fuse != nullptr && p->lgf && splits == 1 && bucket == 0;
     LgemmBatch lb;
     std::memset(&lb, 0, sizeof(lb));
-    int ctr = 0;
     for (size_t i = 0; i < p->segs.size(); ++i) {
       const ParamSeg& g = p->segs[i];
       if (!g.gemm) continue;
@@ -616,8 +611,6 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
       LgemmProblem& q = lb.p[lb.nprob++];
       q.adam_seg = (int32_t)i;
       q.adam_vec4 = (g.C % 4 == 0 && g.off % 4 == 0) ? ITEM_VEC4 : 0;
-      q.ctr0 = ctr;
-      ctr += (g.c_pad / 64) * (g.R / LG_BN);
       const int l = g.layer;
       const bool from_input = (l == 0) || (l == s && g.sub == 1);
       // layer inputs as the chain wrote them: X^T / Y_{l-1}^T fragment images
@@ -636,12 +629,12 @@ int run_weight_grads(inf_plan* p, int Bp, hipStream_t st, int chain, const AdamA
     }
     lb.stamps = p->lg_stamps;
     if (fuse != nullptr) {
-      lb.fused = gt ? 2 : 1;
+      INF_CHECK_ARG(gt, "lgemm: the update fuses into split-K-1 gradient tiles only");
+      lb.fused = 2;
       lb.adam = *fuse;
       lb.n_aux_items = p->n_aux_items;
       lb.n_aux = (int)round_up(p->n_aux_items, 8);
       lb.aux_items = reinterpret_cast<const AdamItem*>(p->ws + p->o_aux_items);
-      lb.counters = p->W<int32_t>(p->o_counters);
     }
     // (128 x 128 tiles measured slower at 2 and 4 splits: step 75.3 / 71.6 vs 68.1-69.9 us,
     // profiles/r04/lgemm_tile_split_sweep.log; so were 4 splits of 64 x 128: 70.5-70.9)
@@ -997,16 +990,6 @@ bool use_chain3(const inf_plan* p, const inf_batch* b, int Bp) {
 // layer as Lx over the activation tile then Ly over X), then the dX layers L-2..1.
 // k_pad > C3_KC (config D): X is streamed in C3_KC-column chunks and phase 0 runs W_y then
 // W_0 over each chunk (W_y x kept in the second accumulator set until the skip layer).
-// INF_FUSED_UPDATE=1 (the update inside a split-K dW launch) where that launch supports
-// it: every weight's rows 16-byte aligned (not config R's k = 1023), at most 4 splits --
-// otherwise the separate update launch, as by default
-static bool fused_update_requested(const inf_plan* p) {
-  if (std::getenv("INF_FUSED_UPDATE") == nullptr) return false;
-  if (p->dw_splits > 4) return false;
-  for (const auto& g : p->segs)
-    if (g.gemm && (g.C % 4 != 0 || g.off % 4 != 0)) return false;
-  return true;
-}
 
 // The input layers on zg.hip ahead of the chain: the default for the chunked-tile tables
 // (k_pad > C3_KC, config D: gather + input GEMM 26.5 us + the hidden-layer chain 31.9 us
@@ -1600,7 +1583,6 @@ int inf_plan_bind(inf_plan* p, float* params, float* grads, float* exp_avg, floa
     INF_HIP_TRY(hipMemcpy(p->ws + p->o_tables_b, tb.data(), tb.size() * sizeof(AdamSeg), hipMemcpyHostToDevice));
   }
   if (int rc = upload_item_subsets(p)) return rc;
-  INF_HIP_TRY(hipMemset(p->ws + p->o_counters, 0, (size_t)(p->o_ws_end - p->o_counters)));
   // padded shadow columns/rows must read as zero
   INF_HIP_TRY(hipMemset(p->shadow, 0, p->shadow_bytes));
   p->bound = true;
@@ -1666,10 +1648,9 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
                            INF_STEP_PART2 | INF_STEP_SHARD)) == 0,
                 "train_step: unknown flags");
   const bool shard = (flags & INF_STEP_SHARD) != 0;
-  INF_CHECK_ARG(!shard || ((flags & (INF_STEP_ADAM | INF_STEP_PART1 | INF_STEP_PART2)) == 0 && p->sh_gsh != nullptr &&
-                           (p->lgf || std::getenv("INF_FUSED_UPDATE") == nullptr)),
+  INF_CHECK_ARG(!shard || ((flags & (INF_STEP_ADAM | INF_STEP_PART1 | INF_STEP_PART2)) == 0 && p->sh_gsh != nullptr),
                 "train_step: INF_STEP_SHARD is a gradient-only step of a plan with bound shard buffers "
-                "(not with ADAM / PART1 / PART2 / INF_FUSED_UPDATE)");
+                "(not with ADAM / PART1 / PART2)");
   if (flags & INF_STEP_ADAM) {
     if (int rc = check_unsharded(p, "train_step with Adam")) return rc;
   }
@@ -1697,8 +1678,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
   // [grad_split, P): the matrices and biases from the skip layer's Ly on, plus the step's
   // loss sums -- into `grads`; PART2 = the same for bucket 2, the arena [0, grad_split)
   // (the earlier layers' biases included).  The caller all-reduces bucket 1 while PART2 runs.
-  const bool bucketed = part != 0 && use_chain3(p, batch, Bp3) && Bp3 % (256 * p->bucket_splits) == 0 &&
-                        std::getenv("INF_FUSED_UPDATE") == nullptr;
+  const bool bucketed = part != 0 && use_chain3(p, batch, Bp3) && Bp3 % (256 * p->bucket_splits) == 0;
   if (part == 1) p->last_part1 = bucketed ? 1 : 0;
   if (shard && !use_chain3(p, batch, Bp3) && !use_chainf(p, batch, Bp3) && !use_chain3x3(p, batch, Bp3)) {
     // the other paths read the row-major shadows, rewritten from the fp32 masters, which a
@@ -1739,10 +1719,7 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     return a;
   };
   if (use_chain3(p, batch, Bp3)) {
-    // fused gather + chain -> dW GEMM (-> update below).  INF_FUSED_UPDATE=1: the update
-    // runs inside the dW launch instead (each tile's last split-K block applies Adam to
-    // it, the first blocks do the biases and the end-of-step sums; bitwise the same) --
-    // slower today: the last arriver's four items run back to back
+    // fused gather + chain -> dW GEMM (-> update below, or inside the dW launch: lgf)
     const int Bp = Bp3;
     const bf16* xpre = nullptr;
     if (xslot >= 0) {
@@ -1757,9 +1734,8 @@ int inf_train_step(inf_plan* p, const inf_batch* batch, float* pred, int flags, 
     nloss = Bp / chain3_bm(Bp);
     p->stepped = true;
     p->last_lgf = false;
-    if (!bucketed && (p->lgf || fused_update_requested(p))) {
-      // the update inside the dW launch: lgf (default, split-K 1: each block its own tile
-      // from LDS) or INF_FUSED_UPDATE (split-K slabs, the last arriving block of a tile)
+    if (!bucketed && p->lgf) {
+      // the update inside the dW launch (split-K 1: each block its own tile from LDS)
       p->last_chain = 3;
       p->last_lgf = p->lgf;
       if ((rc = refresh_tables(p, Bp, st, 3))) return rc;
@@ -1939,10 +1915,7 @@ int inf_plan_can_shard(inf_plan* p, const inf_batch* batch) {
     return 0;
   int Bp3 = 0;
   if (pad_batch(p, batch->batch, true, &Bp3) != INF_OK) return 0;
-  return (use_chain3(p, batch, Bp3) || use_chainf(p, batch, Bp3) || use_chain3x3(p, batch, Bp3)) &&
-                 std::getenv("INF_FUSED_UPDATE") == nullptr
-             ? 1
-             : 0;
+  return use_chain3(p, batch, Bp3) || use_chainf(p, batch, Bp3) || use_chain3x3(p, batch, Bp3) ? 1 : 0;
 }
 
 int inf_plan_bind_shard(inf_plan* p, float* grad_staging, float* grad_chunk, void* weight_staging) {

@@ -488,44 +488,6 @@ def test_bf16_chain_render_matches_layered(monkeypatch):
         np.testing.assert_allclose(imgs[tag].reshape(H, W, 3), d["img_full"], atol=2e-2)
 
 
-@pytest.mark.parametrize("apply_adam", [True, False])
-def test_fused_update_bitwise(apply_adam, monkeypatch):
-    """The split-K slab path (the default): the update fused into the dW GEMM launch
-    (INF_FUSED_UPDATE: the last split-K block of each tile runs the update kernel's own
-    matrix items on the sc1-published partials) leaves exactly the bytes of the separate
-    update launch: parameters, Adam state (or the reduced gradients) and the step's loss
-    sums, over three steps of 4096 rays.  (The fused launch keeps one k group per block, so
-    the separate path runs the same GEMM here: INF_LGEMM_KS=1.)"""
-    monkeypatch.setenv("INF_LGF", "0")
-    monkeypatch.setenv("INF_LGEMM_KS", "1")
-    rng = np.random.default_rng(5)
-    k, H, L, s = CFG["B"]
-    V, B = 3000, 4096
-    E = rng.standard_normal((V, k)).astype(np.float32)
-    E /= (E.max(0) - E.min(0))
-    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(rng.integers(0, V, (B, 3))).cuda(),
-                         torch.from_numpy(rng.dirichlet([1, 1, 1], B).astype(np.float32)).cuda(),
-                         torch.from_numpy(rng.random((B, 3)).astype(np.float32)).cuda())
-    out = {}
-    for tag in ("separate", "fused"):
-        if tag == "fused":
-            monkeypatch.setenv("INF_FUSED_UPDATE", "1")
-        plan, params, w = make_plan("B", mode="bf16", max_batch=B, adam=True)
-        plan.set_lr(1e-3)
-        b = plan.make_batch(source=src, batch=B)
-        sums = []
-        for _ in range(3):
-            plan.train_step(b, None, apply_adam=apply_adam)
-            c = plan.read_ctrl()
-            sums.append((c["loss_sum"], c["sse_sum"]))
-        torch.cuda.synchronize()
-        out[tag] = (params.cpu().numpy().copy(), plan.grads.cpu().numpy().copy(), plan.exp_avg.cpu().numpy().copy(),
-                    plan.exp_avg_sq.cpu().numpy().copy(), sums)
-    for a_, b_ in zip(out["separate"][:4], out["fused"][:4]):
-        assert np.array_equal(a_, b_)
-    assert out["separate"][4] == out["fused"][4]
-
-
 @pytest.mark.parametrize("name,B", [("B", 4096), ("B", 1024), ("R", 2048), ("A", 4096)])
 def test_lgemm_k_groups_match_one_group(name, B, monkeypatch):
     """The dW GEMM's two k groups per block (lgemm.hip KS = 2, the default since round 5)

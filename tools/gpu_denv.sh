@@ -1,6 +1,6 @@
 #!/bin/bash
 # config-D bench section under environment variants, alternated twice:
-#   bash tools/gpu_denv.sh "" "INF_LGF=0" "INF_LGF=0 INF_FUSED_UPDATE=1" ...
+#   bash tools/gpu_denv.sh "" "INF_LGF=0" ...
 set -o pipefail
 for rep in 1 2; do
 for v in "$@"; do
