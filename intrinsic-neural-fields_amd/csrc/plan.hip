@@ -125,6 +125,9 @@ struct inf_plan {
   bool bound = false;
 
   std::vector<AdamSeg> adam_segs;
+  // the bucketed steps' seg table as last uploaded: kept alive with the plan, since an upload
+  // made inside a stream capture becomes a graph node that reads its host source at replay
+  std::vector<AdamSeg> adam_segs_b;
   std::vector<AdamItem> adam_items;
   double beta1 = 0.9, beta2 = 0.999, eps = 1e-8;  // torch holds them as Python doubles
 
@@ -784,12 +787,18 @@ int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
     }
   }
   if (!changed) return INF_OK;
-  // Pageable-source async copies are staged by the runtime before returning, so the
-  // host vector may change afterwards.
+  // Outside a capture, pageable-source async copies are staged by the runtime before
+  // returning; inside one they become graph nodes that read the host source at every replay,
+  // so the sources are the plan's own vectors, updated in place (same storage).
   INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
                              hipMemcpyHostToDevice, st));
-  const std::vector<AdamSeg> tb = bucket_segs(p);
-  INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables_b, tb.data(), tb.size() * sizeof(AdamSeg), hipMemcpyHostToDevice, st));
+  {
+    const std::vector<AdamSeg> tb = bucket_segs(p);
+    if (p->adam_segs_b.size() != tb.size()) p->adam_segs_b.resize(tb.size());
+    std::copy(tb.begin(), tb.end(), p->adam_segs_b.begin());
+  }
+  INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables_b, p->adam_segs_b.data(), p->adam_segs_b.size() * sizeof(AdamSeg),
+                             hipMemcpyHostToDevice, st));
   return INF_OK;
 }
 
