@@ -125,8 +125,8 @@ struct inf_plan {
   bool bound = false;
 
   std::vector<AdamSeg> adam_segs;
-  // the bucketed steps' seg table as last uploaded: kept alive with the plan, since an upload
-  // made inside a stream capture becomes a graph node that reads its host source at replay
+  // the bucketed steps' seg table as last uploaded: kept alive with the plan (an upload made
+  // inside a stream capture is a graph node that may read its host source at replay)
   std::vector<AdamSeg> adam_segs_b;
   std::vector<AdamItem> adam_items;
   double beta1 = 0.9, beta2 = 0.999, eps = 1e-8;  // torch holds them as Python doubles
@@ -788,8 +788,9 @@ int refresh_tables(inf_plan* p, int Bp, hipStream_t st, int chain = 0) {
   }
   if (!changed) return INF_OK;
   // Outside a capture, pageable-source async copies are staged by the runtime before
-  // returning; inside one they become graph nodes that read the host source at every replay,
-  // so the sources are the plan's own vectors, updated in place (same storage).
+  // returning; inside one (a plan whose first step is captured) the copy is a graph node, and
+  // a replay measured as if it re-read its source, so the sources are
+  // the plan's own vectors, updated in place (same storage).
   INF_HIP_TRY(hipMemcpyAsync(p->ws + p->o_tables, p->adam_segs.data(), p->adam_segs.size() * sizeof(AdamSeg),
                              hipMemcpyHostToDevice, st));
   {
