@@ -650,6 +650,42 @@ def test_bf16_chain3_matches_bf16_oracle(name, B, monkeypatch):
         assert e < BF16_ORACLE_GRAD, (n, e)
 
 
+@pytest.mark.parametrize("name,B", [("B", 4000), ("B", 1000), ("A", 100), ("R", 2047), ("B", 9000)])
+def test_bf16_ragged_batches_match_bf16_oracle(name, B):
+    """Ragged batches (not a multiple of the chain's 16- / 64-ray tiles or of its dW split):
+    the padded rays of the last tile must add nothing -- to the loss, the gradients or the
+    bias partials -- so the bf16 step on B rays meets the bf16 oracle on exactly those B rays
+    with the bars of the whole-tile test above (the same arithmetic; the padding only changes
+    which partial sums are zero)."""
+    rng = np.random.default_rng(79)
+    k, H, L, s = CFG[name]
+    w0 = weights(golden(f"g2_forward_{name}.npz"))
+    V = 3000
+    E = rng.standard_normal((V, k)).astype(np.float32)
+    E /= (E.max(0) - E.min(0))
+    vids = rng.integers(0, V, (B, 3))
+    bary = rng.dirichlet([1, 1, 1], B).astype(np.float32)
+    rgb = rng.random((B, 3)).astype(np.float32)
+    src = rt().RaySource(torch.from_numpy(E).cuda(), torch.from_numpy(vids).cuda(), torch.from_numpy(bary).cuda(),
+                         torch.from_numpy(rgb).cuda())
+    plan, params, w = make_plan(name, mode="bf16", max_batch=B, adam=True)
+    pred = torch.empty((B, 3), device="cuda")
+    plan.train_step(plan.make_batch(source=src, batch=B), pred, apply_adam=False)
+    c = plan.read_ctrl()
+    p = pred.cpu().numpy()
+    g = arena_to_dict(plan.grads, w, L, s)
+    p_ref, cache = O.mlp_forward_bf16(w0, O.gather_bf16(E, vids, bary), L, s)
+    g_ref = O.mlp_backward_bf16(w0, cache, O.loss_grad(p_ref, rgb, "L2"), L, s)
+    perr = float(np.abs(p - p_ref).max())
+    lerr = abs(c["loss_sum"] / (3 * B) - O.loss_value(p_ref, rgb, "L2"))
+    gerr = {n: float(np.abs(g[n] - g_ref[n]).max() / max(np.abs(g_ref[n]).max(), 1e-12)) for n in O.layer_names(L, s)}
+    print(name, B, plan.last_step_path(), "pred", perr, "loss", lerr, {n: round(e, 5) for n, e in gerr.items()})
+    assert perr < BF16_ORACLE_RGB, perr
+    assert lerr < 1e-5, lerr
+    for n, e in gerr.items():
+        assert e < BF16_ORACLE_GRAD, (n, e)
+
+
 # bars of test_bf16_chain3_matches_bf16_oracle: seen RGB <= 1.7e-4 and gradients <= 1.3e-2 of
 # each tensor's max (B at 1024 / 4096 rays, A, R; profiles/r02/bf16_oracle_parity.log) --
 # against the fp32 oracle the same path needs 2e-2 / 0.25 (test_bf16_chain_matches_layered_and_oracle)
