@@ -50,6 +50,14 @@ __device__ __forceinline__ Scalars step_scalars(const AdamArgs& a) {
   return s;
 }
 
+// Four consecutive floats at a dword-aligned (not necessarily 16-byte-aligned) address as one
+// 16-byte access: the rows of an arena tensor whose column count is not a multiple of 4
+// (config R's k = 1023) start at every dword offset.  Bitwise the element-wise accesses.
+__device__ __forceinline__ void load4_unaligned(const float* p, float (&dst)[4]) {
+  __builtin_memcpy(dst, p, 16);
+}
+__device__ __forceinline__ void store4_unaligned(float* p, const float (&src)[4]) { __builtin_memcpy(p, src, 16); }
+
 __device__ __forceinline__ void stamp(unsigned long long* st, int i) {
   if (st != nullptr && threadIdx.x == 0) st[i] = wall_clock64();
 }
@@ -96,6 +104,10 @@ __device__ __forceinline__ void mt_apply(const AdamArgs& a, const AdamSeg& seg, 
     if (!ok[i]) return;
     if (VEC4) {
       *reinterpret_cast<float4*>(base + e[i]) = make_float4(src[0], src[1], src[2], src[3]);
+    } else if (gc + 3 < seg.C) {
+      // a whole 4-column group of a row that is not 16-byte aligned in the arena (config R's
+      // k = 1023): one dword-aligned 16-byte store (global dwordx4 needs dword alignment only)
+      store4_unaligned(base + e[i], src);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -291,6 +303,8 @@ __device__ __forceinline__ void matrix_tile(const AdamArgs& a, const AdamSeg& se
     if (VEC4) {
       const float4 t = ok[i] ? *reinterpret_cast<const float4*>(base + e[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
       dst[0] = t.x, dst[1] = t.y, dst[2] = t.z, dst[3] = t.w;
+    } else if (ok[i] && gc + 3 < seg.C) {
+      load4_unaligned(base + e[i], dst);  // (see st4 in mt_apply)
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) dst[j] = (ok[i] && gc + j < seg.C) ? base[e[i] + j] : 0.f;
