@@ -50,7 +50,8 @@ def rays(k, V, N, seed, clear=None):
                                               ("R", 256, "L1", "fp32"), ("R", 2048, "L2", "fp32"),
                                               ("B", 1024, "L2", "fp32"), ("B", 4096, "L2", "fp32"),
                                               ("B", 1000, "L1", "fp32"), ("B", 4096, "L2", "bf16x3"),
-                                              ("R", 2048, "L1", "bf16x3")])
+                                              ("R", 2048, "L1", "bf16x3"), ("B", 1000, "L1", "bf16x3"),
+                                              ("A", 1000, "cauchy", "bf16x3")])
 def test_chainf_matches_oracle_and_layered(name, B, loss, mode, monkeypatch):
     """Both parity modes take their fused chain: fp32 (chainf, exact f32) and bf16x3 (chain3
     X3 on split bf16 products; its layered path runs the forward on 6 products, the dX on 3)."""
